@@ -1,0 +1,31 @@
+"""voxnav -- MI355X-native batched voxel-grid exploration env.
+
+The data-parallel hot path of Noimps/3D-Navigation-Reinforcement-Learning
+(envs/CubicEnv.py step/reset batched as train/Grid_Train.py batches it),
+rebuilt as hand-written HIP kernels for gfx950 behind the C-ABI in
+include/voxnav.h.  Public API:
+
+  rooms.*             room-file parser / room sets / synthetic boxes
+  BatchedGridEnv      N agents per GPU, torch tensors in/out, SB3 auto-reset
+  GridAgent           the reference's single-env gymnasium API
+  compute_gae         GAE advantage/return scan kernel
+  sharding            multi-GPU agent sharding helpers
+"""
+from . import rooms  # noqa: F401
+from ._native import VoxnavError, load as load_library  # noqa: F401
+
+__all__ = ["rooms", "BatchedGridEnv", "GridAgent", "compute_gae", "VoxnavError", "load_library"]
+
+
+def __getattr__(name):
+    # torch-dependent pieces are imported lazily
+    if name == "BatchedGridEnv":
+        from .env import BatchedGridEnv
+        return BatchedGridEnv
+    if name == "GridAgent":
+        from .gym_api import GridAgent
+        return GridAgent
+    if name == "compute_gae":
+        from .gae import compute_gae
+        return compute_gae
+    raise AttributeError(name)

@@ -1,0 +1,60 @@
+"""Compile libvoxnav.so (HIP, gfx950) in-tree.
+
+The library is the drop-in boundary (include/voxnav.h).  It is built with
+plain ``hipcc`` so the product has no build-system dependency; the .so lands
+in ``voxnav/_lib/`` and travels with the repo snapshot to the GPU box.
+"""
+from __future__ import annotations
+
+import os
+import shutil
+import subprocess
+from pathlib import Path
+
+PKG = Path(__file__).resolve().parent
+PROJECT = PKG.parent
+REPO = PROJECT.parent
+CSRC = PROJECT / "csrc"
+INCLUDE = REPO / "include"
+LIBDIR = PKG / "_lib"
+LIB = LIBDIR / "libvoxnav.so"
+SOURCES = [CSRC / "voxnav_env.hip"]
+HEADERS = [INCLUDE / "voxnav.h"]
+ARCH = os.environ.get("VOXNAV_ARCH", "gfx950")
+
+# -ffp-contract=off: the reward (f64) and obs quotients must follow the
+# reference's operation order without fused multiply-adds.
+HIPCC_FLAGS = ["-O3", "-std=c++17", "-ffp-contract=off", "-fPIC", "-shared", f"--offload-arch={ARCH}"]
+
+
+def hipcc() -> str:
+    for cand in (os.environ.get("HIPCC"), shutil.which("hipcc"), "/opt/rocm/bin/hipcc"):
+        if cand and Path(cand).exists():
+            return cand
+    raise RuntimeError("hipcc not found (set HIPCC or install ROCm)")
+
+
+def needs_build() -> bool:
+    if not LIB.exists():
+        return True
+    t = LIB.stat().st_mtime
+    return any(p.stat().st_mtime > t for p in SOURCES + HEADERS + [Path(__file__)])
+
+
+def build(force: bool = False, verbose: bool = False) -> Path:
+    if not force and not needs_build():
+        return LIB
+    LIBDIR.mkdir(parents=True, exist_ok=True)
+    tmp = LIB.with_suffix(".so.tmp")
+    cmd = [hipcc(), *HIPCC_FLAGS, "-I", str(INCLUDE), *map(str, SOURCES), "-o", str(tmp)]
+    if verbose:
+        print(" ".join(cmd))
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"hipcc failed ({r.returncode}):\n{r.stdout}\n{r.stderr}")
+    os.replace(tmp, LIB)
+    return LIB
+
+
+if __name__ == "__main__":
+    print(build(force=True, verbose=True))

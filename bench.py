@@ -1,0 +1,187 @@
+#!/usr/bin/env python3
+"""Headline benchmark: env-steps/s of the batched CubicEnv step on MI355X.
+
+Metric (BASELINE.json): "env-steps/sec at 65536 parallel agents, 32x32x8
+room, 1/2/4/8 MI355X".  Workload (SURVEY.md 8(d), config C3 shape): per GPU
+65,536 agents in a 32x32x8 walled-box room file (reference room grammar,
+random.choice over the one-room set), local_map_length L=10
+(train/Grid_Train.py:36), crash penalty -2.0, uniform random policy
+(Philox4x32-10, seed 42), SB3 auto-reset with the pinned seed schedule
+42 + global_agent_id + N_global * episode.  Inputs live in HBM before the
+timed region; every step writes the full obs [N,80] f32, reward, terminated
+and truncated tensors.
+
+One "step" = one batched env step of all agents on the GPU.  ``--fuse F``
+advances F steps per kernel launch (obs written for every step into a
+[F, N, 80] trajectory buffer, i.e. the rollout-buffer shape); F=1 is the
+drop-in VecEnv.step call.
+
+Usage:  python bench.py [--gpus N] [--steps K] [--warmup W] [--fuse F]
+For N>1 launch one rank per GPU with torch.distributed.run.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+from pathlib import Path
+
+REPO = Path(__file__).resolve().parent
+sys.path.insert(0, str(REPO / "3d-navigation-reinforcement-learning_amd"))
+
+METRIC = "env-steps/sec at 65536 parallel agents, 32×32×8 room, 1/2/4/8 MI355X"
+HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: 8.0 TB/s spec
+
+
+def algorithmic_bytes_per_step(L: int) -> int:
+    """action 1 + window 64 + rays 6L + state 2*16 + obs 320 + reward 4 + flags 2."""
+    return 1 + 64 + 6 * L + 32 + 320 + 4 + 2
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--agents", type=int, default=65536, help="agents per GPU")
+    ap.add_argument("--room", default="32x32x8", help="WxDxH of the walled-box room")
+    ap.add_argument("--L", type=int, default=10, help="local_map_length")
+    ap.add_argument("--fuse", type=int, default=1, help="env steps per kernel launch")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline sample budget (0 = skip)")
+    ap.add_argument("--json-out", default=None)
+    return ap.parse_args()
+
+
+def cpu_baseline(room_whd, L, seconds):
+    """The CPU oracle (C restatement of envs/CubicEnv.py step/reset) on the
+    host cores, same room / L / policy / seed schedule, bounded sample."""
+    import numpy as np
+    sys.path.insert(0, str(REPO))
+    from oracle.oracle import OracleEnv, parse_room_text
+    from voxnav.rooms import box_room, room_to_text
+    cores = len(os.sched_getaffinity(0))
+    threads = max(1, min(cores, int(os.environ.get("OMP_NUM_THREADS", cores))))
+    N = 512 * threads
+    W, D, H = room_whd
+    env = OracleEnv([parse_room_text(room_to_text(box_room(W, D, H)))], n_agents=N, local_map_length=L,
+                    use_room_draw=True)
+    env.run_random(42 + np.arange(N), policy_seed=42, K=1, seed_stride=N, record=False, threads=threads)
+    steps = 0
+    t0 = time.perf_counter()
+    k = 16
+    while True:
+        env.run_random(np.zeros(N, np.int64), policy_seed=42, K=k, t0=1 + steps // N, seed_stride=N,
+                       initial_reset=False, record=False, threads=threads)
+        steps += N * k
+        el = time.perf_counter() - t0
+        if el >= seconds:
+            break
+        k = min(1024, k * 2)
+    return {"value": steps / el, "unit": "env-steps/s", "cores": threads, "kind": "port",
+            "sample": f"{N} agents x {steps // N} steps of the same workload ({el:.1f} s) through "
+                      f"oracle/voxnav_oracle.c (C restatement of envs/CubicEnv.py, OpenMP over agents)"}
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+
+    from voxnav.env import BatchedGridEnv
+    from voxnav.rooms import box_room, single_room_set
+
+    W, D, H = (int(v) for v in args.room.split("x"))
+    N = args.agents
+    F = max(1, args.fuse)
+    env = BatchedGridEnv(num_agents=N, rooms=single_room_set(box_room(W, D, H)), local_map_length=args.L,
+                         autoreset=True, device=dev, agent_id_base=rank * N, seed_stride=N * world)
+    env.reset(seed=42)
+    from voxnav.env import Rollout
+    out = Rollout(torch.empty((F, N, 80), dtype=torch.float32, device=dev),
+                  torch.empty((F, N), dtype=torch.float32, device=dev),
+                  torch.empty((F, N), dtype=torch.uint8, device=dev),
+                  torch.empty((F, N), dtype=torch.uint8, device=dev), None)
+    launches_w = max(1, args.warmup // F)
+    launches = max(1, args.steps // F)
+    steps_timed = launches * F
+    for _ in range(launches_w):
+        env.step_random(F, policy_seed=42, out=out)
+    stream = torch.cuda.current_stream(dev)
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(launches)]
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for i in range(launches):
+        ev[i][0].record(stream)
+        env.step_random(F, policy_seed=42, out=out)
+        ev[i][1].record(stream)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    kern_ms = sum(a.elapsed_time(b) for a, b in ev) / launches
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+        k = torch.tensor([kern_ms], dtype=torch.float64, device=dev)
+        dist.all_reduce(k, op=dist.ReduceOp.MAX)
+        kern_ms = float(k.item())
+
+    # sanity: the trajectory buffer holds real observations
+    assert torch.isfinite(out.obs).all().item()
+
+    total_steps = N * world * steps_timed
+    value = total_steps / elapsed
+    bstep = algorithmic_bytes_per_step(args.L)
+    achieved = bstep * N * F / (kern_ms * 1e-3) / 1e9
+    roof = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": None,
+            "kernel": "env_kernel<12,false>", "kernel_avg_us": round(kern_ms * 1e3, 3),
+            "algorithmic_bytes_per_env_step": bstep, "env_steps_per_launch": N * F}
+    prof = REPO / "profiles" / "pmc_traffic.json"
+    if prof.exists():
+        try:
+            pm = json.loads(prof.read_text())
+            key = f"{W}x{D}x{H}_L{args.L}_N{N}_F{F}"
+            if key in pm:
+                roof["traffic"] = pm[key]["hbm_bytes_per_launch"]
+                roof["traffic_source"] = pm[key].get("source")
+        except Exception:  # noqa: BLE001
+            pass
+
+    if rank == 0:
+        rec = {
+            "metric": METRIC, "value": round(value, 1), "unit": "env-steps/s", "n_gpus": world,
+            "steps": steps_timed, "warmup": launches_w * F, "ms_per_step": round(elapsed * 1e3 / steps_timed, 5),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "int8",
+            "data": "synthetic (walled-box room in the reference room-file grammar; Philox uniform random policy)",
+            "config": {"workload": f"C3 env step: {N} agents/GPU, {W}x{D}x{H} room, L={args.L}, "
+                                   f"random policy, SB3 auto-reset", "agents_per_gpu": N,
+                       "global_agents": N * world, "room": f"{W}x{D}x{H}", "local_map_length": args.L,
+                       "steps_per_launch": F, "parallelism": f"agent-sharded x{world} (no collective in the step)"},
+            "roofline": roof,
+        }
+        if world == 1 and args.cpu_seconds > 0:
+            rec["cpu_baseline"] = cpu_baseline((W, D, H), args.L, args.cpu_seconds)
+        line = json.dumps(rec)
+        print(line, flush=True)
+        if args.json_out:
+            Path(args.json_out).write_text(line + "\n")
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,148 @@
+/*
+ * voxnav.h -- C-ABI of the MI355X-native batched voxel-grid exploration env
+ * (the hot path of Noimps/3D-Navigation-Reinforcement-Learning: envs/CubicEnv.py
+ * step/reset, batched the way train/Grid_Train.py batches it through SB3's
+ * SubprocVecEnv).  Implemented by libvoxnav.so (HIP, gfx950).
+ *
+ * Conventions
+ *   - every function returns 0 on success and a negative VN_ERR_* code on
+ *     failure; vn_last_error() returns a thread-local description.  No C++
+ *     exception ever crosses this boundary.
+ *   - "device" pointers are HIP device (HBM) pointers owned by the caller
+ *     (e.g. torch tensors' data_ptr()), contiguous, naturally aligned.
+ *   - `stream` is a hipStream_t passed as void* (NULL = default stream).
+ *     All env calls are stream-ordered and asynchronous; none synchronises
+ *     the host except to report a launch error.
+ *   - one VnEnv per host thread; a VnEnv is bound to one device.
+ *
+ * Reference interfaces each entry point replaces are cited per function
+ * (file:line into the reference tree).
+ */
+#ifndef VOXNAV_H
+#define VOXNAV_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define VN_ABI_VERSION 1
+#define VN_OBS_DIM 80            /* envs/CubicEnv.py:58-62, :295-311 */
+#define VN_STATE_FIELDS 16
+#define VN_MAX_L 16              /* largest supported local_map_length */
+#define VN_MAX_W 255
+#define VN_MAX_D 255
+#define VN_MAX_H 31
+#define VN_MAX_ROOMS 256
+
+enum {
+    VN_OK = 0,
+    VN_ERR_INVALID = -1,     /* bad argument (shape, range, NULL)          */
+    VN_ERR_HIP = -2,         /* HIP runtime error                          */
+    VN_ERR_ROOM = -3,        /* room has no interior free cell, too big... */
+    VN_ERR_OOM = -4
+};
+
+typedef struct VnEnv VnEnv;
+
+/*
+ * Parsed rooms, exactly what GridAgent.load_room produces per room
+ * (envs/CubicEnv.py:402-448): the dense grid with walls (grid == -2)
+ * flagged, plus an optional "Start position".  Rooms are in the order the
+ * caller wants random.choice to index (the build sorts file names).
+ */
+typedef struct VnRoomSet {
+    int32_t n_rooms;
+    const int32_t *whd;          /* [n_rooms][3]  W, D, H                       */
+    const uint8_t *walls;        /* concat of W*D*H bytes, index (x*D+y)*H+z    */
+    const int32_t *fixed_start;  /* [n_rooms][3] or NULL; -1 = draw a start     */
+} VnRoomSet;
+
+/* GridAgent ctor kwargs (envs/CubicEnv.py:17-29) + batching knobs. */
+typedef struct VnConfig {
+    int32_t local_map_length;    /* L (ctor default 4; Grid_Train uses 10)      */
+    int32_t use_room_draw;       /* 1: room_path given -> random.choice(rooms)  */
+    int32_t autoreset;           /* SB3 VecEnv auto-reset inside vn_step        */
+    int32_t reserved0;
+    double crash_penalty;        /* ctor default -2.0                           */
+    double finish_percentage;    /* FINISH_PERCENTAGE = 0.84 (CubicEnv.py:12)   */
+    int64_t agent_id_base;       /* global id of this shard's agent 0           */
+    int64_t seed_stride;         /* next episode seed = seed + stride (mod 2^32)*/
+} VnConfig;
+
+typedef struct VnInfo {
+    int32_t n_agents;
+    int32_t n_rooms;
+    int32_t local_map_length;
+    int32_t pad_w, pad_d, pad_h; /* belief map padding (max room dims, PH%4==0) */
+    int64_t belief_bytes_per_agent;
+    int64_t device_bytes;        /* total HBM owned by the env                  */
+} VnInfo;
+
+const char *vn_last_error(void);
+int vn_abi_version(void);
+
+/* GridAgent.__init__ for N agents on `device` (envs/CubicEnv.py:17-74). */
+int vn_create(const VnRoomSet *rooms, int32_t n_agents, const VnConfig *cfg, int32_t device, VnEnv **out);
+int vn_destroy(VnEnv *env);
+int vn_get_info(const VnEnv *env, VnInfo *info);
+
+/*
+ * GridAgent.reset(seed) for every agent with mask[i] != 0 (mask NULL = all)
+ * (envs/CubicEnv.py:77-108, draws :407/:462).  seeds: device int64 [N],
+ * each in [0, 2^32) (the reference also calls np.random.seed(seed), :80).
+ * obs: device f32 [N][80]; rows of unmasked agents are left untouched.
+ */
+int vn_reset(VnEnv *env, const int64_t *seeds, const uint8_t *mask, float *obs, void *stream);
+
+/*
+ * GridAgent.step(action) for all N agents (envs/CubicEnv.py:110-132),
+ * followed, when cfg.autoreset, by the SB3 VecEnv auto-reset of every agent
+ * whose step ended the episode (terminated or truncated).
+ *   actions       device i32 [N], each in 0..5
+ *   obs           device f32 [N][80]  (post-reset obs for finished agents)
+ *   reward        device f32 [N]      (may be NULL)  -- f64 reward rounded
+ *   reward64      device f64 [N]      (may be NULL)  -- exact f64 reward
+ *   terminated    device u8  [N]      (may be NULL)
+ *   truncated     device u8  [N]      (may be NULL)
+ *   terminal_obs  device f32 [N][80]  (may be NULL) written only for agents
+ *                 that finished an episode in this step
+ */
+int vn_step(VnEnv *env, const int32_t *actions, float *obs, float *reward, double *reward64,
+            uint8_t *terminated, uint8_t *truncated, float *terminal_obs, void *stream);
+
+/*
+ * k_steps fused steps under the build's uniform random policy
+ * (action = (Philox4x32-10(key=policy_seed, ctr=(gid, t0+k))[0] * 6) >> 32).
+ * Outputs are [k_steps][N]-major (obs [k_steps][N][80]); actions_out
+ * (device i32 [k_steps][N]) may be NULL.
+ */
+int vn_step_random(VnEnv *env, uint64_t policy_seed, uint64_t t0, int32_t k_steps, int32_t *actions_out,
+                   float *obs, float *reward, double *reward64, uint8_t *terminated, uint8_t *truncated,
+                   float *terminal_obs, void *stream);
+
+/*
+ * Parity dumps.  state_out: device i64 [N][16] in the field order
+ * x, y, z, facing, last_action, step_count, visited_count, bump_count,
+ * done, last_bump, near_wall, was_near_wall, cells_insight_down, room,
+ * max_steps, next_seed.
+ * belief_out: device i8 [N][pad_w][pad_d][pad_h] dense x-major; visit
+ * counts saturate at 127, cells outside the agent's room read -128.
+ */
+int vn_export_state(VnEnv *env, int64_t *state_out, void *stream);
+int vn_export_belief(VnEnv *env, int8_t *belief_out, void *stream);
+
+/*
+ * GAE advantage/return scan (SB3 RolloutBuffer.compute_returns_and_advantage,
+ * called from RecurrentPPO.learn at train/Grid_Train.py:228).  All arrays
+ * device f32, [T][N]-major; last_values/dones [N].
+ */
+int vn_gae(const float *rewards, const float *values, const float *episode_starts, const float *last_values,
+           const float *dones, int32_t T, int32_t N, double gamma, double gae_lambda, float *advantages,
+           float *returns, void *stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* VOXNAV_H */

@@ -1,0 +1,50 @@
+"""The C-ABI library builds for gfx950, loads, and exports include/voxnav.h."""
+import ctypes
+import re
+import subprocess
+
+from helpers import REPO
+
+HEADER = REPO / "include" / "voxnav.h"
+
+
+def declared_functions():
+    text = HEADER.read_text()
+    return sorted(set(re.findall(r"^\s*(?:const\s+)?\w+\s*\*?\s*(vn_\w+)\s*\(", text, flags=re.M)))
+
+
+def test_library_loads_and_exports_header_symbols():
+    from voxnav import _native
+    lib = _native.load()
+    decl = declared_functions()
+    assert len(decl) >= 11
+    for name in decl:
+        assert hasattr(lib, name), name
+    assert set(decl) == set(_native.EXPORTED_SYMBOLS)
+    assert lib.vn_abi_version() == 1
+    out = subprocess.run(["nm", "-D", "--defined-only", str(_native._build.LIB)], capture_output=True, text=True)
+    exported = set(re.findall(r" T (vn_\w+)", out.stdout))
+    assert set(decl) <= exported
+
+
+def test_code_object_targets_gfx950():
+    from voxnav import _build
+    blob = _build.LIB.read_bytes()
+    assert b"amdgcn-amd-amdhsa--gfx950" in blob      # the offload bundle id of the device code object
+    assert b"gfx942" not in blob and b"gfx90a" not in blob
+
+
+def test_errors_cross_the_boundary_as_codes():
+    from voxnav import _native
+    lib = _native.load()
+    h = ctypes.c_void_p()
+    cfg = _native.VnConfig(0, 1, 1, 0, -2.0, 0.84, 0, 0)   # L = 0 is invalid
+    rc = lib.vn_create(None, 4, ctypes.byref(cfg), 0, ctypes.byref(h))
+    assert rc < 0 and b"NULL" in lib.vn_last_error()
+    import numpy as np
+    whd = np.array([4, 4, 4], np.int32)
+    walls = np.zeros(64, np.uint8)
+    rs = _native.VnRoomSet(1, whd.ctypes.data, walls.ctypes.data, None)
+    rc = lib.vn_create(ctypes.byref(rs), 4, ctypes.byref(cfg), 0, ctypes.byref(h))
+    assert rc == -1 and b"local_map_length" in lib.vn_last_error()
+    assert lib.vn_step(None, None, None, None, None, None, None, None, None) == -1

@@ -1,0 +1,259 @@
+"""Parity of the HIP env (through the C-ABI) with the golden vectors and the oracle.
+
+Bar: bit-exact obs (f32 bytes), exact f64 reward, identical
+terminated/truncated flags, integer agent state and belief map (visit counts
+compared as min(count, 127), the device's saturating int8) -- on the
+reference's golden trajectories, and against the CPU oracle for batched
+random-policy rollouts with SB3 auto-reset, at sizes the oracle finishes in
+seconds.  Size-independent properties cover the full BASELINE shape.
+"""
+import numpy as np
+import pytest
+
+from helpers import (GOLDEN, STATE13, golden_trajectories, grid_hash, load_golden, oracle_env,
+                     product_room_set)
+
+torch = pytest.importorskip("torch")
+pytestmark = pytest.mark.gpu
+
+STATE_IDX = [0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12]
+
+
+@pytest.fixture(scope="module")
+def voxnav():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    import voxnav
+    voxnav.load_library()
+    return voxnav
+
+
+def make_env(voxnav, src, L, n=1, autoreset=False, **kw):
+    from voxnav.env import BatchedGridEnv
+    return BatchedGridEnv(num_agents=n, rooms=product_room_set(src), local_map_length=L, autoreset=autoreset,
+                          device="cuda:0", **kw)
+
+
+def belief_of(env, agent, whd):
+    W, D, H = whd
+    return env.belief()[agent, :W, :D, :H].cpu().numpy().astype(np.int64)
+
+
+@pytest.mark.parametrize("path", golden_trajectories(), ids=lambda p: p.stem)
+def test_golden_trajectory_on_gpu(voxnav, path):
+    d = load_golden(path)
+    src = str(d["room_source"])
+    env = make_env(voxnav, src, int(d["L"]), crash_penalty=float(d["crash_penalty"]))
+    rooms = env.room_set.rooms
+    seeds = [int(s) for s in d["seeds"]]
+    si = 0
+
+    def do_reset(ri):
+        nonlocal si
+        obs = env.reset(seed=[seeds[si]]).cpu().numpy()[0]
+        si += 1
+        assert obs.tobytes() == d["reset_obs"][ri].tobytes(), f"reset obs {ri}"
+        st = env.export_state()[0].cpu().numpy()
+        assert list(st[STATE_IDX]) == list(d["reset_state"][ri]), f"reset state {ri}"
+        room = rooms[int(st[13])]
+        assert grid_hash(room.grid()) == int(d["room_hash"][ri])
+        return room
+
+    room = do_reset(0)
+    ri = 1
+    dumps = {int(t): i for i, t in enumerate(d["dump_at"])}
+    acts = torch.as_tensor(d["actions"], dtype=torch.int32, device="cuda:0")
+    for t in range(len(d["actions"])):
+        res = env.step(acts[t:t + 1], reward_f64=True, terminal_obs=False)
+        obs = res.obs.cpu().numpy()[0]
+        assert obs.tobytes() == d["obs"][t].tobytes(), f"obs mismatch at step {t}"
+        assert float(res.reward[0].item()) == float(d["reward"][t]), f"reward at step {t}"
+        te, tr = bool(res.terminated[0].item()), bool(res.truncated[0].item())
+        assert (te, tr) == (bool(d["terminated"][t]), bool(d["truncated"][t])), t
+        st = env.export_state()[0].cpu().numpy()
+        assert list(st[STATE_IDX]) == list(d["state"][t]), f"state mismatch at step {t}"
+        if t in dumps or t % 97 == 0:
+            b = belief_of(env, 0, room.shape)
+            if t in dumps:
+                ref = np.minimum(d[f"belief_dump_{dumps[t]}"].astype(np.int64), 127)
+                assert (b == ref).all(), f"belief dump at step {t}"
+            if b.max() < 127:
+                assert grid_hash(b) == int(d["belief_hash"][t]), f"belief hash at step {t}"
+        if te or tr:
+            room = do_reset(ri)
+            ri += 1
+    assert si == len(seeds)
+
+
+ROLLOUT_CASES = [
+    # (room source, L, agents, steps)
+    ("box:8x8x4", 4, 512, 300),
+    ("ctor:8x8x4", 10, 256, 200),
+    ("box:16x16x8", 4, 512, 400),
+    ("ctor:32x32x8", 10, 1024, 150),
+    ("set:P2_training", 10, 1024, 200),
+    ("set:P3_training", 10, 1024, 200),
+    ("set:P1_training", 4, 256, 200),
+    ("file:P3_training/maze_3d_tunnels.txt", 10, 512, 400),
+    ("file:P2_training/tightcorridor.txt", 7, 300, 300),
+    ("file:P3_training/kitchen2.txt", 16, 256, 200),
+]
+
+
+@pytest.mark.parametrize("src,L,N,K", ROLLOUT_CASES, ids=[f"{c[0]}-L{c[1]}" for c in ROLLOUT_CASES])
+def test_random_rollout_matches_oracle(voxnav, src, L, N, K):
+    env = make_env(voxnav, src, L, n=N, autoreset=True)
+    seeds = 42 + np.arange(N, dtype=np.int64)
+    env.reset(seed=42)
+    ro = env.step_random(K, policy_seed=7, t0=0, record_actions=True, reward_f64=True)
+    orc = oracle_env(src, L, n_agents=N).run_random(seeds, policy_seed=7, K=K, seed_stride=N)
+    np.testing.assert_array_equal(ro.actions.cpu().numpy(), orc["actions"])
+    np.testing.assert_array_equal(ro.terminated.cpu().numpy(), orc["terminated"])
+    np.testing.assert_array_equal(ro.truncated.cpu().numpy(), orc["truncated"])
+    np.testing.assert_array_equal(ro.reward.cpu().numpy(), orc["reward"])
+    got = ro.obs.cpu().numpy()
+    bad = np.argwhere((got.view(np.uint32) != orc["obs"].view(np.uint32)).any(-1))
+    assert bad.size == 0, f"obs mismatch at (step, agent) {bad[:5].tolist()}"
+
+
+def test_step_with_actions_autoreset_terminal_obs(voxnav):
+    """vn_step with explicit actions: obs/terminal_obs/flags vs oracle (SB3 semantics)."""
+    src, L, N, K = "box:8x8x4", 4, 384, 160
+    env = make_env(voxnav, src, L, n=N, autoreset=True)
+    env.reset(seed=1000)
+    rng = np.random.default_rng(3)
+    acts = rng.integers(0, 6, size=(K, N)).astype(np.int32)
+    orc = oracle_env(src, L, n_agents=N).run_random(1000 + np.arange(N), policy_seed=0, K=K, seed_stride=N,
+                                                    actions=acts, terminal_obs=True)
+    at = torch.as_tensor(acts, device="cuda:0")
+    ended = 0
+    for k in range(K):
+        res = env.step(at[k], reward_f64=True, terminal_obs=True)
+        np.testing.assert_array_equal(res.obs.cpu().numpy(), orc["obs"][k])
+        np.testing.assert_array_equal(res.reward.cpu().numpy(), orc["reward"][k])
+        te, tr = res.terminated.cpu().numpy(), res.truncated.cpu().numpy()
+        np.testing.assert_array_equal(te, orc["terminated"][k].astype(bool))
+        np.testing.assert_array_equal(tr, orc["truncated"][k].astype(bool))
+        done = te | tr
+        ended += int(done.sum())
+        np.testing.assert_array_equal(res.terminal_obs.cpu().numpy()[done], orc["terminal_obs"][k][done])
+    assert ended >= N  # every agent finished at least one 72-step episode
+
+
+@pytest.mark.parametrize("tag", ["P1_training", "P2_training", "P3_training", "P2_evaluate", "box32x32x8"])
+def test_reset_draws_match_reference_on_gpu(voxnav, tag):
+    z = load_golden(GOLDEN / f"reset_table_{tag}.npz")
+    src = "ctor:32x32x8" if tag.startswith("box") else f"set:{tag}"
+    seeds = z["seeds"].astype(np.int64)
+    env = make_env(voxnav, src, 10, n=len(seeds))
+    env.reset(seed=seeds)
+    st = env.export_state().cpu().numpy()
+    got = np.stack([st[:, 13], st[:, 0], st[:, 1], st[:, 2]], axis=1)
+    np.testing.assert_array_equal(got, z["draws"])
+
+
+def test_reset_many_rejections_slow_path(voxnav):
+    """Seeds whose reset needs > 8 MT words exercise the device slow path."""
+    src = "set:P2_evaluate"   # 7 rooms: k=3 bits, reject 1/8
+    orc = oracle_env(src, 4)
+    found = []
+    for s in range(200000):
+        room, xyz, draws = orc.reset_draw(s)
+        if draws >= 6:
+            found.append((s, room, xyz, draws))
+        if len(found) >= 64:
+            break
+    assert max(f[3] for f in found) >= 9, "no seed needing > 8 draws found"
+    seeds = np.array([f[0] for f in found], np.int64)
+    env = make_env(voxnav, src, 4, n=len(seeds))
+    env.reset(seed=seeds)
+    st = env.export_state().cpu().numpy()
+    for i, (s, room, xyz, draws) in enumerate(found):
+        assert (st[i, 13], st[i, 0], st[i, 1], st[i, 2]) == (room, *xyz), (s, draws)
+
+
+def test_sharding_is_bitwise_invariant(voxnav):
+    """Two shards (agent_id_base 0 and N/2) == one env of N agents."""
+    src, L, N, K = "set:P3_training", 10, 512, 120
+    full = make_env(voxnav, src, L, n=N, autoreset=True)
+    full.reset(seed=42)
+    a = full.step_random(K, policy_seed=5, t0=0)
+    parts = []
+    for base in (0, N // 2):
+        sh = make_env(voxnav, src, L, n=N // 2, autoreset=True, agent_id_base=base, seed_stride=N)
+        sh.reset(seed=42)
+        parts.append(sh.step_random(K, policy_seed=5, t0=0))
+    obs = torch.cat([parts[0].obs, parts[1].obs], dim=1)
+    assert torch.equal(obs, a.obs)
+    assert torch.equal(torch.cat([parts[0].reward, parts[1].reward], 1), a.reward)
+
+
+def test_fused_k_equals_single_steps(voxnav):
+    src, L, N = "set:P2_training", 10, 640
+    e1 = make_env(voxnav, src, L, n=N, autoreset=True)
+    e2 = make_env(voxnav, src, L, n=N, autoreset=True)
+    e1.reset(seed=9)
+    e2.reset(seed=9)
+    a = e1.step_random(64, policy_seed=11, t0=100)
+    for k in range(64):
+        b = e2.step_random(1, policy_seed=11, t0=100 + k)
+        assert torch.equal(a.obs[k], b.obs[0]), k
+        assert torch.equal(a.reward[k], b.reward[0]), k
+
+
+def test_full_size_properties(voxnav):
+    """BASELINE config at full size (65536 agents, 32x32x8, L=10): a sampled
+    subset of agents against the oracle + size-independent invariants."""
+    N, L, K = 65536, 10, 64
+    env = make_env(voxnav, "box:32x32x8", L, n=N, autoreset=True)
+    env.reset(seed=42)
+    ro = env.step_random(K, policy_seed=42, t0=0, reward_f64=True)
+    obs = ro.obs.cpu().numpy()
+    # window values lie on the (v+2)/22 lattice, facing one-hot sums to 1
+    lattice = (np.arange(23, dtype=np.float32) / np.float32(22.0)).astype(np.float32)
+    assert np.isin(obs[:, :, :64], lattice).all()
+    np.testing.assert_array_equal(obs[:, :, 64:68].sum(-1), 1.0)
+    assert (obs[:, :, 73:] == 0).all()
+    # sampled agents replayed alone through the oracle (agents are independent)
+    rng = np.random.default_rng(0)
+    for g in rng.choice(N, size=24, replace=False):
+        orc = oracle_env("box:32x32x8", L, n_agents=1).run_random(
+            [42 + int(g)], policy_seed=42, K=K, gid_base=int(g), seed_stride=N)
+        assert obs[:, g].tobytes() == orc["obs"][:, 0].tobytes(), g
+        np.testing.assert_array_equal(ro.reward[:, g].cpu().numpy(), orc["reward"][:, 0])
+
+
+def test_gae_matches_oracle(voxnav):
+    from oracle.oracle import gae as oracle_gae
+    from voxnav.gae import compute_gae
+    T, N = 128, 3000
+    rng = np.random.default_rng(1)
+    r = rng.normal(size=(T, N)).astype(np.float32)
+    v = rng.normal(size=(T, N)).astype(np.float32)
+    s = (rng.random((T, N)) < 0.05).astype(np.float32)
+    s[0] = 1
+    lv = rng.normal(size=N).astype(np.float32)
+    dn = (rng.random(N) < 0.1).astype(np.float32)
+    adv, ret = compute_gae(*(torch.as_tensor(a, device="cuda:0") for a in (r, v, s, lv, dn)))
+    ea, er = oracle_gae(r, v, s, lv, dn)
+    np.testing.assert_array_equal(adv.cpu().numpy(), ea)
+    np.testing.assert_array_equal(ret.cpu().numpy(), er)
+
+
+def test_gridagent_facade_matches_golden(voxnav):
+    from voxnav.gym_api import GridAgent
+    d = load_golden(GOLDEN / "traj_box8x8x4_file_L4_explore.npz")
+    ag = GridAgent(local_map_length=4, rooms=product_room_set("box:8x8x4").rooms)
+    obs, info = ag.reset(seed=int(d["seeds"][0]))
+    assert obs.dtype == np.float32 and obs.shape == (80,) and info == {}
+    assert obs.tobytes() == d["reset_obs"][0].tobytes()
+    si = 1
+    for t, a in enumerate(d["actions"][:150]):
+        obs, r, te, tr, info = ag.step(int(a))
+        assert isinstance(r, np.float64) and r == d["reward"][t]
+        assert obs.tobytes() == d["obs"][t].tobytes()
+        assert ag.visited_count == d["state"][t][6] and ag.bump_count == d["state"][t][7]
+        if te or tr:
+            ag.reset(seed=int(d["seeds"][si]))
+            si += 1
+    ag.close()
