@@ -655,7 +655,7 @@ __global__ __launch_bounds__(256) void env_kernel(Params p) {
                                           | (3u << 16) | (1u << 18) | (2u << 20) | (0u << 22)  // back
                                           | (1u << 24) | (2u << 26) | (0u << 28) | (3u << 30); // left
                 dir = (int)((kDir >> (2 * (a * 4 + g.facing))) & 3u);
-                g.facing = (int)((0x9Cu >> (2 * dir)) & 3u);  // +x->E(1) -x->W(3) +y->N(0) -y->S(2)
+                g.facing = (int)((0x8Du >> (2 * dir)) & 3u);  // +x->E(1) -x->W(3) +y->N(0) -y->S(2)
             } else {
                 dir = (a == 4) ? 4 : 5;
             }

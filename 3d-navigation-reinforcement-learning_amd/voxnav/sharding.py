@@ -1,0 +1,79 @@
+"""Agent sharding across GPUs (one process per GPU, torch.distributed).
+
+The reference runs one env per OS process (train/Grid_Train.py:191-192);
+agents never interact.  Here GPU ``rank`` of ``world`` owns global agents
+``[rank * n_local, (rank + 1) * n_local)``; seeds and the random-policy
+stream are keyed by the global agent id, so the union of the shards is
+bitwise identical to a single-GPU run over the same ids.  The env step has
+NO collective.  The only data exchange is at the rollout boundary:
+``allgather_rollout`` gathers the trajectory buffers (RCCL over xGMI with
+the "nccl" backend; gloo on CPU in tests).
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+from typing import Dict, Optional
+
+import torch
+import torch.distributed as dist
+
+
+@dataclass(frozen=True)
+class Shard:
+    rank: int
+    world: int
+    n_local: int
+
+    @property
+    def agent_id_base(self) -> int:
+        return self.rank * self.n_local
+
+    @property
+    def n_global(self) -> int:
+        return self.n_local * self.world
+
+    @property
+    def seed_stride(self) -> int:
+        """Seed increment between consecutive episodes of one agent."""
+        return self.n_global
+
+
+def shard_for(n_local: int, rank: Optional[int] = None, world: Optional[int] = None) -> Shard:
+    if rank is None or world is None:
+        if dist.is_available() and dist.is_initialized():
+            rank, world = dist.get_rank(), dist.get_world_size()
+        else:
+            rank, world = 0, 1
+    return Shard(int(rank), int(world), int(n_local))
+
+
+def allgather_rollout(buffers: Dict[str, torch.Tensor], agent_dim: int = 1,
+                      group=None) -> Dict[str, torch.Tensor]:
+    """All-gather per-shard trajectory buffers along the agent dimension.
+
+    Each tensor is [T, n_local, ...] (agent_dim=1); the result is
+    [T, n_global, ...] ordered by rank, i.e. by global agent id.  One
+    collective per buffer, issued back to back (large messages: the ring is
+    per-link bound on xGMI, so fewer bigger transfers are preferable).
+    """
+    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size(group) == 1:
+        return dict(buffers)
+    world = dist.get_world_size(group)
+    out = {}
+    for name, t in buffers.items():
+        t = t.contiguous()
+        moved = t.movedim(agent_dim, 0).contiguous()
+        gathered = torch.empty((world * moved.shape[0],) + tuple(moved.shape[1:]), dtype=moved.dtype,
+                               device=moved.device)
+        dist.all_gather_into_tensor(gathered, moved, group=group)
+        out[name] = gathered.movedim(0, agent_dim).contiguous()
+    return out
+
+
+def max_over_ranks(value: float, device=None, group=None) -> float:
+    """Max of a scalar over ranks (the bench's timing rule)."""
+    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size(group) == 1:
+        return float(value)
+    t = torch.tensor([value], dtype=torch.float64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
+    return float(t.item())

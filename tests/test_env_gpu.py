@@ -66,7 +66,12 @@ def test_golden_trajectory_on_gpu(voxnav, path):
     for t in range(len(d["actions"])):
         res = env.step(acts[t:t + 1], reward_f64=True, terminal_obs=False)
         obs = res.obs.cpu().numpy()[0]
-        assert obs.tobytes() == d["obs"][t].tobytes(), f"obs mismatch at step {t}"
+        if obs.tobytes() != d["obs"][t].tobytes():
+            idx = np.nonzero(obs.view(np.uint32) != d["obs"][t].view(np.uint32))[0]
+            st = env.export_state()[0].cpu().numpy()
+            raise AssertionError(f"obs mismatch at step {t} (action {d['actions'][t]}): idx {idx.tolist()} "
+                                 f"got {obs[idx].tolist()} want {d['obs'][t][idx].tolist()}; "
+                                 f"state got {st[STATE_IDX].tolist()} want {d['state'][t].tolist()}")
         assert float(res.reward[0].item()) == float(d["reward"][t]), f"reward at step {t}"
         te, tr = bool(res.terminated[0].item()), bool(res.truncated[0].item())
         assert (te, tr) == (bool(d["terminated"][t]), bool(d["truncated"][t])), t
