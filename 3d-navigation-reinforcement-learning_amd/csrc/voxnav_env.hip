@@ -34,6 +34,7 @@
 
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <new>
 #include <string>
@@ -81,12 +82,13 @@ struct RoomDesc {          // 32 B, two uint4
     uint32_t start_off;    // first packed start cell (x | y<<8 | z<<16)
     int32_t fixed_start;   // packed "Start position" or -1
     uint32_t bricks;       // ceil(W/4) | ceil(D/4)<<16
-    uint32_t pad0, pad1;
+    uint32_t finish_visits;// smallest visited count with visited/total >= finish (f64)
+    uint32_t pad1;
 };
 
 struct Room {
     int W, D, H;
-    uint32_t total_free, ray_off, start_off;
+    uint32_t total_free, ray_off, start_off, finish_visits;
     int32_t fixed_start;
     int nbx, nby;
 };
@@ -108,7 +110,10 @@ struct Params {
     const float *lut;
     int32_t *err;
     int N, L, nby, ph;
-    uint32_t map_bytes;
+    uint32_t map_bytes;      // byte map (bricked) per agent
+    uint32_t agent_bytes;    // stride: byte map + x-plane + y-plane
+    uint32_t xp_off, yp_off; // plane offsets inside the agent block
+    int nwx, nwy;            // u64 words per plane row
     int n_rooms, use_room_draw, autoreset;
     uint32_t seed_stride;
     double crash_penalty, finish;
@@ -123,6 +128,7 @@ struct Params {
     uint8_t *term, *trunc;
     const int64_t *seeds;    // reset-only launches
     const uint8_t *mask;
+    uint32_t ablate;         // diagnostics only (VOXNAV_ABLATE): skip parts of the step, results invalid
 };
 
 __device__ __forceinline__ Agent unpack(uint4 s) {
@@ -169,13 +175,10 @@ __device__ __forceinline__ Room load_room(const Params &p, int r) {
     R.fixed_start = (int32_t)b.x;
     R.nbx = b.y & 0xffff;
     R.nby = b.y >> 16;
+    R.finish_visits = b.z;
     return R;
 }
 
-// byte offset of cell (x,y,z) inside one agent's bricked belief map
-__device__ __forceinline__ uint32_t boff(int x, int y, int z, int nby, int ph) {
-    return (uint32_t)((((((x >> 2) * nby + (y >> 2)) << 4) + ((x & 3) << 2) + (y & 3)) * ph) + z);
-}
 
 // ----------------------------------------------------------------------------
 // CPython random: streaming MT19937 seed (init_by_array with a one-word key)
@@ -290,10 +293,12 @@ struct MtStream {
 };
 
 // ----------------------------------------------------------------------------
-// Philox4x32-10 random policy (build-defined)
+// Philox4x32-10 random policy (build-defined): one call per
+// agent per 4 steps, counter = (global agent id, t / 4), word t % 4,
+// action = (word * 6) >> 32.
 // ----------------------------------------------------------------------------
-__device__ __forceinline__ int philox_action(uint64_t key, uint64_t gid, uint64_t t) {
-    uint32_t c0 = (uint32_t)gid, c1 = (uint32_t)(gid >> 32), c2 = (uint32_t)t, c3 = (uint32_t)(t >> 32);
+__device__ __forceinline__ uint4 philox4x32_10(uint64_t key, uint64_t gid, uint64_t blk) {
+    uint32_t c0 = (uint32_t)gid, c1 = (uint32_t)(gid >> 32), c2 = (uint32_t)blk, c3 = (uint32_t)(blk >> 32);
     uint32_t k0 = (uint32_t)key, k1 = (uint32_t)(key >> 32);
 #pragma unroll
     for (int r = 0; r < 10; ++r) {
@@ -308,259 +313,351 @@ __device__ __forceinline__ int philox_action(uint64_t key, uint64_t gid, uint64_
         c2 = hi0 ^ c3 ^ k1;
         c3 = lo0;
     }
-    return (int)(((uint64_t)c0 * 6u) >> 32);
+    return make_uint4(c0, c1, c2, c3);
 }
 
 // ----------------------------------------------------------------------------
-// sensing + observation (get_obs, envs/CubicEnv.py:254-312, with the ray
-// side effects of _sense_direction :345-397 and the visit update of
-// _mark_visited/do_action :156-166 folded into the same belief pass)
+// Agent groups: 4 lanes per agent (16 agents per wave64).
+//
+// Lane q of an agent owns window row dy = q - 2: it loads the 4 columns
+// (x+i-2, y+q-2), i = 0..3 (z contiguous, one 8/16/32-byte access each) and
+// writes obs[16i+4q .. 16i+4q+3] -- the 4 lanes of an agent store 64
+// contiguous bytes per instruction.  The horizontal ray cells beyond the
+// window are spread over the 4 lanes (4 consecutive cells of one ray per
+// instruction), so every wave instruction touches ~1-2 cache lines per agent.
+// Control state (pose, counters, flags, reward) is held redundantly by the
+// 4 lanes.
+//
+// Belief byte encoding (OR-able):  bit7 = known, bit6 = wall, bits0-5 =
+// visit count (saturating at 63; obs clips at 20, reward caps at 25).
+//   unknown (-1) = 0x00, known free (0) = 0x80, visited n = 0x80|n,
+//   known wall (-2) = 0xC0.
+// Sensing marks a free cell by OR 0x80 and the first wall by OR 0xC0,
+// idempotent, so a cell already known is never rewritten.
 // ----------------------------------------------------------------------------
-// ray directions: 0 +x, 1 -x, 2 +y, 3 -y, 4 +z (up), 5 -z (down)
+constexpr int GROUP = 4;
+constexpr uint32_t KNOWN = 0x80u, WALLB = 0xC0u;
+// LDS table: [0,256) obs value of each belief byte; [256,262) f32(a/5);
+// [264,281) f32(c/L)   (get_obs :273-275, :284, :287)
+constexpr int TAB_ACTION = 256, TAB_CID = 264, TAB_SIZE = 288;
 
-__device__ __forceinline__ uint32_t patch_byte(uint32_t b, int s, int nf, bool wh) {
-    if (s <= nf) return b == 0xffu ? 0u : b;       // known free: -1 -> 0  (:386-387)
-    if (wh && s == nf + 1) return 0xfeu;            // first wall -> -2     (:374-375)
-    return b;
+__device__ __forceinline__ int decode_count(uint32_t b) {   // center cell: known free or unknown
+    return (b & KNOWN) ? (int)(b & 0x3fu) : -1;
+}
+
+template <int PH>
+struct Col {
+    uint32_t w[PH / 4];
+};
+
+template <int PH>
+__device__ __forceinline__ void col_load(const int8_t *p, Col<PH> &c) {
+    if constexpr (PH == 8) {
+        const uint2 v = *reinterpret_cast<const uint2 *>(p);
+        c.w[0] = v.x;
+        c.w[1] = v.y;
+    } else {
+#pragma unroll
+        for (int q = 0; q < PH / 16; ++q) {
+            const uint4 v = reinterpret_cast<const uint4 *>(p)[q];
+            c.w[4 * q + 0] = v.x;
+            c.w[4 * q + 1] = v.y;
+            c.w[4 * q + 2] = v.z;
+            c.w[4 * q + 3] = v.w;
+        }
+    }
+}
+
+template <int PH>
+__device__ __forceinline__ void col_store(int8_t *p, const Col<PH> &c) {
+    if constexpr (PH == 8) {
+        *reinterpret_cast<uint2 *>(p) = make_uint2(c.w[0], c.w[1]);
+    } else {
+#pragma unroll
+        for (int q = 0; q < PH / 16; ++q)
+            reinterpret_cast<uint4 *>(p)[q] = make_uint4(c.w[4 * q], c.w[4 * q + 1], c.w[4 * q + 2], c.w[4 * q + 3]);
+    }
+}
+
+// byte i (dynamic) of the column; 0 (= unknown) outside [0, PH)
+template <int PH>
+__device__ __forceinline__ uint32_t col_byte(const Col<PH> &c, int i) {
+    uint32_t w = 0;
+#pragma unroll
+    for (int k = 0; k < PH / 4; ++k) w = ((i >> 2) == k) ? c.w[k] : w;
+    return (i >= 0 && i < PH) ? ((w >> (8 * (i & 3))) & 0xffu) : 0u;
+}
+
+template <int PH>
+__device__ __forceinline__ void col_or(Col<PH> &c, int i, uint32_t v) {
+#pragma unroll
+    for (int k = 0; k < PH / 4; ++k)
+        if ((i >> 2) == k) c.w[k] |= v << (8 * (i & 3));
+}
+
+template <int PH>
+__device__ __forceinline__ void col_set(Col<PH> &c, int i, uint32_t v) {
+#pragma unroll
+    for (int k = 0; k < PH / 4; ++k)
+        if ((i >> 2) == k) c.w[k] = (c.w[k] & ~(0xffu << (8 * (i & 3)))) | (v << (8 * (i & 3)));
+}
+
+// OR `v` into bytes [lo, hi] (inclusive) -- the z rays
+template <int PH>
+__device__ __forceinline__ void col_or_range(Col<PH> &c, int lo, int hi, uint32_t v) {
+#pragma unroll
+    for (int k = 0; k < PH / 4; ++k) {
+        uint32_t m = 0;
+#pragma unroll
+        for (int b = 0; b < 4; ++b) {
+            const int i = 4 * k + b;
+            m |= (i >= lo && i <= hi) ? (v << (8 * b)) : 0u;
+        }
+        c.w[k] |= m;
+    }
+}
+
+template <int PH>
+__device__ __forceinline__ bool col_differs(const Col<PH> &a, const Col<PH> &b) {
+    bool d = false;
+#pragma unroll
+    for (int k = 0; k < PH / 4; ++k) d |= a.w[k] != b.w[k];
+    return d;
+}
+
+template <int PH>
+__device__ __forceinline__ uint32_t boff(int x, int y, int z, int nby) {
+    return (uint32_t)((((((x >> 2) * nby + (y >> 2)) << 4) + ((x & 3) << 2) + (y & 3)) * PH) + z);
 }
 
 // Destination of the observation row.  With auto-reset, a step that ends the
 // episode writes its obs to the terminal row (NULL: dropped) and the reset
-// obs goes to the regular row; `ends` needs the post-move visited count.
+// obs goes to the regular row.
 struct ObsDst {
     float *row;
     float *term_row;
-    bool select;       // auto-reset step: choose between row and term_row
+    bool select;
     bool truncated;
 };
 
-template <int LMAX, bool FRESH>
-__device__ __forceinline__ int sense_observe(const Params &p, int8_t *map, Agent &g, const Room &R, bool moved,
-                                             bool &explored, const float *lut, ObsDst dst) {
-    const int x = g.x, y = g.y, z = g.z, nby = p.nby, ph = p.ph, L = p.L;
-    const uint2 rec = p.rays[R.ray_off + (uint32_t)((x * R.D + y) * R.H + z)];
-
-    // ---- 4x4x4 window, one funnel-shifted dword pair per (x,y) column ----
-    uint32_t win[16];
-    if (FRESH) {
-#pragma unroll
-        for (int c = 0; c < 16; ++c) win[c] = 0xffffffffu;
-    } else {
-        const int d0 = (z - 2) >> 2;
-        const int sh = ((z - 2) & 3) * 8;
-        const int ndw = ph >> 2;
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                const int cx = x + i - 2, cy = y + j - 2;
-                uint32_t lo = 0xffffffffu, hi = 0xffffffffu;
-                if (cx >= 0 && cx < R.W && cy >= 0 && cy < R.D) {
-                    const uint32_t *col = reinterpret_cast<const uint32_t *>(map + boff(cx, cy, 0, nby, ph));
-                    if (d0 >= 0) lo = col[d0];
-                    if (d0 + 1 < ndw) hi = col[d0 + 1];
-                }
-                win[i * 4 + j] = (uint32_t)(((((uint64_t)hi) << 32) | lo) >> sh);
-            }
-        }
-    }
-
-    // ---- ray extents ----
+struct Rays {
     int nf[6];
     bool wh[6];
+};
+
+// sensing mark of ray r at step s for a byte of a register column
+template <int PH>
+__device__ __forceinline__ void mark(Col<PH> &c, int z, const Rays &ry, int r, int s) {
+    if (s <= ry.nf[r]) col_or<PH>(c, z, KNOWN);
+    else if (ry.wh[r] && s == ry.nf[r] + 1) col_or<PH>(c, z, WALLB);
+}
+
+// One sensing pass (get_obs :254-312 with _sense_direction :345-397 and the
+// visit update of _mark_visited/do_action :156-166) for this lane's agent.
+// Returns the center cell's visit count after the update.
+template <int PH, int LMAX, bool FRESH>
+__device__ __forceinline__ int sense_observe(const Params &p, int8_t *map, Agent &g, const Room &R, bool moved,
+                                             bool &explored, const float *tab, ObsDst dst, int q) {
+    const int x = g.x, y = g.y, z = g.z, nby = p.nby, L = p.L;
+    const uint2 rec = p.rays[R.ray_off + (uint32_t)((x * R.D + y) * R.H + z)];
+
+    // ---- this lane's 4 window columns ----
+    const int cy = y + q - 2;
+    const bool yin = cy >= 0 && cy < R.D;
+    Col<PH> col[4];
+    bool cin[4];
+    uint32_t coff[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int cx = x + i - 2;
+        cin[i] = yin && cx >= 0 && cx < R.W;
+        coff[i] = boff<PH>(cin[i] ? cx : x, cin[i] ? cy : y, 0, nby);
+#pragma unroll
+        for (int k = 0; k < PH / 4; ++k) col[i].w[k] = 0u;
+        if (!FRESH && cin[i] && !(p.ablate & 1u)) col_load<PH>(map + coff[i], col[i]);
+    }
+    Col<PH> orig[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) orig[i] = col[i];
+
+    // ---- ray extents from the room's 8-byte record (bit7: ended at a wall) ----
+    Rays ry;
     bool near = false;
-    int center;
     uint32_t mm = 0;
 #pragma unroll
     for (int r = 0; r < 6; ++r) {
         const uint32_t e = (r < 4 ? (rec.x >> (8 * r)) : (rec.y >> (8 * (r - 4)))) & 0xffu;
         const int n = (int)(e & 0x7fu);
         const bool wf = (e >> 7) != 0;
-        nf[r] = n < L ? n : L;
-        wh[r] = wf && n < L;
-        near |= (n == 0) && wf;   // wall at step 1 -> near_wall (:378-379)
+        ry.nf[r] = n < L ? n : L;
+        ry.wh[r] = wf && n < L;
+        near |= (n == 0) && wf;          // wall at step 1 -> near_wall (:378-379)
         mm |= (n > 0 ? 1u : 0u) << r;
     }
 
-    // ---- ray cells outside the window: load (all first), patch, store ----
-    // in-window steps: +x,+y,+z s=1; -x,-y,-z s=1,2
-    constexpr int NS = LMAX;  // slots s = 0..LMAX-1 map to steps s0+slot
-    uint32_t rv[6][NS];
-    const uint32_t cb = boff(x, y, 0, nby, ph);
+    // ---- x / y rays through the per-axis "marked" bit planes ----
+    // Row (y, z) of the x-plane holds one bit per x: set once an x-ray (or the
+    // agent standing there) has marked the cell.  The agent's own cell is
+    // marked in both planes, so a cell newly marked here is never a visited
+    // cell and its byte can be written blind (0x80 free / 0xC0 first wall).
+    // Lane 0 owns the x row, lane 1 the y row.
+    uint64_t pm[2] = {0, 0}, pn[2] = {0, 0};
+    uint64_t *prow = nullptr;
+    int pa = 0, pw0 = 0, pwend = 0, pc = 0, nfp = 0, nfm = 0;
+    bool whp = false, whm = false;
+    if (q < 2) {
+        const bool xr = q == 0;
+        pc = xr ? x : y;                                   // agent coordinate along the axis
+        nfp = xr ? ry.nf[0] : ry.nf[2];
+        nfm = xr ? ry.nf[1] : ry.nf[3];
+        whp = xr ? ry.wh[0] : ry.wh[2];
+        whm = xr ? ry.wh[1] : ry.wh[3];
+        pa = pc - nfm - (whm ? 1 : 0);                     // marked span [pa, pb]
+        const int pb = pc + nfp + (whp ? 1 : 0);
+        pw0 = pa >> 6;
+        pwend = pb >> 6;
+        const int nw = xr ? p.nwx : p.nwy;
+        prow = reinterpret_cast<uint64_t *>(map + (xr ? p.xp_off : p.yp_off)) +
+               (size_t)((xr ? y : x) * PH + z) * nw;
 #pragma unroll
-    for (int r = 0; r < 6; ++r) {
-        const int s0 = (r & 1) ? 3 : 2;
-        const int lim = nf[r] + (wh[r] ? 1 : 0);
-#pragma unroll
-        for (int t = 0; t < NS; ++t) {
-            const int s = s0 + t;
-            rv[r][t] = 0xffu;
-            if (!FRESH && s <= LMAX && s <= lim) {
-                uint32_t a;
-                switch (r) {
-                    case 0: a = boff(x + s, y, z, nby, ph); break;
-                    case 1: a = boff(x - s, y, z, nby, ph); break;
-                    case 2: a = boff(x, y + s, z, nby, ph); break;
-                    case 3: a = boff(x, y - s, z, nby, ph); break;
-                    case 4: a = cb + z + s; break;
-                    default: a = cb + z - s; break;
-                }
-                rv[r][t] = (uint8_t)map[a];
-            }
+        for (int w = 0; w < 2; ++w) {
+            const int base = (pw0 + w) * 64;
+            const int lo = pa - base < 0 ? 0 : pa - base, hi = pb - base > 63 ? 63 : pb - base;
+            pm[w] = (w == 0 || pw0 + 1 <= pwend) && hi >= lo ? ((~0ull) >> (63 - (hi - lo))) << lo : 0ull;
+        }
+        if (!FRESH) {
+            pn[0] = prow[pw0];
+            if (pwend > pw0) pn[1] = prow[pw0 + 1];
         }
     }
+
+    // ---- in-window ray cells, z rays and the center ----
+    uint32_t cold = 0;
+    if (q == 2) {                       // row dy = 0: -x s=2, -x s=1, center, +x s=1
+        mark<PH>(col[0], z, ry, 1, 2);
+        mark<PH>(col[1], z, ry, 1, 1);
+        mark<PH>(col[3], z, ry, 0, 1);
+        cold = col_byte<PH>(col[2], z);
+        col_or_range<PH>(col[2], z + 1, z + ry.nf[4], KNOWN);                    // up
+        if (ry.wh[4]) col_or<PH>(col[2], z + ry.nf[4] + 1, WALLB);
+        col_or_range<PH>(col[2], z - ry.nf[5], z - 1, KNOWN);                    // down
+        if (ry.wh[5]) col_or<PH>(col[2], z - ry.nf[5] - 1, WALLB);
+    } else {                            // column dx = 0: -y s=2 (q0), -y s=1 (q1), +y s=1 (q3)
+        mark<PH>(col[2], z, ry, q == 3 ? 2 : 3, q == 0 ? 2 : 1);
+    }
+    cold = (uint32_t)__shfl((int)cold, 2, GROUP);
+    int t;
+    if (FRESH) {
+        t = 1;                                                                  // start cell (:85)
+    } else {
+        t = decode_count(cold);
+        if (moved) {
+            if (t == 0) {
+                t = 1;
+                ++g.visited;
+                explored = true;
+            } else if (t > 0) {
+                t += 1;
+            }
+        }
+        t += 1;
+        if (t > 63) t = 63;
+    }
+    if (q == 2) col_set<PH>(col[2], z, KNOWN | (uint32_t)t);
+
+    // ---- write back changed columns and ray cells ----
 #pragma unroll
-    for (int r = 0; r < 6; ++r) {
-        const int s0 = (r & 1) ? 3 : 2;
-        const int lim = nf[r] + (wh[r] ? 1 : 0);
+    for (int i = 0; i < 4; ++i)
+        if (cin[i] && col_differs<PH>(col[i], orig[i]) && !(p.ablate & 8u)) col_store<PH>(map + coff[i], col[i]);
+    if (q < 2) {
 #pragma unroll
-        for (int t = 0; t < NS; ++t) {
-            const int s = s0 + t;
-            if (s <= LMAX && s <= lim) {
-                const uint32_t nb = patch_byte(rv[r][t], s, nf[r], wh[r]);
-                if (nb != rv[r][t]) {
-                    uint32_t a;
-                    switch (r) {
-                        case 0: a = boff(x + s, y, z, nby, ph); break;
-                        case 1: a = boff(x - s, y, z, nby, ph); break;
-                        case 2: a = boff(x, y + s, z, nby, ph); break;
-                        case 3: a = boff(x, y - s, z, nby, ph); break;
-                        case 4: a = cb + z + s; break;
-                        default: a = cb + z - s; break;
+        for (int w = 0; w < 2; ++w) {
+            uint64_t nw = pm[w] & ~pn[w];
+            if (nw) {
+                prow[pw0 + w] = pn[w] | pm[w];
+                const int base = (pw0 + w) * 64;
+                while (nw) {
+                    const int pos = base + __ffsll((unsigned long long)nw) - 1;
+                    nw &= nw - 1;
+                    const int d = pos - pc;                       // in-window cells -2..+1 are in registers
+                    if (d >= 2 || d <= -3) {
+                        const uint32_t v = (d == nfp + 1 || d == -nfm - 1) ? WALLB : KNOWN;
+                        const int bx = q == 0 ? pos : x, by = q == 0 ? y : pos;
+                        map[boff<PH>(bx, by, z, nby)] = (int8_t)v;
                     }
-                    map[a] = (int8_t)nb;
                 }
             }
         }
     }
-
-    // ---- center cell: _mark_visited(target) then the +1 of :165-166 ----
-    {
-        int t;
-        if (FRESH) {
-            t = 1;                                    // start cell (:85)
-        } else {
-            t = (int)(int8_t)((win[10] >> 16) & 0xffu);
-            if (moved) {
-                if (t == 0) {
-                    t = 1;
-                    ++g.visited;
-                    explored = true;
-                } else if (t > 0) {
-                    t += 1;
-                }
-            }
-            t += 1;
-            if (t > 127) t = 127;
-        }
-        win[10] = (win[10] & 0xff00ffffu) | ((uint32_t)(t & 0xff) << 16);
-        map[cb + z] = (int8_t)t;
-        center = t;
-    }
-
-    // ---- in-window ray cells: patch + store ----
-    // (column index c = (dx+2)*4 + (dy+2), byte = dz+2)
-    auto patch_win = [&](int c, int byte, int r, int s) {
-        const uint32_t b = (win[c] >> (8 * byte)) & 0xffu;
-        if (s <= nf[r] || (wh[r] && s == nf[r] + 1)) {
-            const uint32_t nb = patch_byte(b, s, nf[r], wh[r]);
-            if (nb != b) {
-                win[c] = (win[c] & ~(0xffu << (8 * byte))) | (nb << (8 * byte));
-                uint32_t a;
-                switch (r) {
-                    case 0: a = boff(x + s, y, z, nby, ph); break;
-                    case 1: a = boff(x - s, y, z, nby, ph); break;
-                    case 2: a = boff(x, y + s, z, nby, ph); break;
-                    case 3: a = boff(x, y - s, z, nby, ph); break;
-                    case 4: a = cb + z + s; break;
-                    default: a = cb + z - s; break;
-                }
-                map[a] = (int8_t)nb;
-            }
-        }
-    };
-    patch_win(14, 2, 0, 1);
-    patch_win(6, 2, 1, 1);
-    patch_win(2, 2, 1, 2);
-    patch_win(11, 2, 2, 1);
-    patch_win(9, 2, 3, 1);
-    patch_win(8, 2, 3, 2);
-    patch_win(10, 3, 4, 1);
-    patch_win(10, 1, 5, 1);
-    patch_win(10, 0, 5, 2);
 
     g.near_wall = g.near_wall || near;
-    g.cid = nf[5];
+    g.cid = ry.nf[5];
     g.move_mask = mm;
 
-    // ---- observation row (80 f32, 20 x 16-B stores) ----
+    // ---- observation row: lane q writes obs[16i+4q..+3] and tail float4 q ----
     float *obs_row = dst.row;
-    if (dst.select &&
-        (dst.truncated || g.done || (double)g.visited / (double)R.total_free >= p.finish))
-        obs_row = dst.term_row;
+    if (dst.select && (dst.truncated || g.done || g.visited >= R.finish_visits)) obs_row = dst.term_row;
+    if (p.ablate & 4u) obs_row = nullptr;
     if (obs_row) {
         float4 *o4 = reinterpret_cast<float4 *>(obs_row);
 #pragma unroll
-        for (int c = 0; c < 16; ++c) {
-            float v[4];
-#pragma unroll
-            for (int b = 0; b < 4; ++b) {
-                int cv = (int)(int8_t)((win[c] >> (8 * b)) & 0xffu);
-                cv = (cv > 20 ? 20 : cv) + 2;           // clip(-2, 20) + 2   (:274-275)
-                v[b] = lut[cv];
-            }
-            o4[c] = make_float4(v[0], v[1], v[2], v[3]);
+        for (int i = 0; i < 4; ++i) {
+            float4 v;
+            v.x = tab[col_byte<PH>(col[i], z - 2)];
+            v.y = tab[col_byte<PH>(col[i], z - 1)];
+            v.z = tab[col_byte<PH>(col[i], z)];
+            v.w = tab[col_byte<PH>(col[i], z + 1)];
+            o4[4 * i + q] = v;
         }
-        float t[16];
-#pragma unroll
-        for (int k = 0; k < 16; ++k) t[k] = 0.0f;
-#pragma unroll
-        for (int k = 0; k < 4; ++k) t[k] = (g.facing == k) ? 1.0f : 0.0f;   // (:279-280)
-        t[4] = (float)((double)g.last_action / 5.0);                   // (:284)
-        t[5] = g.was_near_wall ? 1.0f : 0.0f;                          // (:285)
-        t[6] = g.last_bump ? 1.0f : 0.0f;                              // (:286)
-        t[7] = (float)((double)g.cid / (double)L);                     // (:287)
-        t[8] = (float)((double)g.visited / (double)R.total_free);      // (:291)
-#pragma unroll
-        for (int c = 0; c < 4; ++c) o4[16 + c] = make_float4(t[4 * c], t[4 * c + 1], t[4 * c + 2], t[4 * c + 3]);
+        float4 tv;
+        if (q == 0) {
+            tv = make_float4(g.facing == 0 ? 1.0f : 0.0f, g.facing == 1 ? 1.0f : 0.0f,
+                             g.facing == 2 ? 1.0f : 0.0f, g.facing == 3 ? 1.0f : 0.0f);       // (:279-280)
+        } else if (q == 1) {
+            tv = make_float4(tab[TAB_ACTION + g.last_action], g.was_near_wall ? 1.0f : 0.0f,
+                             g.last_bump ? 1.0f : 0.0f, tab[TAB_CID + g.cid]);                // (:284-287)
+        } else if (q == 2) {
+            tv = make_float4((float)((double)g.visited / (double)R.total_free), 0.f, 0.f, 0.f);  // (:291)
+        } else {
+            tv = make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+        o4[16 + q] = tv;
     }
-    return center;
+    return t;
+}
+
+// load_room's draws (CubicEnv.py:407, :462-466) for seed: returns
+// x | y<<8 | z<<16 | room<<24.  Out of line: the ~1.2k-iteration MT seeding
+// is rare and keeps its registers away from the step loop.
+__device__ __noinline__ uint32_t reset_draw(const Params &p, uint32_t seed) {
+    MtStream mt;
+    mt.seed = seed;
+    mt.used = 0;
+    mt.err = p.err;
+    mt_first_outputs(seed, mt.buf);
+    const int room = p.use_room_draw ? (int)mt.below((uint32_t)p.n_rooms) : 0;
+    const Room R = load_room(p, room);
+    uint32_t s;
+    if (R.fixed_start >= 0) s = (uint32_t)R.fixed_start;
+    else s = p.starts[R.start_off + mt.below(R.total_free)];
+    const int sx = s & 0xff, sy = (s >> 8) & 0xff, sz = (s >> 16) & 0xff;
+    const uint2 rec = p.rays[R.ray_off + (uint32_t)((sx * R.D + sy) * R.H + sz)];
+    if ((rec.y >> 16) & 1u) s = p.starts[R.start_off + mt.below(R.total_free)];   // start in a wall
+    return (s & 0xffffffu) | ((uint32_t)room << 24);
 }
 
 // ----------------------------------------------------------------------------
-// reset (envs/CubicEnv.py:77-108): draws for lanes with `need`, then the
-// whole wave clears each resetting agent's bricks (1 KiB per instruction),
-// then each resetting lane senses from its start cell.
+// reset (envs/CubicEnv.py:77-108) for the groups with `need`: draws, clear of
+// the new room's bricks by the 4 lanes, then sensing from the start cell.
 // ----------------------------------------------------------------------------
-template <int LMAX>
-__device__ __forceinline__ void wave_reset(const Params &p, int8_t *belief_base, int agent, bool need, uint32_t seed,
-                                           Agent &g, Room &R, const float *lut, float *obs_row) {
+template <int PH, int LMAX>
+__device__ __forceinline__ void group_reset(const Params &p, int8_t *map, bool need, uint32_t seed, Agent &g,
+                                            Room &R, const float *tab, float *obs_row, int q) {
     if (need) {
-        MtStream mt;
-        mt.seed = seed;
-        mt.used = 0;
-        mt.err = p.err;
-        mt_first_outputs(seed, mt.buf);
-        const int room = p.use_room_draw ? (int)mt.below((uint32_t)p.n_rooms) : 0;   // :407
+        const uint32_t drawn = reset_draw(p, seed);
+        const int room = (int)(drawn >> 24);
         R = load_room(p, room);
-        int sx, sy, sz;
-        if (R.fixed_start >= 0) {
-            sx = R.fixed_start & 0xff;
-            sy = (R.fixed_start >> 8) & 0xff;
-            sz = (R.fixed_start >> 16) & 0xff;
-        } else {
-            const uint32_t s = p.starts[R.start_off + mt.below(R.total_free)];      // :462
-            sx = s & 0xff;
-            sy = (s >> 8) & 0xff;
-            sz = (s >> 16) & 0xff;
-        }
-        const uint2 rec = p.rays[R.ray_off + (uint32_t)((sx * R.D + sy) * R.H + sz)];
-        if ((rec.y >> 16) & 1u) {                                                   // :464-466
-            const uint32_t s = p.starts[R.start_off + mt.below(R.total_free)];
-            sx = s & 0xff;
-            sy = (s >> 8) & 0xff;
-            sz = (s >> 16) & 0xff;
-        }
+        const int sx = drawn & 0xff, sy = (drawn >> 8) & 0xff, sz = (drawn >> 16) & 0xff;
         g.room = room;
         g.x = sx;
         g.y = sy;
@@ -573,69 +670,74 @@ __device__ __forceinline__ void wave_reset(const Params &p, int8_t *belief_base,
         g.bumps = 0;
         g.cid = 0;
         g.move_mask = 0;
-    }
-    // cooperative clear of the new room's bricks to -1 (0xff)
-    uint64_t m = __ballot(need);
-    const int lane = threadIdx.x & 63;
-    const uint32_t brick16 = (uint32_t)p.ph;  // 16-byte chunks per brick
-    while (m) {
-        const int l = __ffsll((unsigned long long)m) - 1;
-        m &= m - 1;
-        const int a = __shfl(agent, l);
-        const int nbx = __shfl(R.nbx, l);
-        const int nbyr = __shfl(R.nby, l);
-        uint4 *base = reinterpret_cast<uint4 *>(belief_base + (size_t)a * p.map_bytes);
-        const uint32_t total = (uint32_t)(nbx * nbyr) * brick16;
-        for (uint32_t c = lane; c < total; c += 64) {
-            const uint32_t brick = c / brick16, w = c - brick * brick16;
-            const uint32_t bx = brick / (uint32_t)nbyr, by = brick - bx * (uint32_t)nbyr;
-            base[(bx * (uint32_t)p.nby + by) * brick16 + w] = make_uint4(~0u, ~0u, ~0u, ~0u);
+        // clear the room's bricks to "unknown" (0x00), 16 B per lane per store
+        uint4 *base = reinterpret_cast<uint4 *>(map);
+        const uint32_t per_brick = (uint32_t)PH;          // 16-byte chunks per brick
+        const uint32_t total = (uint32_t)(R.nbx * R.nby) * per_brick;
+        for (uint32_t c = (uint32_t)q; c < total; c += GROUP) {
+            const uint32_t brick = c / per_brick, w = c - brick * per_brick;
+            const uint32_t bx = brick / (uint32_t)R.nby, by = brick - bx * (uint32_t)R.nby;
+            base[(bx * (uint32_t)p.nby + by) * per_brick + w] = make_uint4(0u, 0u, 0u, 0u);
         }
-        (void)nbx;
+        // and both marked-bit planes
+        uint4 *pl = reinterpret_cast<uint4 *>(map + p.xp_off);
+        const uint32_t pchunks = (p.agent_bytes - p.xp_off) / 16u;
+        for (uint32_t c = (uint32_t)q; c < pchunks; c += GROUP) pl[c] = make_uint4(0u, 0u, 0u, 0u);
     }
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
     if (need) {
         bool explored = false;
-        sense_observe<LMAX, true>(p, belief_base + (size_t)agent * p.map_bytes, g, R, false, explored, lut,
-                                  ObsDst{obs_row, nullptr, false, false});
+        sense_observe<PH, LMAX, true>(p, map, g, R, false, explored, tab, ObsDst{obs_row, nullptr, false, false}, q);
     }
 }
 
 // ----------------------------------------------------------------------------
-// the step kernel: one lane per agent, K fused steps, SB3 auto-reset
+// the step kernel: 4 lanes per agent, K fused steps, SB3 auto-reset
 // ----------------------------------------------------------------------------
-template <int LMAX, bool RESET_ONLY>
+template <int PH, int LMAX, bool RESET_ONLY>
 __global__ __launch_bounds__(256) void env_kernel(Params p) {
-    __shared__ float lut[32];
-    if (threadIdx.x < 32) lut[threadIdx.x] = p.lut[threadIdx.x];
+    __shared__ float tab[TAB_SIZE];
+    for (int k = threadIdx.x; k < TAB_SIZE; k += blockDim.x) tab[k] = p.lut[k];
     __syncthreads();
 
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    const int q = threadIdx.x & (GROUP - 1);
+    const int i = (int)((blockIdx.x * blockDim.x + threadIdx.x) / GROUP);
     const bool active = i < p.N;
     const int ai = active ? i : 0;
     Agent g = unpack(p.hot[ai]);
     Room R = load_room(p, active ? g.room : 0);
     uint32_t next_seed = p.next_seed[ai];
-    int8_t *map = p.belief + (size_t)ai * p.map_bytes;
+    int8_t *map = p.belief + (size_t)ai * p.agent_bytes;
 
     if (RESET_ONLY) {
         const bool need = active && (p.mask == nullptr || p.mask[i] != 0);
         const uint32_t seed = need ? (uint32_t)p.seeds[i] : 0u;
-        wave_reset<LMAX>(p, p.belief, ai, need, seed, g, R, lut, need ? p.obs + (size_t)i * VN_OBS_DIM : nullptr);
-        if (need) {
+        group_reset<PH, LMAX>(p, map, need, seed, g, R, tab, need ? p.obs + (size_t)i * VN_OBS_DIM : nullptr, q);
+        if (need && q == 0) {
             p.hot[i] = pack(g);
             p.next_seed[i] = seed + p.seed_stride;
         }
         return;
     }
 
+    uint32_t pw0 = 0, pw1 = 0, pw2 = 0, pw3 = 0;   // Philox words of the current 4-step block
     for (int k = 0; k < p.K; ++k) {
         bool finished = false;
         const size_t row = (size_t)k * (size_t)p.N + (size_t)i;
+        const uint64_t tt = p.t0 + (uint64_t)k;
+        if (!p.actions && (k == 0 || (tt & 3u) == 0)) {
+            uint4 o = philox4x32_10(p.policy_seed, p.gid_base + (uint64_t)ai, tt >> 2);
+            pw0 = o.x; pw1 = o.y; pw2 = o.z; pw3 = o.w;
+        }
         if (active) {
-            const int a = p.actions ? p.actions[row]
-                                    : philox_action(p.policy_seed, p.gid_base + (uint64_t)i, p.t0 + (uint64_t)k);
-            if (p.actions_out) p.actions_out[row] = a;
+            int a;
+            if (p.actions) {
+                a = p.actions[row];
+            } else {
+                const uint32_t w = (tt & 3u) == 0 ? pw0 : (tt & 3u) == 1 ? pw1 : (tt & 3u) == 2 ? pw2 : pw3;
+                a = (int)__umulhi(w, 6u);
+            }
+            if (p.actions_out && q == 0) p.actions_out[row] = a;
 
             // step() prologue (:111-116)
             if (g.near_wall) {
@@ -648,10 +750,9 @@ __global__ __launch_bounds__(256) void env_kernel(Params p) {
             // do_action (:134-166): relative move table by facing -> axis dir
             int dir;
             if (a < 4) {
-                // rows: fwd, right, back, left; cols: facing N,E,S,W
-                // dirs 0 +x, 1 -x, 2 +y, 3 -y
-                constexpr uint32_t kDir = (2u << 0) | (0u << 2) | (3u << 4) | (1u << 6)      // fwd
-                                          | (0u << 8) | (3u << 10) | (1u << 12) | (2u << 14)  // right
+                // rows fwd, right, back, left; cols facing N,E,S,W; dirs 0 +x, 1 -x, 2 +y, 3 -y
+                constexpr uint32_t kDir = (2u << 0) | (0u << 2) | (3u << 4) | (1u << 6)       // fwd
+                                          | (0u << 8) | (3u << 10) | (1u << 12) | (2u << 14)   // right
                                           | (3u << 16) | (1u << 18) | (2u << 20) | (0u << 22)  // back
                                           | (1u << 24) | (2u << 26) | (0u << 28) | (3u << 30); // left
                 dir = (int)((kDir >> (2 * (a * 4 + g.facing))) & 3u);
@@ -668,16 +769,15 @@ __global__ __launch_bounds__(256) void env_kernel(Params p) {
 
             bool explored = false;
             const ObsDst dst{p.obs + row * VN_OBS_DIM,
-                             p.terminal_obs ? p.terminal_obs + row * VN_OBS_DIM : nullptr,
-                             p.autoreset != 0, truncated};
-            const int vv = sense_observe<LMAX, false>(p, map, g, R, moved, explored, lut, dst);
+                             p.terminal_obs ? p.terminal_obs + row * VN_OBS_DIM : nullptr, p.autoreset != 0,
+                             truncated};
+            const int vv = sense_observe<PH, LMAX, false>(p, map, g, R, moved, explored, tab, dst, q);
 
             // compute_reward (:169-224), f64 in the reference's order
             double r = -0.05;
             const double pen = (double)vv * 0.02;
             r -= (0.5 < pen) ? 0.5 : pen;
-            const bool bumped = !moved;
-            if (bumped) {
+            if (!moved) {
                 g.last_bump = true;
                 if (g.bumps < 0x3ffffffu) ++g.bumps;
                 r += p.crash_penalty;
@@ -691,29 +791,29 @@ __global__ __launch_bounds__(256) void env_kernel(Params p) {
                 if (g.last_action == 2 && a == 2) r -= 0.5;
             }
             if (explored) r += 1.0;
-            const double pct2 = (double)g.visited / (double)R.total_free;
-            if (pct2 >= p.finish) {
+            if (g.visited >= R.finish_visits) {            // visited / total >= 0.84 (:212-215)
                 g.done = true;
                 r += 100.0;
             }
             if (truncated) r += -5.0;
             g.last_action = a;
 
-            if (p.reward) p.reward[row] = (float)r;
-            if (p.reward64) p.reward64[row] = r;
-            if (p.term) p.term[row] = g.done ? 1 : 0;
-            if (p.trunc) p.trunc[row] = truncated ? 1 : 0;
+            if (q == 0) {
+                if (p.reward) p.reward[row] = (float)r;
+                if (p.reward64) p.reward64[row] = r;
+                if (p.term) p.term[row] = g.done ? 1 : 0;
+                if (p.trunc) p.trunc[row] = truncated ? 1 : 0;
+            }
             finished = g.done || truncated;
         }
         const bool need = p.autoreset && finished;
         if (__ballot(need)) {
             const uint32_t seed = next_seed;
-            wave_reset<LMAX>(p, p.belief, ai, need, seed, g, R, lut,
-                             need ? p.obs + row * VN_OBS_DIM : nullptr);
+            group_reset<PH, LMAX>(p, map, need, seed, g, R, tab, need ? p.obs + row * VN_OBS_DIM : nullptr, q);
             if (need) next_seed = seed + p.seed_stride;
         }
     }
-    if (active) {
+    if (active && q == 0) {
         p.hot[i] = pack(g);
         p.next_seed[i] = next_seed;
     }
@@ -744,7 +844,11 @@ __global__ void export_belief_kernel(Params p, int8_t *out, int pw, int pd) {
     const Agent g = unpack(p.hot[i]);
     const Room R = load_room(p, g.room);
     int8_t v = -128;
-    if (x < R.W && y < R.D && z < R.H) v = p.belief[(size_t)i * p.map_bytes + boff(x, y, z, p.nby, p.ph)];
+    if (x < R.W && y < R.D && z < R.H) {
+        const uint32_t off = (uint32_t)((((((x >> 2) * p.nby + (y >> 2)) << 4) + ((x & 3) << 2) + (y & 3)) * p.ph) + z);
+        const uint32_t b = (uint8_t)p.belief[(size_t)i * p.agent_bytes + off];
+        v = (b & KNOWN) ? ((b & 0x40u) ? (int8_t)-2 : (int8_t)(b & 0x3fu)) : (int8_t)-1;
+    }
     out[gid] = v;
 }
 
@@ -791,7 +895,8 @@ struct VnEnv {
     VnConfig cfg{};
     int n_rooms = 0;
     int pw = 0, pd = 0, ph = 0, nbx = 0, nby = 0;
-    uint32_t map_bytes = 0;
+    uint32_t map_bytes = 0, agent_bytes = 0, xp_off = 0, yp_off = 0;
+    int nwx = 1, nwy = 1;
     size_t device_bytes = 0;
     std::vector<uint32_t> total_free;
     uint4 *d_rooms = nullptr;
@@ -802,6 +907,7 @@ struct VnEnv {
     uint32_t *d_seed = nullptr;
     int8_t *d_belief = nullptr;
     int32_t *d_err = nullptr;
+    uint32_t ablate = 0;
 };
 
 namespace {
@@ -847,6 +953,11 @@ Params base_params(VnEnv *e) {
     p.nby = e->nby;
     p.ph = e->ph;
     p.map_bytes = e->map_bytes;
+    p.agent_bytes = e->agent_bytes;
+    p.xp_off = e->xp_off;
+    p.yp_off = e->yp_off;
+    p.nwx = e->nwx;
+    p.nwy = e->nwy;
     p.n_rooms = e->n_rooms;
     p.use_room_draw = e->cfg.use_room_draw;
     p.autoreset = e->cfg.autoreset;
@@ -855,24 +966,32 @@ Params base_params(VnEnv *e) {
     p.finish = e->cfg.finish_percentage;
     p.gid_base = (uint64_t)e->cfg.agent_id_base;
     p.K = 1;
+    p.ablate = e->ablate;
     return p;
+}
+
+template <int PH, bool RESET_ONLY>
+int launch_ph(int L, dim3 grid, dim3 block, hipStream_t s, const Params &p) {
+    if (L <= 4)
+        hipLaunchKernelGGL((env_kernel<PH, 4, RESET_ONLY>), grid, block, 0, s, p);
+    else if (L <= 8)
+        hipLaunchKernelGGL((env_kernel<PH, 8, RESET_ONLY>), grid, block, 0, s, p);
+    else if (L <= 10)
+        hipLaunchKernelGGL((env_kernel<PH, 10, RESET_ONLY>), grid, block, 0, s, p);
+    else
+        hipLaunchKernelGGL((env_kernel<PH, 16, RESET_ONLY>), grid, block, 0, s, p);
+    VN_HIP(hipGetLastError());
+    return VN_OK;
 }
 
 template <bool RESET_ONLY>
 int launch_env(VnEnv *e, const Params &p, hipStream_t s) {
     const dim3 block(256);
-    const dim3 grid((unsigned)((e->N + 255) / 256));
+    const dim3 grid((unsigned)(((size_t)e->N * GROUP + 255) / 256));
     const int L = e->cfg.local_map_length;
-    if (L <= 4)
-        hipLaunchKernelGGL((env_kernel<4, RESET_ONLY>), grid, block, 0, s, p);
-    else if (L <= 8)
-        hipLaunchKernelGGL((env_kernel<8, RESET_ONLY>), grid, block, 0, s, p);
-    else if (L <= 12)
-        hipLaunchKernelGGL((env_kernel<12, RESET_ONLY>), grid, block, 0, s, p);
-    else
-        hipLaunchKernelGGL((env_kernel<16, RESET_ONLY>), grid, block, 0, s, p);
-    VN_HIP(hipGetLastError());
-    return VN_OK;
+    if (e->ph == 8) return launch_ph<8, RESET_ONLY>(L, grid, block, s, p);
+    if (e->ph == 16) return launch_ph<16, RESET_ONLY>(L, grid, block, s, p);
+    return launch_ph<32, RESET_ONLY>(L, grid, block, s, p);
 }
 
 void free_env(VnEnv *e) {
@@ -978,6 +1097,13 @@ int vn_create(const VnRoomSet *rooms, int32_t n_agents, const VnConfig *cfg, int
         d[3] = start_off;
         d[4] = (uint32_t)fixed;
         d[5] = (uint32_t)((W + 3) / 4) | ((uint32_t)((D + 3) / 4) << 16);
+        {   // done <=> visited / total >= finish in f64 (CubicEnv.py:212-213); monotone in visited
+            const double fin = cfg->finish_percentage == 0.0 ? 0.84 : cfg->finish_percentage;
+            uint32_t v = 0;
+            const uint32_t vmax = (uint32_t)W * D * H + 1;
+            while (v < vmax && !((double)v / (double)tf >= fin)) ++v;
+            d[6] = v;
+        }
         maxW = W > maxW ? W : maxW;
         maxD = D > maxD ? D : maxD;
         maxH = H > maxH ? H : maxH;
@@ -993,12 +1119,20 @@ int vn_create(const VnRoomSet *rooms, int32_t n_agents, const VnConfig *cfg, int
     if (e->cfg.seed_stride == 0) e->cfg.seed_stride = n_agents;
     e->n_rooms = nr;
     e->total_free = total_free;
+    // timing diagnostics only; every ablation keeps all addresses inside the
+    // agent's room (bits: 1 column loads, 2 ray slots, 4 obs stores, 8 column stores)
+    if (const char *ab = getenv("VOXNAV_ABLATE")) e->ablate = (uint32_t)strtoul(ab, nullptr, 0) & 0xfu;
     e->nbx = (maxW + 3) / 4;
     e->nby = (maxD + 3) / 4;
     e->pw = e->nbx * 4;
     e->pd = e->nby * 4;
-    e->ph = (maxH + 3) & ~3;
+    e->ph = maxH <= 8 ? 8 : maxH <= 16 ? 16 : 32;   // whole column = one 8/16/32-byte access
     e->map_bytes = (uint32_t)(e->nbx * e->nby * 16 * e->ph);
+    e->nwx = (e->pw + 63) / 64;
+    e->nwy = (e->pd + 63) / 64;
+    e->xp_off = e->map_bytes;                                        // rows (y, z): pd * ph * nwx words
+    e->yp_off = e->xp_off + (uint32_t)(e->pd * e->ph * e->nwx * 8);  // rows (x, z): pw * ph * nwy words
+    e->agent_bytes = (e->yp_off + (uint32_t)(e->pw * e->ph * e->nwy * 8) + 15u) & ~15u;
 
     DeviceGuard dg(device);
     int rc = ensure_mt_table(device);
@@ -1006,13 +1140,21 @@ int vn_create(const VnRoomSet *rooms, int32_t n_agents, const VnConfig *cfg, int
         delete e;
         return rc;
     }
-    // f32 obs table: (v + 2) / 22 for v = -2..20, IEEE f32 division on the host
-    float lut[32];
-    for (int k = 0; k < 32; ++k) {
-        volatile float num = (float)(k < 23 ? k : 22);
-        lut[k] = num / 22.0f;
+    // LDS table (TAB_SIZE floats): obs value of every belief byte (decode,
+    // clip to [-2, 20], (v + 2) / 22 in IEEE f32 -- :273-275), f32(a / 5.0)
+    // (:284) and f32(c / L) (:287), all computed on the host.
+    float lut[TAB_SIZE];
+    for (int k = 0; k < TAB_SIZE; ++k) lut[k] = 0.0f;
+    for (int b = 0; b < 256; ++b) {
+        int v = (b & 0x80) ? ((b & 0x40) ? -2 : (b & 0x3f)) : -1;
+        if (v > 20) v = 20;
+        volatile float num = (float)(v + 2);
+        lut[b] = num / 22.0f;
     }
-    const size_t belief_bytes = (size_t)e->map_bytes * (size_t)n_agents;
+    for (int a = 0; a < 6; ++a) lut[TAB_ACTION + a] = (float)((double)a / 5.0);
+    for (int c = 0; c <= cfg->local_map_length; ++c)
+        lut[TAB_CID + c] = (float)((double)c / (double)cfg->local_map_length);
+    const size_t belief_bytes = (size_t)e->agent_bytes * (size_t)n_agents;
 #define VN_ALLOC(ptr, bytes)                                                                    \
     do {                                                                                        \
         hipError_t e_ = hipMalloc((void **)&(ptr), (bytes));                                    \
@@ -1039,7 +1181,7 @@ int vn_create(const VnRoomSet *rooms, int32_t n_agents, const VnConfig *cfg, int
     if (he == hipSuccess) he = hipMemcpy(e->d_lut, lut, sizeof(lut), hipMemcpyHostToDevice);
     if (he == hipSuccess) he = hipMemset(e->d_hot, 0, (size_t)n_agents * sizeof(uint4));
     if (he == hipSuccess) he = hipMemset(e->d_seed, 0, (size_t)n_agents * sizeof(uint32_t));
-    if (he == hipSuccess) he = hipMemset(e->d_belief, 0xff, belief_bytes);
+    if (he == hipSuccess) he = hipMemset(e->d_belief, 0, belief_bytes);   // 0x00 = unknown
     if (he == hipSuccess) he = hipMemset(e->d_err, 0, sizeof(int32_t));
     if (he == hipSuccess) he = hipDeviceSynchronize();
     if (he != hipSuccess) {
@@ -1066,7 +1208,7 @@ int vn_get_info(const VnEnv *env, VnInfo *info) {
     info->pad_w = env->pw;
     info->pad_d = env->pd;
     info->pad_h = env->ph;
-    info->belief_bytes_per_agent = env->map_bytes;
+    info->belief_bytes_per_agent = env->agent_bytes;
     info->device_bytes = (int64_t)env->device_bytes;
     return VN_OK;
 }

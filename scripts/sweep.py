@@ -1,0 +1,79 @@
+#!/usr/bin/env python3
+"""Throughput sweep of the env kernel over launch shapes (one process,
+interleaved rounds so variants see the same device state)."""
+import argparse
+import json
+import sys
+import time
+from pathlib import Path
+
+REPO = Path(__file__).resolve().parent.parent
+sys.path.insert(0, str(REPO / "3d-navigation-reinforcement-learning_amd"))
+
+import torch  # noqa: E402
+
+from voxnav.env import BatchedGridEnv, Rollout  # noqa: E402
+from voxnav.rooms import box_room, load_archive_set, single_room_set  # noqa: E402
+
+
+def make(n, room, L, ablate=0):
+    import os
+    os.environ["VOXNAV_ABLATE"] = str(ablate)
+    rs = load_archive_set(room) if room.startswith("P") else single_room_set(box_room(*map(int, room.split("x"))))
+    e = BatchedGridEnv(num_agents=n, rooms=rs, local_map_length=L, autoreset=True, device="cuda:0")
+    e.reset(seed=42)
+    os.environ.pop("VOXNAV_ABLATE", None)
+    return e
+
+
+def timed(env, F, steps):
+    n = env.num_agents
+    out = Rollout(torch.empty((F, n, 80), device="cuda:0"), torch.empty((F, n), device="cuda:0"),
+                  torch.empty((F, n), dtype=torch.uint8, device="cuda:0"),
+                  torch.empty((F, n), dtype=torch.uint8, device="cuda:0"), None)
+    for _ in range(3):
+        env.step_random(F, out=out)
+    launches = max(1, steps // F)
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    s.record()
+    for _ in range(launches):
+        env.step_random(F, out=out)
+    e.record()
+    torch.cuda.synchronize()
+    wall = time.perf_counter() - t0
+    gpu = s.elapsed_time(e) * 1e-3
+    return n * launches * F / wall, n * launches * F / gpu
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--configs", default="65536:32x32x8:10:1,65536:32x32x8:10:16,262144:32x32x8:10:1")
+    ap.add_argument("--steps", type=int, default=128)
+    ap.add_argument("--rounds", type=int, default=3)
+    args = ap.parse_args()
+    cfgs = []
+    for c in args.configs.split(","):
+        f = c.split(":")
+        n, room, L, F = f[:4]
+        ab = int(f[4], 0) if len(f) > 4 else 0
+        cfgs.append((int(n), room, int(L), int(F), ab))
+    envs = {}
+    for n, room, L, F, ab in cfgs:
+        if (n, room, L, ab) not in envs:
+            envs[(n, room, L, ab)] = make(n, room, L, ab)
+    res = {c: [] for c in cfgs}
+    for _ in range(args.rounds):
+        for c in cfgs:
+            n, room, L, F, ab = c
+            res[c].append(timed(envs[(n, room, L, ab)], F, args.steps))
+    for c, v in res.items():
+        wall = max(x[0] for x in v)
+        gpu = max(x[1] for x in v)
+        print(json.dumps({"agents": c[0], "room": c[1], "L": c[2], "fuse": c[3], "ablate": c[4],
+                          "Gsteps_wall": round(wall / 1e9, 3), "Gsteps_gpu": round(gpu / 1e9, 3)}))
+
+
+if __name__ == "__main__":
+    main()
