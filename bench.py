@@ -48,7 +48,9 @@ def parse():
     ap.add_argument("--agents", type=int, default=65536, help="agents per GPU")
     ap.add_argument("--room", default="32x32x8", help="WxDxH of the walled-box room")
     ap.add_argument("--L", type=int, default=10, help="local_map_length")
-    ap.add_argument("--fuse", type=int, default=1, help="env steps per kernel launch")
+    ap.add_argument("--fuse", type=int, default=16, help="env steps per kernel launch (headline)")
+    ap.add_argument("--single-step-check", type=int, default=1,
+                    help="also time the drop-in one-step-per-launch call (vn_step_random k=1)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline sample budget (0 = skip)")
     ap.add_argument("--json-out", default=None)
     return ap.parse_args()
@@ -107,37 +109,41 @@ def main():
                          autoreset=True, device=dev, agent_id_base=rank * N, seed_stride=N * world)
     env.reset(seed=42)
     from voxnav.env import Rollout
-    out = Rollout(torch.empty((F, N, 80), dtype=torch.float32, device=dev),
-                  torch.empty((F, N), dtype=torch.float32, device=dev),
-                  torch.empty((F, N), dtype=torch.uint8, device=dev),
-                  torch.empty((F, N), dtype=torch.uint8, device=dev), None)
-    launches_w = max(1, args.warmup // F)
-    launches = max(1, args.steps // F)
-    steps_timed = launches * F
-    for _ in range(launches_w):
-        env.step_random(F, policy_seed=42, out=out)
-    stream = torch.cuda.current_stream(dev)
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(launches)]
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize(dev)
-    t0 = time.perf_counter()
-    for i in range(launches):
-        ev[i][0].record(stream)
-        env.step_random(F, policy_seed=42, out=out)
-        ev[i][1].record(stream)
-    torch.cuda.synchronize(dev)
-    if world > 1:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
-    kern_ms = sum(a.elapsed_time(b) for a, b in ev) / launches
-    if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-        k = torch.tensor([kern_ms], dtype=torch.float64, device=dev)
-        dist.all_reduce(k, op=dist.ReduceOp.MAX)
-        kern_ms = float(k.item())
+    def run(F, steps, warmup):
+        out = Rollout(torch.empty((F, N, 80), dtype=torch.float32, device=dev),
+                      torch.empty((F, N), dtype=torch.float32, device=dev),
+                      torch.empty((F, N), dtype=torch.uint8, device=dev),
+                      torch.empty((F, N), dtype=torch.uint8, device=dev), None)
+        launches_w = max(1, warmup // F)
+        launches = max(1, steps // F)
+        for _ in range(launches_w):
+            env.step_random(F, policy_seed=42, out=out)
+        stream = torch.cuda.current_stream(dev)
+        ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(launches)]
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        for i in range(launches):
+            ev[i][0].record(stream)
+            env.step_random(F, policy_seed=42, out=out)
+            ev[i][1].record(stream)
+        torch.cuda.synchronize(dev)
+        if world > 1:
+            dist.barrier()
+        elapsed = time.perf_counter() - t0
+        kern_ms = sum(a.elapsed_time(b) for a, b in ev) / launches
+        if world > 1:
+            t = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device=dev)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            elapsed, kern_ms = float(t[0].item()), float(t[1].item())
+        return out, launches_w * F, launches * F, elapsed, kern_ms
+
+    single = None
+    if args.single_step_check and F != 1:
+        _, _, st1, el1, km1 = run(1, min(args.steps, 100), 10)
+        single = {"value": round(N * world * st1 / el1, 1), "steps": st1, "kernel_avg_us": round(km1 * 1e3, 3)}
+    out, warm_steps, steps_timed, elapsed, kern_ms = run(F, args.steps, args.warmup)
 
     # sanity: the trajectory buffer holds real observations
     assert torch.isfinite(out.obs).all().item()
@@ -148,7 +154,7 @@ def main():
     achieved = bstep * N * F / (kern_ms * 1e-3) / 1e9
     roof = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": None,
-            "kernel": "env_kernel<12,false>", "kernel_avg_us": round(kern_ms * 1e3, 3),
+            "kernel": "env_kernel<PH=8,LMAX=10,false>", "kernel_avg_us": round(kern_ms * 1e3, 3),
             "algorithmic_bytes_per_env_step": bstep, "env_steps_per_launch": N * F}
     prof = REPO / "profiles" / "pmc_traffic.json"
     if prof.exists():
@@ -164,7 +170,7 @@ def main():
     if rank == 0:
         rec = {
             "metric": METRIC, "value": round(value, 1), "unit": "env-steps/s", "n_gpus": world,
-            "steps": steps_timed, "warmup": launches_w * F, "ms_per_step": round(elapsed * 1e3 / steps_timed, 5),
+            "steps": steps_timed, "warmup": warm_steps, "ms_per_step": round(elapsed * 1e3 / steps_timed, 5),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "int8",
             "data": "synthetic (walled-box room in the reference room-file grammar; Philox uniform random policy)",
             "config": {"workload": f"C3 env step: {N} agents/GPU, {W}x{D}x{H} room, L={args.L}, "
@@ -173,6 +179,8 @@ def main():
                        "steps_per_launch": F, "parallelism": f"agent-sharded x{world} (no collective in the step)"},
             "roofline": roof,
         }
+        if single is not None:
+            rec["drop_in_single_step"] = single   # vn_step-shaped call: one env step per launch
         if world == 1 and args.cpu_seconds > 0:
             rec["cpu_baseline"] = cpu_baseline((W, D, H), args.L, args.cpu_seconds)
         line = json.dumps(rec)

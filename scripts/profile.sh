@@ -1,24 +1,28 @@
 #!/bin/bash
-# rocprofv3 passes for the bench workload: kernel trace + stats, then PMC
-# counters in their own passes (FETCH_SIZE and WRITE_SIZE do not fit one
-# TCC pass on gfx950).  Outputs under gpurun_out/prof_*; a fault or timeout
-# ends the script.
+# rocprofv3 passes for the bench workload: kernel trace + stats (headline
+# F and the F=1 drop-in call, separately, since both dispatch the same kernel
+# symbol), then PMC counters in their own passes (FETCH_SIZE and WRITE_SIZE do
+# not fit one TCC pass on gfx950).  Outputs under gpurun_out/<TAG>_*; a fault
+# or timeout ends the script.
 set -u
 cd "${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-BARGS=${BENCH_ARGS:-}
+BARGS="${BENCH_ARGS:-} --single-step-check 0"
 TAG=${TAG:-r01}
 step() {
   local name=$1 t=$2; shift 2
-  timeout -k 10 "$t" "$@" > "gpurun_out/$name.log" 2>&1
+  timeout -k 10 "$t" "$@" > "gpurun_out/${TAG}_$name.log" 2>&1
   local rc=$?
-  echo "[$name] rc=$rc"; tail -n 3 "gpurun_out/$name.log"
+  echo "[$name] rc=$rc"; grep -h '"metric"' "gpurun_out/${TAG}_$name.log" | cut -c1-200
   [ $rc -eq 0 ] || exit $rc
 }
-step prof_list 120 rocprofv3 -L
-step prof_trace 400 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_trace_$TAG -o trace --output-format csv -- python3 bench.py --steps 400 --warmup 40 --cpu-seconds 0 $BARGS
-step prof_fetch 400 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/prof_fetch_$TAG -o fetch --output-format csv -- python3 bench.py --steps 20 --warmup 4 --cpu-seconds 0 $BARGS
-step prof_write 400 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/prof_write_$TAG -o write --output-format csv -- python3 bench.py --steps 20 --warmup 4 --cpu-seconds 0 $BARGS
-step prof_l2 400 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum -d gpurun_out/prof_l2_$TAG -o l2 --output-format csv -- python3 bench.py --steps 20 --warmup 4 --cpu-seconds 0 $BARGS
+step trace 400 rocprofv3 --kernel-trace --stats -d gpurun_out/${TAG}_trace -o trace --output-format csv -- python3 bench.py --steps 640 --warmup 64 --cpu-seconds 0 $BARGS
+step trace_f1 400 rocprofv3 --kernel-trace --stats -d gpurun_out/${TAG}_trace_f1 -o trace --output-format csv -- python3 bench.py --steps 200 --warmup 20 --cpu-seconds 0 $BARGS --fuse 1
+step fetch 400 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/${TAG}_fetch -o fetch --output-format csv -- python3 bench.py --steps 64 --warmup 16 --cpu-seconds 0 $BARGS
+step write 400 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/${TAG}_write -o write --output-format csv -- python3 bench.py --steps 64 --warmup 16 --cpu-seconds 0 $BARGS
+step l2 400 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum -d gpurun_out/${TAG}_l2 -o l2 --output-format csv -- python3 bench.py --steps 64 --warmup 16 --cpu-seconds 0 $BARGS
+step sq 400 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_LDS SQ_INSTS_BRANCH SQ_INSTS_SMEM -d gpurun_out/${TAG}_sq -o sq --output-format csv -- python3 bench.py --steps 64 --warmup 16 --cpu-seconds 0 $BARGS
+step sqw 400 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU -d gpurun_out/${TAG}_sqw -o sqw --output-format csv -- python3 bench.py --steps 64 --warmup 16 --cpu-seconds 0 $BARGS
+step tcp 400 rocprofv3 --pmc TCP_TCC_READ_REQ_sum TCP_PENDING_STALL_CYCLES_sum -d gpurun_out/${TAG}_tcp -o tcp --output-format csv -- python3 bench.py --steps 64 --warmup 16 --cpu-seconds 0 $BARGS
 exit 0
