@@ -452,29 +452,163 @@ __device__ __forceinline__ void mark(Col<PH> &c, int z, const Rays &ry, int r, i
     else if (ry.wh[r] && s == ry.nf[r] + 1) col_or<PH>(c, z, WALLB);
 }
 
+// ----------------------------------------------------------------------------
+// Per-agent LDS tile: the 16 window columns, toroidally indexed by
+// slot = (x & 3) << 2 | (y & 3).  The window [x-2, x+1] x [y-2, y+1] covers
+// each residue pair exactly once, so the tile always holds exactly the
+// current window; after a horizontal move the 4 columns entering the window
+// take the slots of the 4 leaving it.  Dirty slots are written back on
+// eviction and at the end of the launch.
+// ----------------------------------------------------------------------------
+template <int PH>
+struct TileGeom {
+    static constexpr int DW = PH / 4;                   // dwords per column
+    static constexpr int STRIDE = 16 * DW + 2;          // dwords per agent tile (+2: bank spread)
+};
+
+template <int PH>
+__device__ __forceinline__ void tile_read(const uint32_t *tile, int slot, Col<PH> &c) {
+    const uint32_t *s = tile + slot * TileGeom<PH>::DW;
+    if constexpr (PH == 8) {
+        const uint2 v = *reinterpret_cast<const uint2 *>(s);
+        c.w[0] = v.x;
+        c.w[1] = v.y;
+    } else {
+#pragma unroll
+        for (int k = 0; k < PH / 4; k += 2) {
+            const uint2 v = *reinterpret_cast<const uint2 *>(s + k);
+            c.w[k] = v.x;
+            c.w[k + 1] = v.y;
+        }
+    }
+}
+
+template <int PH>
+__device__ __forceinline__ void tile_write(uint32_t *tile, int slot, const Col<PH> &c) {
+    uint32_t *s = tile + slot * TileGeom<PH>::DW;
+#pragma unroll
+    for (int k = 0; k < PH / 4; k += 2) *reinterpret_cast<uint2 *>(s + k) = make_uint2(c.w[k], c.w[k + 1]);
+}
+
+__device__ __forceinline__ int tslot(int x, int y) { return ((x & 3) << 2) | (y & 3); }
+
+// OR a 16-bit slot mask over the 4 lanes of the agent group
+__device__ __forceinline__ uint32_t group_or(uint32_t m) {
+    m |= (uint32_t)__shfl_xor((int)m, 1, GROUP);
+    m |= (uint32_t)__shfl_xor((int)m, 2, GROUP);
+    return m;
+}
+
+struct PlaneCache {      // lane 0: x-plane row, lane 1: y-plane row
+    uint64_t w[2];
+    int row, w0;         // cached row index and first word; row < 0: invalid
+};
+
+// Fill the tile from HBM (launch start): lane q loads its 4 window columns.
+template <int PH>
+__device__ __forceinline__ void tile_fill(const Params &p, const int8_t *map, uint32_t *tile, const Agent &g,
+                                          const Room &R, int q) {
+    const int cy = g.y + q - 2;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int cx = g.x + i - 2;
+        Col<PH> c;
+#pragma unroll
+        for (int k = 0; k < PH / 4; ++k) c.w[k] = 0u;
+        if (cx >= 0 && cx < R.W && cy >= 0 && cy < R.D) col_load<PH>(map + boff<PH>(cx, cy, 0, p.nby), c);
+        tile_write<PH>(tile, tslot(cx, cy), c);
+    }
+}
+
+// Write the dirty window columns back to HBM (launch end).
+template <int PH>
+__device__ __forceinline__ void tile_flush(const Params &p, int8_t *map, const uint32_t *tile, const Agent &g,
+                                           const Room &R, uint32_t dirty, int q) {
+    const int cy = g.y + q - 2;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int cx = g.x + i - 2;
+        const int s = tslot(cx, cy);
+        if (((dirty >> s) & 1u) && cx >= 0 && cx < R.W && cy >= 0 && cy < R.D) {
+            Col<PH> c;
+            tile_read<PH>(tile, s, c);
+            col_store<PH>(map + boff<PH>(cx, cy, 0, p.nby), c);
+        }
+    }
+}
+
+// After a horizontal move in axis dir (0 +x, 1 -x, 2 +y, 3 -y) to (x, y):
+// lane q swaps one slot -- writes the leaving column back if dirty, loads
+// the entering one.  Returns the updated dirty mask.
+template <int PH>
+__device__ __forceinline__ uint32_t tile_shift(const Params &p, int8_t *map, uint32_t *tile, int dir, int x, int y,
+                                               const Room &R, uint32_t dirty, int q) {
+    int ex, ey, lx, ly;
+    uint32_t entering;
+    if (dir < 2) {
+        ex = dir == 0 ? x + 1 : x - 2;
+        ey = y + q - 2;
+        lx = dir == 0 ? ex - 4 : ex + 4;
+        ly = ey;
+        entering = 0xfu << ((ex & 3) << 2);
+    } else {
+        ex = x + q - 2;
+        ey = dir == 2 ? y + 1 : y - 2;
+        lx = ex;
+        ly = dir == 2 ? ey - 4 : ey + 4;
+        entering = 0x1111u << (ey & 3);
+    }
+    const int s = tslot(ex, ey);
+    if (((dirty >> s) & 1u) && lx >= 0 && lx < R.W && ly >= 0 && ly < R.D) {
+        Col<PH> old;
+        tile_read<PH>(tile, s, old);
+        col_store<PH>(map + boff<PH>(lx, ly, 0, p.nby), old);
+    }
+    Col<PH> c;
+#pragma unroll
+    for (int k = 0; k < PH / 4; ++k) c.w[k] = 0u;
+    if (ex >= 0 && ex < R.W && ey >= 0 && ey < R.D) col_load<PH>(map + boff<PH>(ex, ey, 0, p.nby), c);
+    tile_write<PH>(tile, s, c);
+    return dirty & ~entering;
+}
+
 // One sensing pass (get_obs :254-312 with _sense_direction :345-397 and the
-// visit update of _mark_visited/do_action :156-166) for this lane's agent.
+// visit update of _mark_visited/do_action :156-166) on the agent's tile.
 // Returns the center cell's visit count after the update.
-template <int PH, int LMAX, bool FRESH>
-__device__ __forceinline__ int sense_observe(const Params &p, int8_t *map, Agent &g, const Room &R, bool moved,
-                                             bool &explored, const float *tab, ObsDst dst, int q) {
+template <int PH, bool FRESH>
+__device__ __forceinline__ int sense_observe(const Params &p, int8_t *map, uint32_t *tile, uint32_t &dirty,
+                                             PlaneCache &pc_, Agent &g, const Room &R, bool moved, bool &explored,
+                                             const float *tab, ObsDst dst, int q) {
     const int x = g.x, y = g.y, z = g.z, nby = p.nby, L = p.L;
     const uint2 rec = p.rays[R.ray_off + (uint32_t)((x * R.D + y) * R.H + z)];
 
-    // ---- this lane's 4 window columns ----
+    // ---- x / y marked-bit plane rows (lane 0: x row (y,z), lane 1: y row (x,z)) ----
+    int pa = 0, pw0 = 0, pwend = 0, pcoord = 0, nfp = 0, nfm = 0;
+    uint64_t pm[2] = {0, 0};
+    uint64_t *prow = nullptr;
+    int rowi = 0;
+    if (q < 2) {
+        const bool xr = q == 0;
+        const int nw = xr ? p.nwx : p.nwy;
+        rowi = (xr ? y : x) * PH + z;
+        prow = reinterpret_cast<uint64_t *>(map + (xr ? p.xp_off : p.yp_off)) + (size_t)rowi * nw;
+        pcoord = xr ? x : y;
+        // the row words needed depend on the span; fetch lazily below
+        (void)nw;
+    }
+
+    // ---- this lane's 4 window columns from the tile ----
     const int cy = y + q - 2;
     const bool yin = cy >= 0 && cy < R.D;
     Col<PH> col[4];
-    bool cin[4];
-    uint32_t coff[4];
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-        const int cx = x + i - 2;
-        cin[i] = yin && cx >= 0 && cx < R.W;
-        coff[i] = boff<PH>(cin[i] ? cx : x, cin[i] ? cy : y, 0, nby);
+        if (FRESH) {
 #pragma unroll
-        for (int k = 0; k < PH / 4; ++k) col[i].w[k] = 0u;
-        if (!FRESH && cin[i] && !(p.ablate & 1u)) col_load<PH>(map + coff[i], col[i]);
+            for (int k = 0; k < PH / 4; ++k) col[i].w[k] = 0u;
+        } else {
+            tile_read<PH>(tile, tslot(x + i - 2, cy), col[i]);
+        }
     }
     Col<PH> orig[4];
 #pragma unroll
@@ -495,40 +629,37 @@ __device__ __forceinline__ int sense_observe(const Params &p, int8_t *map, Agent
         mm |= (n > 0 ? 1u : 0u) << r;
     }
 
-    // ---- x / y rays through the per-axis "marked" bit planes ----
-    // Row (y, z) of the x-plane holds one bit per x: set once an x-ray (or the
-    // agent standing there) has marked the cell.  The agent's own cell is
-    // marked in both planes, so a cell newly marked here is never a visited
-    // cell and its byte can be written blind (0x80 free / 0xC0 first wall).
-    // Lane 0 owns the x row, lane 1 the y row.
-    uint64_t pm[2] = {0, 0}, pn[2] = {0, 0};
-    uint64_t *prow = nullptr;
-    int pa = 0, pw0 = 0, pwend = 0, pc = 0, nfp = 0, nfm = 0;
-    bool whp = false, whm = false;
+    // ---- plane rows: span, cached words, new marks ----
+    uint64_t pn[2] = {0, 0};
     if (q < 2) {
         const bool xr = q == 0;
-        pc = xr ? x : y;                                   // agent coordinate along the axis
+        const int nw = xr ? p.nwx : p.nwy;
         nfp = xr ? ry.nf[0] : ry.nf[2];
         nfm = xr ? ry.nf[1] : ry.nf[3];
-        whp = xr ? ry.wh[0] : ry.wh[2];
-        whm = xr ? ry.wh[1] : ry.wh[3];
-        pa = pc - nfm - (whm ? 1 : 0);                     // marked span [pa, pb]
-        const int pb = pc + nfp + (whp ? 1 : 0);
+        const bool whp = xr ? ry.wh[0] : ry.wh[2];
+        const bool whm = xr ? ry.wh[1] : ry.wh[3];
+        pa = pcoord - nfm - (whm ? 1 : 0);                 // marked span [pa, pb]
+        const int pb = pcoord + nfp + (whp ? 1 : 0);
         pw0 = pa >> 6;
         pwend = pb >> 6;
-        const int nw = xr ? p.nwx : p.nwy;
-        prow = reinterpret_cast<uint64_t *>(map + (xr ? p.xp_off : p.yp_off)) +
-               (size_t)((xr ? y : x) * PH + z) * nw;
 #pragma unroll
         for (int w = 0; w < 2; ++w) {
             const int base = (pw0 + w) * 64;
             const int lo = pa - base < 0 ? 0 : pa - base, hi = pb - base > 63 ? 63 : pb - base;
             pm[w] = (w == 0 || pw0 + 1 <= pwend) && hi >= lo ? ((~0ull) >> (63 - (hi - lo))) << lo : 0ull;
         }
-        if (!FRESH) {
-            pn[0] = prow[pw0];
-            if (pwend > pw0) pn[1] = prow[pw0 + 1];
+        if (FRESH) {
+            pc_.row = rowi;
+            pc_.w0 = pw0;
+            pc_.w[0] = pc_.w[1] = 0ull;
+        } else if (pc_.row != rowi || pc_.w0 != pw0) {
+            pc_.row = rowi;
+            pc_.w0 = pw0;
+            pc_.w[0] = prow[pw0];
+            pc_.w[1] = pw0 + 1 < nw ? prow[pw0 + 1] : 0ull;
         }
+        pn[0] = pc_.w[0];
+        pn[1] = pc_.w[1];
     }
 
     // ---- in-window ray cells, z rays and the center ----
@@ -565,21 +696,33 @@ __device__ __forceinline__ int sense_observe(const Params &p, int8_t *map, Agent
     }
     if (q == 2) col_set<PH>(col[2], z, KNOWN | (uint32_t)t);
 
-    // ---- write back changed columns and ray cells ----
+    // ---- changed columns back to the tile (dirty), new plane marks to HBM ----
+    uint32_t dm = 0;
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
-        if (cin[i] && col_differs<PH>(col[i], orig[i]) && !(p.ablate & 8u)) col_store<PH>(map + coff[i], col[i]);
+    for (int i = 0; i < 4; ++i) {
+        const bool inroom = yin && x + i - 2 >= 0 && x + i - 2 < R.W;
+        // after a reset every slot is rewritten (zeros outside the room), so no
+        // column of the previous episode's window survives in the tile
+        if (FRESH || (inroom && col_differs<PH>(col[i], orig[i]))) {
+            const int s = tslot(x + i - 2, cy);
+            tile_write<PH>(tile, s, col[i]);
+            if (inroom) dm |= 1u << s;
+        }
+    }
+    dirty |= group_or(dm);
+
     if (q < 2) {
 #pragma unroll
         for (int w = 0; w < 2; ++w) {
             uint64_t nw = pm[w] & ~pn[w];
             if (nw) {
-                prow[pw0 + w] = pn[w] | pm[w];
+                pc_.w[w] = pn[w] | pm[w];
+                prow[pw0 + w] = pc_.w[w];
                 const int base = (pw0 + w) * 64;
                 while (nw) {
                     const int pos = base + __ffsll((unsigned long long)nw) - 1;
                     nw &= nw - 1;
-                    const int d = pos - pc;                       // in-window cells -2..+1 are in registers
+                    const int d = pos - pcoord;                   // window cells -2..+1 live in the tile
                     if (d >= 2 || d <= -3) {
                         const uint32_t v = (d == nfp + 1 || d == -nfm - 1) ? WALLB : KNOWN;
                         const int bx = q == 0 ? pos : x, by = q == 0 ? y : pos;
@@ -629,7 +772,7 @@ __device__ __forceinline__ int sense_observe(const Params &p, int8_t *map, Agent
 // load_room's draws (CubicEnv.py:407, :462-466) for seed: returns
 // x | y<<8 | z<<16 | room<<24.  Out of line: the ~1.2k-iteration MT seeding
 // is rare and keeps its registers away from the step loop.
-__device__ __noinline__ uint32_t reset_draw(const Params &p, uint32_t seed) {
+__device__ __forceinline__ uint32_t reset_draw(const Params &p, uint32_t seed) {
     MtStream mt;
     mt.seed = seed;
     mt.used = 0;
@@ -648,20 +791,21 @@ __device__ __noinline__ uint32_t reset_draw(const Params &p, uint32_t seed) {
 
 // ----------------------------------------------------------------------------
 // reset (envs/CubicEnv.py:77-108) for the groups with `need`: draws, clear of
-// the new room's bricks by the 4 lanes, then sensing from the start cell.
+// the new room's bricks and planes in HBM by the 4 lanes, a zero tile, then
+// sensing from the start cell.  The old episode's dirty tile is dropped.
 // ----------------------------------------------------------------------------
-template <int PH, int LMAX>
-__device__ __forceinline__ void group_reset(const Params &p, int8_t *map, bool need, uint32_t seed, Agent &g,
-                                            Room &R, const float *tab, float *obs_row, int q) {
+template <int PH>
+__device__ __forceinline__ void group_reset(const Params &p, int8_t *map, uint32_t *tile, uint32_t &dirty,
+                                            PlaneCache &pc_, bool need, uint32_t seed, Agent &g, Room &R,
+                                            const float *tab, float *obs_row, int q) {
     if (need) {
         const uint32_t drawn = reset_draw(p, seed);
         const int room = (int)(drawn >> 24);
         R = load_room(p, room);
-        const int sx = drawn & 0xff, sy = (drawn >> 8) & 0xff, sz = (drawn >> 16) & 0xff;
         g.room = room;
-        g.x = sx;
-        g.y = sy;
-        g.z = sz;
+        g.x = drawn & 0xff;
+        g.y = (drawn >> 8) & 0xff;
+        g.z = (drawn >> 16) & 0xff;
         g.facing = 0;
         g.last_action = 0;
         g.done = g.last_bump = g.near_wall = g.was_near_wall = false;
@@ -683,20 +827,27 @@ __device__ __forceinline__ void group_reset(const Params &p, int8_t *map, bool n
         uint4 *pl = reinterpret_cast<uint4 *>(map + p.xp_off);
         const uint32_t pchunks = (p.agent_bytes - p.xp_off) / 16u;
         for (uint32_t c = (uint32_t)q; c < pchunks; c += GROUP) pl[c] = make_uint4(0u, 0u, 0u, 0u);
+        dirty = 0;
+        pc_.row = -1;
     }
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
     if (need) {
         bool explored = false;
-        sense_observe<PH, LMAX, true>(p, map, g, R, false, explored, tab, ObsDst{obs_row, nullptr, false, false}, q);
+        sense_observe<PH, true>(p, map, tile, dirty, pc_, g, R, false, explored, tab,
+                                ObsDst{obs_row, nullptr, false, false}, q);
     }
 }
 
 // ----------------------------------------------------------------------------
 // the step kernel: 4 lanes per agent, K fused steps, SB3 auto-reset
 // ----------------------------------------------------------------------------
+constexpr int BLOCK = 256;
+constexpr int AGENTS_PER_BLOCK = BLOCK / GROUP;
+
 template <int PH, int LMAX, bool RESET_ONLY>
-__global__ __launch_bounds__(256) void env_kernel(Params p) {
+__global__ __launch_bounds__(BLOCK) void env_kernel(Params p) {
     __shared__ float tab[TAB_SIZE];
+    __shared__ __attribute__((aligned(16))) uint32_t tiles[AGENTS_PER_BLOCK * TileGeom<PH>::STRIDE];
     for (int k = threadIdx.x; k < TAB_SIZE; k += blockDim.x) tab[k] = p.lut[k];
     __syncthreads();
 
@@ -704,21 +855,33 @@ __global__ __launch_bounds__(256) void env_kernel(Params p) {
     const int i = (int)((blockIdx.x * blockDim.x + threadIdx.x) / GROUP);
     const bool active = i < p.N;
     const int ai = active ? i : 0;
+    uint32_t *tile = tiles + (threadIdx.x / GROUP) * TileGeom<PH>::STRIDE;
     Agent g = unpack(p.hot[ai]);
     Room R = load_room(p, active ? g.room : 0);
     uint32_t next_seed = p.next_seed[ai];
     int8_t *map = p.belief + (size_t)ai * p.agent_bytes;
+    uint32_t dirty = 0;
+    PlaneCache pc_;
+    pc_.row = -1;
+    pc_.w0 = 0;
+    pc_.w[0] = pc_.w[1] = 0ull;
 
     if (RESET_ONLY) {
         const bool need = active && (p.mask == nullptr || p.mask[i] != 0);
         const uint32_t seed = need ? (uint32_t)p.seeds[i] : 0u;
-        group_reset<PH, LMAX>(p, map, need, seed, g, R, tab, need ? p.obs + (size_t)i * VN_OBS_DIM : nullptr, q);
-        if (need && q == 0) {
-            p.hot[i] = pack(g);
-            p.next_seed[i] = seed + p.seed_stride;
+        group_reset<PH>(p, map, tile, dirty, pc_, need, seed, g, R, tab,
+                        need ? p.obs + (size_t)i * VN_OBS_DIM : nullptr, q);
+        if (need) {
+            tile_flush<PH>(p, map, tile, g, R, dirty, q);
+            if (q == 0) {
+                p.hot[i] = pack(g);
+                p.next_seed[i] = seed + p.seed_stride;
+            }
         }
         return;
     }
+
+    if (active) tile_fill<PH>(p, map, tile, g, R, q);
 
     uint32_t pw0 = 0, pw1 = 0, pw2 = 0, pw3 = 0;   // Philox words of the current 4-step block
     for (int k = 0; k < p.K; ++k) {
@@ -765,13 +928,14 @@ __global__ __launch_bounds__(256) void env_kernel(Params p) {
                 g.x += (dir == 0) - (dir == 1);
                 g.y += (dir == 2) - (dir == 3);
                 g.z += (dir == 4) - (dir == 5);
+                if (dir < 4) dirty = tile_shift<PH>(p, map, tile, dir, g.x, g.y, R, dirty, q);
             }
 
             bool explored = false;
             const ObsDst dst{p.obs + row * VN_OBS_DIM,
                              p.terminal_obs ? p.terminal_obs + row * VN_OBS_DIM : nullptr, p.autoreset != 0,
                              truncated};
-            const int vv = sense_observe<PH, LMAX, false>(p, map, g, R, moved, explored, tab, dst, q);
+            const int vv = sense_observe<PH, false>(p, map, tile, dirty, pc_, g, R, moved, explored, tab, dst, q);
 
             // compute_reward (:169-224), f64 in the reference's order
             double r = -0.05;
@@ -809,13 +973,17 @@ __global__ __launch_bounds__(256) void env_kernel(Params p) {
         const bool need = p.autoreset && finished;
         if (__ballot(need)) {
             const uint32_t seed = next_seed;
-            group_reset<PH, LMAX>(p, map, need, seed, g, R, tab, need ? p.obs + row * VN_OBS_DIM : nullptr, q);
+            group_reset<PH>(p, map, tile, dirty, pc_, need, seed, g, R, tab,
+                            need ? p.obs + row * VN_OBS_DIM : nullptr, q);
             if (need) next_seed = seed + p.seed_stride;
         }
     }
-    if (active && q == 0) {
-        p.hot[i] = pack(g);
-        p.next_seed[i] = next_seed;
+    if (active) {
+        tile_flush<PH>(p, map, tile, g, R, dirty, q);
+        if (q == 0) {
+            p.hot[i] = pack(g);
+            p.next_seed[i] = next_seed;
+        }
     }
 }
 
