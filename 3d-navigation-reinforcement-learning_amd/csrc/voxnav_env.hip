@@ -100,7 +100,19 @@ struct Agent {
     int cid, room;
 };
 
+// Env-constant values the (rare, out-of-line) reset path reads from device
+// memory, so they need not stay live in SGPRs across the step loop.
+struct EnvConst {
+    const uint4 *rooms;
+    const uint2 *rays;
+    const uint32_t *starts;
+    int32_t *err;
+    int n_rooms, use_room_draw, nby, pad0;
+    uint32_t agent_bytes, xp_off, pad1, pad2;
+};
+
 struct Params {
+    const EnvConst *envc;
     uint4 *hot;
     uint32_t *next_seed;
     int8_t *belief;
@@ -347,23 +359,26 @@ __device__ __forceinline__ int decode_count(uint32_t b) {   // center cell: know
 
 template <int PH>
 struct Col {
-    uint32_t w[PH / 4];
+    static constexpr int NQ = PH / 8;     // 64-bit words per column
+    uint64_t w[NQ];
 };
+
+template <int PH>
+__device__ __forceinline__ void col_zero(Col<PH> &c) {
+#pragma unroll
+    for (int k = 0; k < Col<PH>::NQ; ++k) c.w[k] = 0ull;
+}
 
 template <int PH>
 __device__ __forceinline__ void col_load(const int8_t *p, Col<PH> &c) {
     if constexpr (PH == 8) {
-        const uint2 v = *reinterpret_cast<const uint2 *>(p);
-        c.w[0] = v.x;
-        c.w[1] = v.y;
+        c.w[0] = *reinterpret_cast<const uint64_t *>(p);
     } else {
 #pragma unroll
-        for (int q = 0; q < PH / 16; ++q) {
-            const uint4 v = reinterpret_cast<const uint4 *>(p)[q];
-            c.w[4 * q + 0] = v.x;
-            c.w[4 * q + 1] = v.y;
-            c.w[4 * q + 2] = v.z;
-            c.w[4 * q + 3] = v.w;
+        for (int k = 0; k < PH / 16; ++k) {
+            const ulonglong2 v = reinterpret_cast<const ulonglong2 *>(p)[k];
+            c.w[2 * k] = v.x;
+            c.w[2 * k + 1] = v.y;
         }
     }
 }
@@ -371,49 +386,68 @@ __device__ __forceinline__ void col_load(const int8_t *p, Col<PH> &c) {
 template <int PH>
 __device__ __forceinline__ void col_store(int8_t *p, const Col<PH> &c) {
     if constexpr (PH == 8) {
-        *reinterpret_cast<uint2 *>(p) = make_uint2(c.w[0], c.w[1]);
+        *reinterpret_cast<uint64_t *>(p) = c.w[0];
     } else {
 #pragma unroll
-        for (int q = 0; q < PH / 16; ++q)
-            reinterpret_cast<uint4 *>(p)[q] = make_uint4(c.w[4 * q], c.w[4 * q + 1], c.w[4 * q + 2], c.w[4 * q + 3]);
+        for (int k = 0; k < PH / 16; ++k)
+            reinterpret_cast<ulonglong2 *>(p)[k] = make_ulonglong2(c.w[2 * k], c.w[2 * k + 1]);
+    }
+}
+
+// word holding byte i (i in [0, PH)), 0 outside
+template <int PH>
+__device__ __forceinline__ uint64_t col_word(const Col<PH> &c, int k) {
+    if constexpr (PH == 8) {
+        return k == 0 ? c.w[0] : 0ull;
+    } else {
+        uint64_t w = 0;
+#pragma unroll
+        for (int j = 0; j < Col<PH>::NQ; ++j) w = (k == j) ? c.w[j] : w;
+        return w;
     }
 }
 
 // byte i (dynamic) of the column; 0 (= unknown) outside [0, PH)
 template <int PH>
 __device__ __forceinline__ uint32_t col_byte(const Col<PH> &c, int i) {
-    uint32_t w = 0;
-#pragma unroll
-    for (int k = 0; k < PH / 4; ++k) w = ((i >> 2) == k) ? c.w[k] : w;
-    return (i >= 0 && i < PH) ? ((w >> (8 * (i & 3))) & 0xffu) : 0u;
+    const uint64_t w = (i >= 0 && i < PH) ? col_word<PH>(c, i >> 3) : 0ull;
+    return (uint32_t)(w >> (8 * (i & 7))) & 0xffu;
+}
+
+// the 4 bytes [z-2, z+1] as one u32 (byte 0 = z-2), zeros outside the column
+template <int PH>
+__device__ __forceinline__ uint32_t col_window(const Col<PH> &c, int z) {
+    const int o = z - 2;
+    if (o < 0) return (uint32_t)(c.w[0] << (8 * (-o)));
+    const int k = o >> 3, sh = 8 * (o & 7);
+    const uint64_t lo = col_word<PH>(c, k);
+    const uint64_t hi = col_word<PH>(c, k + 1);
+    return (uint32_t)(sh ? (lo >> sh) | (hi << (64 - sh)) : lo);
 }
 
 template <int PH>
 __device__ __forceinline__ void col_or(Col<PH> &c, int i, uint32_t v) {
 #pragma unroll
-    for (int k = 0; k < PH / 4; ++k)
-        if ((i >> 2) == k) c.w[k] |= v << (8 * (i & 3));
+    for (int k = 0; k < Col<PH>::NQ; ++k)
+        if ((i >> 3) == k) c.w[k] |= (uint64_t)v << (8 * (i & 7));
 }
 
 template <int PH>
 __device__ __forceinline__ void col_set(Col<PH> &c, int i, uint32_t v) {
 #pragma unroll
-    for (int k = 0; k < PH / 4; ++k)
-        if ((i >> 2) == k) c.w[k] = (c.w[k] & ~(0xffu << (8 * (i & 3)))) | (v << (8 * (i & 3)));
+    for (int k = 0; k < Col<PH>::NQ; ++k)
+        if ((i >> 3) == k) c.w[k] = (c.w[k] & ~(0xffull << (8 * (i & 7)))) | ((uint64_t)v << (8 * (i & 7)));
 }
 
-// OR `v` into bytes [lo, hi] (inclusive) -- the z rays
+// OR byte value `v` into bytes [lo, hi] (inclusive; empty when hi < lo) -- the z rays
 template <int PH>
 __device__ __forceinline__ void col_or_range(Col<PH> &c, int lo, int hi, uint32_t v) {
+    const uint64_t vv = (uint64_t)v * 0x0101010101010101ull;
 #pragma unroll
-    for (int k = 0; k < PH / 4; ++k) {
-        uint32_t m = 0;
-#pragma unroll
-        for (int b = 0; b < 4; ++b) {
-            const int i = 4 * k + b;
-            m |= (i >= lo && i <= hi) ? (v << (8 * b)) : 0u;
-        }
-        c.w[k] |= m;
+    for (int k = 0; k < Col<PH>::NQ; ++k) {
+        const int a = lo - 8 * k < 0 ? 0 : lo - 8 * k;
+        const int b = hi - 8 * k > 7 ? 7 : hi - 8 * k;
+        if (a <= b) c.w[k] |= vv & ((~0ull) >> (8 * (7 - b))) & ((~0ull) << (8 * a));
     }
 }
 
@@ -421,7 +455,7 @@ template <int PH>
 __device__ __forceinline__ bool col_differs(const Col<PH> &a, const Col<PH> &b) {
     bool d = false;
 #pragma unroll
-    for (int k = 0; k < PH / 4; ++k) d |= a.w[k] != b.w[k];
+    for (int k = 0; k < Col<PH>::NQ; ++k) d |= a.w[k] != b.w[k];
     return d;
 }
 
@@ -434,8 +468,9 @@ __device__ __forceinline__ uint32_t boff(int x, int y, int z, int nby) {
 // episode writes its obs to the terminal row (NULL: dropped) and the reset
 // obs goes to the regular row.
 struct ObsDst {
-    float *row;
-    float *term_row;
+    float *row;          // direct HBM row (NULL: none)
+    float *term_row;     // terminal-obs HBM row under auto-reset (NULL: dropped)
+    float *stage;        // LDS staging row: used instead of `row` when set
     bool select;
     bool truncated;
 };
@@ -462,32 +497,22 @@ __device__ __forceinline__ void mark(Col<PH> &c, int z, const Rays &ry, int r, i
 // ----------------------------------------------------------------------------
 template <int PH>
 struct TileGeom {
-    static constexpr int DW = PH / 4;                   // dwords per column
-    static constexpr int STRIDE = 16 * DW + 2;          // dwords per agent tile (+2: bank spread)
+    static constexpr int QW = PH / 8;                   // u64 per column
+    static constexpr int STRIDE = 16 * QW + 1;          // u64 per agent tile (+1: bank spread)
 };
 
 template <int PH>
-__device__ __forceinline__ void tile_read(const uint32_t *tile, int slot, Col<PH> &c) {
-    const uint32_t *s = tile + slot * TileGeom<PH>::DW;
-    if constexpr (PH == 8) {
-        const uint2 v = *reinterpret_cast<const uint2 *>(s);
-        c.w[0] = v.x;
-        c.w[1] = v.y;
-    } else {
+__device__ __forceinline__ void tile_read(const uint64_t *tile, int slot, Col<PH> &c) {
+    const uint64_t *s = tile + slot * TileGeom<PH>::QW;
 #pragma unroll
-        for (int k = 0; k < PH / 4; k += 2) {
-            const uint2 v = *reinterpret_cast<const uint2 *>(s + k);
-            c.w[k] = v.x;
-            c.w[k + 1] = v.y;
-        }
-    }
+    for (int k = 0; k < Col<PH>::NQ; ++k) c.w[k] = s[k];
 }
 
 template <int PH>
-__device__ __forceinline__ void tile_write(uint32_t *tile, int slot, const Col<PH> &c) {
-    uint32_t *s = tile + slot * TileGeom<PH>::DW;
+__device__ __forceinline__ void tile_write(uint64_t *tile, int slot, const Col<PH> &c) {
+    uint64_t *s = tile + slot * TileGeom<PH>::QW;
 #pragma unroll
-    for (int k = 0; k < PH / 4; k += 2) *reinterpret_cast<uint2 *>(s + k) = make_uint2(c.w[k], c.w[k + 1]);
+    for (int k = 0; k < Col<PH>::NQ; ++k) s[k] = c.w[k];
 }
 
 __device__ __forceinline__ int tslot(int x, int y) { return ((x & 3) << 2) | (y & 3); }
@@ -506,15 +531,14 @@ struct PlaneCache {      // lane 0: x-plane row, lane 1: y-plane row
 
 // Fill the tile from HBM (launch start): lane q loads its 4 window columns.
 template <int PH>
-__device__ __forceinline__ void tile_fill(const Params &p, const int8_t *map, uint32_t *tile, const Agent &g,
+__device__ __forceinline__ void tile_fill(const Params &p, const int8_t *map, uint64_t *tile, const Agent &g,
                                           const Room &R, int q) {
     const int cy = g.y + q - 2;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
         const int cx = g.x + i - 2;
         Col<PH> c;
-#pragma unroll
-        for (int k = 0; k < PH / 4; ++k) c.w[k] = 0u;
+        col_zero<PH>(c);
         if (cx >= 0 && cx < R.W && cy >= 0 && cy < R.D) col_load<PH>(map + boff<PH>(cx, cy, 0, p.nby), c);
         tile_write<PH>(tile, tslot(cx, cy), c);
     }
@@ -522,7 +546,7 @@ __device__ __forceinline__ void tile_fill(const Params &p, const int8_t *map, ui
 
 // Write the dirty window columns back to HBM (launch end).
 template <int PH>
-__device__ __forceinline__ void tile_flush(const Params &p, int8_t *map, const uint32_t *tile, const Agent &g,
+__device__ __forceinline__ void tile_flush(const Params &p, int8_t *map, const uint64_t *tile, const Agent &g,
                                            const Room &R, uint32_t dirty, int q) {
     const int cy = g.y + q - 2;
 #pragma unroll
@@ -541,7 +565,7 @@ __device__ __forceinline__ void tile_flush(const Params &p, int8_t *map, const u
 // lane q swaps one slot -- writes the leaving column back if dirty, loads
 // the entering one.  Returns the updated dirty mask.
 template <int PH>
-__device__ __forceinline__ uint32_t tile_shift(const Params &p, int8_t *map, uint32_t *tile, int dir, int x, int y,
+__device__ __forceinline__ uint32_t tile_shift(const Params &p, int8_t *map, uint64_t *tile, int dir, int x, int y,
                                                const Room &R, uint32_t dirty, int q) {
     int ex, ey, lx, ly;
     uint32_t entering;
@@ -565,8 +589,7 @@ __device__ __forceinline__ uint32_t tile_shift(const Params &p, int8_t *map, uin
         col_store<PH>(map + boff<PH>(lx, ly, 0, p.nby), old);
     }
     Col<PH> c;
-#pragma unroll
-    for (int k = 0; k < PH / 4; ++k) c.w[k] = 0u;
+    col_zero<PH>(c);
     if (ex >= 0 && ex < R.W && ey >= 0 && ey < R.D) col_load<PH>(map + boff<PH>(ex, ey, 0, p.nby), c);
     tile_write<PH>(tile, s, c);
     return dirty & ~entering;
@@ -576,7 +599,7 @@ __device__ __forceinline__ uint32_t tile_shift(const Params &p, int8_t *map, uin
 // visit update of _mark_visited/do_action :156-166) on the agent's tile.
 // Returns the center cell's visit count after the update.
 template <int PH, bool FRESH>
-__device__ __forceinline__ int sense_observe(const Params &p, int8_t *map, uint32_t *tile, uint32_t &dirty,
+__device__ __forceinline__ int sense_observe(const Params &p, int8_t *map, uint64_t *tile, uint32_t &dirty,
                                              PlaneCache &pc_, Agent &g, const Room &R, bool moved, bool &explored,
                                              const float *tab, ObsDst dst, int q) {
     const int x = g.x, y = g.y, z = g.z, nby = p.nby, L = p.L;
@@ -604,8 +627,7 @@ __device__ __forceinline__ int sense_observe(const Params &p, int8_t *map, uint3
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
         if (FRESH) {
-#pragma unroll
-            for (int k = 0; k < PH / 4; ++k) col[i].w[k] = 0u;
+            col_zero<PH>(col[i]);
         } else {
             tile_read<PH>(tile, tslot(x + i - 2, cy), col[i]);
         }
@@ -711,25 +733,48 @@ __device__ __forceinline__ int sense_observe(const Params &p, int8_t *map, uint3
     }
     dirty |= group_or(dm);
 
+    // new marks: row bits set now for the first time.  Those inside the window
+    // (d = -2..+1 from the agent) live in the tile; the others get their
+    // byte written blind.  A row change makes a burst of new cells, so the
+    // burst is spread over the 4 lanes of the group by position mod 4.
+    uint64_t rel = 0;                      // lanes 0/1: new bits relative to the span start pa
     if (q < 2) {
+        uint64_t nwd[2];
 #pragma unroll
         for (int w = 0; w < 2; ++w) {
-            uint64_t nw = pm[w] & ~pn[w];
-            if (nw) {
+            nwd[w] = pm[w] & ~pn[w];
+            if (nwd[w]) {
                 pc_.w[w] = pn[w] | pm[w];
                 prow[pw0 + w] = pc_.w[w];
-                const int base = (pw0 + w) * 64;
-                while (nw) {
-                    const int pos = base + __ffsll((unsigned long long)nw) - 1;
-                    nw &= nw - 1;
-                    const int d = pos - pcoord;                   // window cells -2..+1 live in the tile
-                    if (d >= 2 || d <= -3) {
-                        const uint32_t v = (d == nfp + 1 || d == -nfm - 1) ? WALLB : KNOWN;
-                        const int bx = q == 0 ? pos : x, by = q == 0 ? y : pos;
-                        map[boff<PH>(bx, by, z, nby)] = (int8_t)v;
-                    }
-                }
             }
+        }
+        const int sh = pa - pw0 * 64;      // 0..63
+        rel = sh == 0 ? nwd[0] : (nwd[0] >> sh) | (nwd[1] << (64 - sh));
+        const int c = pcoord - pa;         // the agent's own bit; window cells are c-2 .. c+1
+        rel &= ~(c >= 2 ? (0xfull << (c - 2)) : ((1ull << (c + 2)) - 1ull));
+    }
+    {
+        const uint32_t rxl = (uint32_t)__shfl((int)(uint32_t)rel, 0, GROUP);
+        const uint32_t rxh = (uint32_t)__shfl((int)(uint32_t)(rel >> 32), 0, GROUP);
+        const uint32_t ryl = (uint32_t)__shfl((int)(uint32_t)rel, 1, GROUP);
+        const uint32_t ryh = (uint32_t)__shfl((int)(uint32_t)(rel >> 32), 1, GROUP);
+        const int pax = __shfl(pa, 0, GROUP), pay = __shfl(pa, 1, GROUP);
+        const uint64_t lane_sel = 0x1111111111111111ull << q;
+        uint64_t mx = (((uint64_t)rxh << 32) | rxl) & lane_sel;
+        uint64_t my = (((uint64_t)ryh << 32) | ryl) & lane_sel;
+        while (mx) {
+            const int pos = pax + __ffsll((unsigned long long)mx) - 1;
+            mx &= mx - 1;
+            const int d = pos - x;
+            const uint32_t v = (d == ry.nf[0] + 1 || d == -ry.nf[1] - 1) ? WALLB : KNOWN;
+            map[boff<PH>(pos, y, z, nby)] = (int8_t)v;
+        }
+        while (my) {
+            const int pos = pay + __ffsll((unsigned long long)my) - 1;
+            my &= my - 1;
+            const int d = pos - y;
+            const uint32_t v = (d == ry.nf[2] + 1 || d == -ry.nf[3] - 1) ? WALLB : KNOWN;
+            map[boff<PH>(x, pos, z, nby)] = (int8_t)v;
         }
     }
 
@@ -738,18 +783,19 @@ __device__ __forceinline__ int sense_observe(const Params &p, int8_t *map, uint3
     g.move_mask = mm;
 
     // ---- observation row: lane q writes obs[16i+4q..+3] and tail float4 q ----
-    float *obs_row = dst.row;
+    float *obs_row = dst.stage ? dst.stage : dst.row;
     if (dst.select && (dst.truncated || g.done || g.visited >= R.finish_visits)) obs_row = dst.term_row;
     if (p.ablate & 4u) obs_row = nullptr;
     if (obs_row) {
         float4 *o4 = reinterpret_cast<float4 *>(obs_row);
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
+            const uint32_t wb = col_window<PH>(col[i], z);
             float4 v;
-            v.x = tab[col_byte<PH>(col[i], z - 2)];
-            v.y = tab[col_byte<PH>(col[i], z - 1)];
-            v.z = tab[col_byte<PH>(col[i], z)];
-            v.w = tab[col_byte<PH>(col[i], z + 1)];
+            v.x = tab[wb & 0xffu];
+            v.y = tab[(wb >> 8) & 0xffu];
+            v.z = tab[(wb >> 16) & 0xffu];
+            v.w = tab[wb >> 24];
             o4[4 * i + q] = v;
         }
         float4 tv;
@@ -769,23 +815,58 @@ __device__ __forceinline__ int sense_observe(const Params &p, int8_t *map, uint3
     return t;
 }
 
-// load_room's draws (CubicEnv.py:407, :462-466) for seed: returns
-// x | y<<8 | z<<16 | room<<24.  Out of line: the ~1.2k-iteration MT seeding
-// is rare and keeps its registers away from the step loop.
-__device__ __forceinline__ uint32_t reset_draw(const Params &p, uint32_t seed) {
+__device__ __forceinline__ Room load_room_c(const EnvConst *ec, int r) {
+    const uint4 a = ec->rooms[2 * r];
+    const uint4 b = ec->rooms[2 * r + 1];
+    Room R;
+    R.W = a.x & 0xff;
+    R.D = (a.x >> 8) & 0xff;
+    R.H = (a.x >> 16) & 0xff;
+    R.total_free = a.y;
+    R.ray_off = a.z;
+    R.start_off = a.w;
+    R.fixed_start = (int32_t)b.x;
+    R.nbx = b.y & 0xffff;
+    R.nby = b.y >> 16;
+    R.finish_visits = b.z;
+    return R;
+}
+
+// The out-of-line half of reset (envs/CubicEnv.py:77-108): load_room's
+// draws (:407, :462-466) for `seed`, then lane q's share of clearing the new
+// room's bricks and both marked-bit planes.  Returns x | y<<8 | z<<16 |
+// room<<24.  Reads only through `ec` (device memory), so the step loop
+// keeps none of this in registers.
+template <int PH>
+__device__ __noinline__ uint32_t reset_prepare(const EnvConst *ec, uint32_t seed, int8_t *map, int q) {
     MtStream mt;
     mt.seed = seed;
     mt.used = 0;
-    mt.err = p.err;
+    mt.err = ec->err;
     mt_first_outputs(seed, mt.buf);
-    const int room = p.use_room_draw ? (int)mt.below((uint32_t)p.n_rooms) : 0;
-    const Room R = load_room(p, room);
+    const int room = ec->use_room_draw ? (int)mt.below((uint32_t)ec->n_rooms) : 0;
+    const Room R = load_room_c(ec, room);
     uint32_t s;
     if (R.fixed_start >= 0) s = (uint32_t)R.fixed_start;
-    else s = p.starts[R.start_off + mt.below(R.total_free)];
-    const int sx = s & 0xff, sy = (s >> 8) & 0xff, sz = (s >> 16) & 0xff;
-    const uint2 rec = p.rays[R.ray_off + (uint32_t)((sx * R.D + sy) * R.H + sz)];
-    if ((rec.y >> 16) & 1u) s = p.starts[R.start_off + mt.below(R.total_free)];   // start in a wall
+    else s = ec->starts[R.start_off + mt.below(R.total_free)];
+    {
+        const int sx = s & 0xff, sy = (s >> 8) & 0xff, sz = (s >> 16) & 0xff;
+        const uint2 rec = ec->rays[R.ray_off + (uint32_t)((sx * R.D + sy) * R.H + sz)];
+        if ((rec.y >> 16) & 1u) s = ec->starts[R.start_off + mt.below(R.total_free)];   // start in a wall
+    }
+    // clear the room's bricks to "unknown" (0x00), 16 B per lane per store
+    uint4 *base = reinterpret_cast<uint4 *>(map);
+    const uint32_t per_brick = (uint32_t)PH;          // 16-byte chunks per brick
+    const uint32_t total = (uint32_t)(R.nbx * R.nby) * per_brick;
+    for (uint32_t c = (uint32_t)q; c < total; c += 4u) {
+        const uint32_t brick = c / per_brick, w = c - brick * per_brick;
+        const uint32_t bx = brick / (uint32_t)R.nby, by = brick - bx * (uint32_t)R.nby;
+        base[(bx * (uint32_t)ec->nby + by) * per_brick + w] = make_uint4(0u, 0u, 0u, 0u);
+    }
+    // and both marked-bit planes
+    uint4 *pl = reinterpret_cast<uint4 *>(map + ec->xp_off);
+    const uint32_t pchunks = (ec->agent_bytes - ec->xp_off) / 16u;
+    for (uint32_t c = (uint32_t)q; c < pchunks; c += 4u) pl[c] = make_uint4(0u, 0u, 0u, 0u);
     return (s & 0xffffffu) | ((uint32_t)room << 24);
 }
 
@@ -795,11 +876,11 @@ __device__ __forceinline__ uint32_t reset_draw(const Params &p, uint32_t seed) {
 // sensing from the start cell.  The old episode's dirty tile is dropped.
 // ----------------------------------------------------------------------------
 template <int PH>
-__device__ __forceinline__ void group_reset(const Params &p, int8_t *map, uint32_t *tile, uint32_t &dirty,
+__device__ __forceinline__ void group_reset(const Params &p, int8_t *map, uint64_t *tile, uint32_t &dirty,
                                             PlaneCache &pc_, bool need, uint32_t seed, Agent &g, Room &R,
-                                            const float *tab, float *obs_row, int q) {
+                                            const float *tab, float *obs_row, float *stage_row, int q) {
     if (need) {
-        const uint32_t drawn = reset_draw(p, seed);
+        const uint32_t drawn = reset_prepare<PH>(p.envc, seed, map, q);
         const int room = (int)(drawn >> 24);
         R = load_room(p, room);
         g.room = room;
@@ -814,19 +895,6 @@ __device__ __forceinline__ void group_reset(const Params &p, int8_t *map, uint32
         g.bumps = 0;
         g.cid = 0;
         g.move_mask = 0;
-        // clear the room's bricks to "unknown" (0x00), 16 B per lane per store
-        uint4 *base = reinterpret_cast<uint4 *>(map);
-        const uint32_t per_brick = (uint32_t)PH;          // 16-byte chunks per brick
-        const uint32_t total = (uint32_t)(R.nbx * R.nby) * per_brick;
-        for (uint32_t c = (uint32_t)q; c < total; c += GROUP) {
-            const uint32_t brick = c / per_brick, w = c - brick * per_brick;
-            const uint32_t bx = brick / (uint32_t)R.nby, by = brick - bx * (uint32_t)R.nby;
-            base[(bx * (uint32_t)p.nby + by) * per_brick + w] = make_uint4(0u, 0u, 0u, 0u);
-        }
-        // and both marked-bit planes
-        uint4 *pl = reinterpret_cast<uint4 *>(map + p.xp_off);
-        const uint32_t pchunks = (p.agent_bytes - p.xp_off) / 16u;
-        for (uint32_t c = (uint32_t)q; c < pchunks; c += GROUP) pl[c] = make_uint4(0u, 0u, 0u, 0u);
         dirty = 0;
         pc_.row = -1;
     }
@@ -834,7 +902,7 @@ __device__ __forceinline__ void group_reset(const Params &p, int8_t *map, uint32
     if (need) {
         bool explored = false;
         sense_observe<PH, true>(p, map, tile, dirty, pc_, g, R, false, explored, tab,
-                                ObsDst{obs_row, nullptr, false, false}, q);
+                                ObsDst{obs_row, nullptr, stage_row, false, false}, q);
     }
 }
 
@@ -845,9 +913,14 @@ constexpr int BLOCK = 256;
 constexpr int AGENTS_PER_BLOCK = BLOCK / GROUP;
 
 template <int PH, int LMAX, bool RESET_ONLY>
-__global__ __launch_bounds__(BLOCK) void env_kernel(Params p) {
+#ifndef VN_MIN_WAVES_PER_SIMD
+#define VN_MIN_WAVES_PER_SIMD 1
+#endif
+__global__ __launch_bounds__(BLOCK, VN_MIN_WAVES_PER_SIMD) void env_kernel(Params p) {
     __shared__ float tab[TAB_SIZE];
-    __shared__ __attribute__((aligned(16))) uint32_t tiles[AGENTS_PER_BLOCK * TileGeom<PH>::STRIDE];
+    __shared__ __attribute__((aligned(16))) uint64_t tiles[AGENTS_PER_BLOCK * TileGeom<PH>::STRIDE];
+    // obs rows of the step, staged per wave so HBM sees 1 KiB contiguous stores
+    __shared__ __attribute__((aligned(16))) float4 stage[AGENTS_PER_BLOCK * (VN_OBS_DIM / 4)];
     for (int k = threadIdx.x; k < TAB_SIZE; k += blockDim.x) tab[k] = p.lut[k];
     __syncthreads();
 
@@ -855,7 +928,7 @@ __global__ __launch_bounds__(BLOCK) void env_kernel(Params p) {
     const int i = (int)((blockIdx.x * blockDim.x + threadIdx.x) / GROUP);
     const bool active = i < p.N;
     const int ai = active ? i : 0;
-    uint32_t *tile = tiles + (threadIdx.x / GROUP) * TileGeom<PH>::STRIDE;
+    uint64_t *tile = tiles + (threadIdx.x / GROUP) * TileGeom<PH>::STRIDE;
     Agent g = unpack(p.hot[ai]);
     Room R = load_room(p, active ? g.room : 0);
     uint32_t next_seed = p.next_seed[ai];
@@ -870,7 +943,7 @@ __global__ __launch_bounds__(BLOCK) void env_kernel(Params p) {
         const bool need = active && (p.mask == nullptr || p.mask[i] != 0);
         const uint32_t seed = need ? (uint32_t)p.seeds[i] : 0u;
         group_reset<PH>(p, map, tile, dirty, pc_, need, seed, g, R, tab,
-                        need ? p.obs + (size_t)i * VN_OBS_DIM : nullptr, q);
+                        need ? p.obs + (size_t)i * VN_OBS_DIM : nullptr, nullptr, q);
         if (need) {
             tile_flush<PH>(p, map, tile, g, R, dirty, q);
             if (q == 0) {
@@ -882,24 +955,28 @@ __global__ __launch_bounds__(BLOCK) void env_kernel(Params p) {
     }
 
     if (active) tile_fill<PH>(p, map, tile, g, R, q);
+#ifndef VN_STAGE_OBS
+#define VN_STAGE_OBS 1
+#endif
+    float *stage_row =
+        VN_STAGE_OBS ? reinterpret_cast<float *>(stage + (size_t)(threadIdx.x / GROUP) * (VN_OBS_DIM / 4)) : nullptr;
 
-    uint32_t pw0 = 0, pw1 = 0, pw2 = 0, pw3 = 0;   // Philox words of the current 4-step block
-    for (int k = 0; k < p.K; ++k) {
+    // outer loop: one Philox call per agent per 4-step block of the global
+    // step counter; inner loop: the steps of that block
+    for (int k = 0; k < p.K;) {
+    const uint64_t tb = p.t0 + (uint64_t)k;
+    uint32_t acts = 0;                                    // 4 actions, 8 bits each, by (t & 3)
+    if (!p.actions) {
+        const uint4 o = philox4x32_10(p.policy_seed, p.gid_base + (uint64_t)ai, tb >> 2);
+        acts = __umulhi(o.x, 6u) | (__umulhi(o.y, 6u) << 8) | (__umulhi(o.z, 6u) << 16) | (__umulhi(o.w, 6u) << 24);
+    }
+    const int jn = (4 - (int)(tb & 3u)) < (p.K - k) ? (4 - (int)(tb & 3u)) : (p.K - k);
+    for (int j = 0; j < jn; ++j, ++k) {
         bool finished = false;
         const size_t row = (size_t)k * (size_t)p.N + (size_t)i;
-        const uint64_t tt = p.t0 + (uint64_t)k;
-        if (!p.actions && (k == 0 || (tt & 3u) == 0)) {
-            uint4 o = philox4x32_10(p.policy_seed, p.gid_base + (uint64_t)ai, tt >> 2);
-            pw0 = o.x; pw1 = o.y; pw2 = o.z; pw3 = o.w;
-        }
+        const uint64_t tt = tb + (uint64_t)j;
         if (active) {
-            int a;
-            if (p.actions) {
-                a = p.actions[row];
-            } else {
-                const uint32_t w = (tt & 3u) == 0 ? pw0 : (tt & 3u) == 1 ? pw1 : (tt & 3u) == 2 ? pw2 : pw3;
-                a = (int)__umulhi(w, 6u);
-            }
+            const int a = p.actions ? p.actions[row] : (int)((acts >> (8 * (uint32_t)(tt & 3u))) & 0xffu);
             if (p.actions_out && q == 0) p.actions_out[row] = a;
 
             // step() prologue (:111-116)
@@ -933,8 +1010,8 @@ __global__ __launch_bounds__(BLOCK) void env_kernel(Params p) {
 
             bool explored = false;
             const ObsDst dst{p.obs + row * VN_OBS_DIM,
-                             p.terminal_obs ? p.terminal_obs + row * VN_OBS_DIM : nullptr, p.autoreset != 0,
-                             truncated};
+                             p.terminal_obs ? p.terminal_obs + row * VN_OBS_DIM : nullptr, stage_row,
+                             p.autoreset != 0, truncated};
             const int vv = sense_observe<PH, false>(p, map, tile, dirty, pc_, g, R, moved, explored, tab, dst, q);
 
             // compute_reward (:169-224), f64 in the reference's order
@@ -974,9 +1051,23 @@ __global__ __launch_bounds__(BLOCK) void env_kernel(Params p) {
         if (__ballot(need)) {
             const uint32_t seed = next_seed;
             group_reset<PH>(p, map, tile, dirty, pc_, need, seed, g, R, tab,
-                            need ? p.obs + row * VN_OBS_DIM : nullptr, q);
+                            need ? p.obs + row * VN_OBS_DIM : nullptr, stage_row, q);
             if (need) next_seed = seed + p.seed_stride;
         }
+        // flush the wave's 16 staged obs rows: contiguous in [K][N][80]
+        if (VN_STAGE_OBS) {
+            const int lane = threadIdx.x & 63;
+            const int wave_agent0 = (int)((blockIdx.x * blockDim.x + (threadIdx.x & ~63)) / GROUP);
+            const float4 *ws = stage + (size_t)((threadIdx.x & ~63) / GROUP) * (VN_OBS_DIM / 4);
+            float4 *dst4 = reinterpret_cast<float4 *>(p.obs + ((size_t)k * p.N + wave_agent0) * VN_OBS_DIM);
+            const int nvalid = (p.N - wave_agent0) * (VN_OBS_DIM / 4);   // float4s of active agents
+#pragma unroll
+            for (int j = 0; j < (64 / GROUP) * (VN_OBS_DIM / 4) / 64; ++j) {
+                const int f = lane + 64 * j;
+                if (f < nvalid) dst4[f] = ws[f];
+            }
+        }
+    }
     }
     if (active) {
         tile_flush<PH>(p, map, tile, g, R, dirty, q);
@@ -1075,6 +1166,7 @@ struct VnEnv {
     uint32_t *d_seed = nullptr;
     int8_t *d_belief = nullptr;
     int32_t *d_err = nullptr;
+    EnvConst *d_envc = nullptr;
     uint32_t ablate = 0;
 };
 
@@ -1108,6 +1200,7 @@ int ensure_mt_table(int device) {
 Params base_params(VnEnv *e) {
     Params p;
     std::memset(&p, 0, sizeof(p));
+    p.envc = e->d_envc;
     p.hot = e->d_hot;
     p.next_seed = e->d_seed;
     p.belief = e->d_belief;
@@ -1172,6 +1265,7 @@ void free_env(VnEnv *e) {
     (void)hipFree(e->d_seed);
     (void)hipFree(e->d_belief);
     (void)hipFree(e->d_err);
+    (void)hipFree(e->d_envc);
     delete e;
 }
 
@@ -1340,6 +1434,7 @@ int vn_create(const VnRoomSet *rooms, int32_t n_agents, const VnConfig *cfg, int
     VN_ALLOC(e->d_seed, (size_t)n_agents * sizeof(uint32_t));
     VN_ALLOC(e->d_belief, belief_bytes);
     VN_ALLOC(e->d_err, sizeof(int32_t));
+    VN_ALLOC(e->d_envc, sizeof(EnvConst));
 #undef VN_ALLOC
     hipError_t he = hipSuccess;
     if (he == hipSuccess) he = hipMemcpy(e->d_rooms, desc.data(), desc.size() * sizeof(uint32_t), hipMemcpyHostToDevice);
@@ -1351,6 +1446,20 @@ int vn_create(const VnRoomSet *rooms, int32_t n_agents, const VnConfig *cfg, int
     if (he == hipSuccess) he = hipMemset(e->d_seed, 0, (size_t)n_agents * sizeof(uint32_t));
     if (he == hipSuccess) he = hipMemset(e->d_belief, 0, belief_bytes);   // 0x00 = unknown
     if (he == hipSuccess) he = hipMemset(e->d_err, 0, sizeof(int32_t));
+    if (he == hipSuccess) {
+        EnvConst ec;
+        std::memset(&ec, 0, sizeof(ec));
+        ec.rooms = e->d_rooms;
+        ec.rays = e->d_rays;
+        ec.starts = e->d_starts;
+        ec.err = e->d_err;
+        ec.n_rooms = e->n_rooms;
+        ec.use_room_draw = e->cfg.use_room_draw;
+        ec.nby = e->nby;
+        ec.agent_bytes = e->agent_bytes;
+        ec.xp_off = e->xp_off;
+        he = hipMemcpy(e->d_envc, &ec, sizeof(ec), hipMemcpyHostToDevice);
+    }
     if (he == hipSuccess) he = hipDeviceSynchronize();
     if (he != hipSuccess) {
         free_env(e);

@@ -41,6 +41,20 @@ def needs_build() -> bool:
     return any(p.stat().st_mtime > t for p in SOURCES + HEADERS + [Path(__file__)])
 
 
+def build_variant(name: str, defines=(), verbose: bool = False) -> Path:
+    """A differently-configured build (-D flags) under _lib/variants/ for A/B timing."""
+    out = LIBDIR / "variants" / f"libvoxnav_{name}.so"
+    out.parent.mkdir(parents=True, exist_ok=True)
+    cmd = [hipcc(), *HIPCC_FLAGS, "-I", str(INCLUDE), *[f"-D{d}" for d in defines], *map(str, SOURCES),
+           "-o", str(out)]
+    if verbose:
+        print(" ".join(cmd))
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"hipcc failed ({r.returncode}):\n{r.stdout}\n{r.stderr}")
+    return out
+
+
 def build(force: bool = False, verbose: bool = False) -> Path:
     if not force and not needs_build():
         return LIB

@@ -65,6 +65,22 @@ _SIGS = {
 EXPORTED_SYMBOLS = tuple(_SIGS)
 
 
+def _bind(lib):
+    for name, (res, args) in _SIGS.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    if lib.vn_abi_version() != 1:
+        raise VoxnavError("libvoxnav ABI version mismatch")
+    return lib
+
+
+def load_variant(path):
+    """Load another build of the library (A/B benchmarking); separate handle."""
+    import torch  # noqa: F401
+    return _bind(C.CDLL(str(path)))
+
+
 def load(build_if_missing: bool = True):
     """Load libvoxnav.so (building it with hipcc first if it is stale)."""
     global _lib
@@ -78,15 +94,8 @@ def load(build_if_missing: bool = True):
         # torch first: its libamdhip64.so.7 then satisfies our NEEDED entry, so
         # the process has one HIP runtime.
         import torch  # noqa: F401
-        lib = C.CDLL(str(_build.LIB))
-        for name, (res, args) in _SIGS.items():
-            fn = getattr(lib, name)
-            fn.restype = res
-            fn.argtypes = args
-        if lib.vn_abi_version() != 1:
-            raise VoxnavError("libvoxnav ABI version mismatch")
-        _lib = lib
-        return lib
+        _lib = _bind(C.CDLL(str(_build.LIB)))
+        return _lib
 
 
 def check(rc: int, what: str = "voxnav"):

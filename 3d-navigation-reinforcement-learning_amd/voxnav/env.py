@@ -70,10 +70,10 @@ class BatchedGridEnv:
                  local_map_length: int = 4, crash_penalty: float = -2.0, width: int = 20, depth: int = 20,
                  height: int = 12, autoreset: bool = True, device: Union[int, str, torch.device, None] = None,
                  agent_id_base: int = 0, seed_stride: Optional[int] = None,
-                 finish_percentage: float = FINISH_PERCENTAGE):
+                 finish_percentage: float = FINISH_PERCENTAGE, lib=None):
         if not torch.cuda.is_available():
             raise _native.VoxnavError("BatchedGridEnv needs a ROCm GPU (torch.cuda.is_available() is False)")
-        self.lib = _native.load()
+        self.lib = lib if lib is not None else _native.load()
         self.room_set = as_room_set(rooms, room_path, width, depth, height)
         self.num_agents = int(num_agents)
         self.local_map_length = int(local_map_length)

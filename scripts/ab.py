@@ -1,0 +1,62 @@
+#!/usr/bin/env python3
+"""Interleaved A/B timing of library variants in ONE process (same device,
+same state), e.g.  python scripts/ab.py --variants base:path.so,lb4:other.so"""
+import argparse
+import json
+import sys
+import time
+from pathlib import Path
+
+REPO = Path(__file__).resolve().parent.parent
+sys.path.insert(0, str(REPO / "3d-navigation-reinforcement-learning_amd"))
+import torch  # noqa: E402
+
+from voxnav import _native  # noqa: E402
+from voxnav.env import BatchedGridEnv, Rollout  # noqa: E402
+from voxnav.rooms import box_room, load_archive_set, single_room_set  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--variants", required=True)
+    ap.add_argument("--configs", default="65536:32x32x8:10:16")
+    ap.add_argument("--steps", type=int, default=256)
+    ap.add_argument("--rounds", type=int, default=5)
+    a = ap.parse_args()
+    libs = {}
+    for v in a.variants.split(","):
+        name, path = v.split(":", 1)
+        libs[name] = _native.load_variant(REPO / path if not path.startswith("/") else path)
+    cfgs = [c.split(":") for c in a.configs.split(",")]
+    envs, outs = {}, {}
+    for name, lib in libs.items():
+        for c in cfgs:
+            n, room, L, F = int(c[0]), c[1], int(c[2]), int(c[3])
+            rs = load_archive_set(room) if room.startswith("P") else single_room_set(box_room(*map(int, room.split("x"))))
+            e = BatchedGridEnv(num_agents=n, rooms=rs, local_map_length=L, autoreset=True, device="cuda:0", lib=lib)
+            e.reset(seed=42)
+            envs[(name, tuple(c))] = e
+            outs[(name, tuple(c))] = Rollout(torch.empty((F, n, 80), device="cuda:0"), torch.empty((F, n), device="cuda:0"),
+                                              torch.empty((F, n), dtype=torch.uint8, device="cuda:0"),
+                                              torch.empty((F, n), dtype=torch.uint8, device="cuda:0"), None)
+    res = {k: [] for k in envs}
+    for r in range(a.rounds):
+        for k, e in envs.items():
+            F = int(k[1][3])
+            o = outs[k]
+            for _ in range(2):
+                e.step_random(F, out=o)
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            for _ in range(max(1, a.steps // F)):
+                e.step_random(F, out=o)
+            torch.cuda.synchronize()
+            res[k].append(e.num_agents * max(1, a.steps // F) * F / (time.perf_counter() - t0))
+    for k, v in res.items():
+        v = sorted(v)
+        print(json.dumps({"variant": k[0], "config": ":".join(k[1]), "Gsteps_median": round(v[len(v) // 2] / 1e9, 3),
+                          "Gsteps_max": round(v[-1] / 1e9, 3)}))
+
+
+if __name__ == "__main__":
+    main()
