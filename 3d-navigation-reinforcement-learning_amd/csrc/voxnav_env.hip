@@ -3,8 +3,8 @@
 // The hot path of Noimps/3D-Navigation-Reinforcement-Learning is
 // GridAgent.step/reset in envs/CubicEnv.py, run one agent per OS process
 // under SB3's SubprocVecEnv (train/Grid_Train.py:191-192).  Here every agent
-// is one lane of a 64-wide wavefront and a launch advances all N agents by
-// K steps.  See DESIGN.md for the data layout and the roofline.
+// is a group of 4 lanes of a 64-wide wavefront (16 agents per wave) and a
+// launch advances all N agents by K steps.  See DESIGN.md for the data layout and the roofline.
 //
 // Layout in HBM
 //   hot state   uint4 per agent (16 B, SoA across agents -> coalesced)
@@ -14,10 +14,10 @@
 //     w2 = visited_count (24 b) | room<<24
 //     w3 = bump_count (26 b, saturating) | move_mask<<26  (6 b: first cell
 //          free in +x,-x,+y,-y,+z,-z -> the next move needs no memory read)
-//   belief map  int8 per cell (the reference's internal_grid; -2 wall,
-//     -1 unknown, 0 known free, n visits saturating at 127 -- the obs clips
-//     at 20 (CubicEnv.py:274) and the reward caps at 25 (:180), so the
-//     saturation is observationally exact).  Per agent the map is bricked:
+//   belief map  one byte per cell (the reference's internal_grid): bit7
+//     known, bit6 wall, bits0-5 visit count saturating at 63 -- the obs
+//     clips at 20 (CubicEnv.py:274) and the reward caps at 25 (:180), so
+//     the saturation is observationally exact.  Per agent the map is bricked:
 //     4x4 (x,y) columns of PH bytes (z contiguous), bricks x-major, so the
 //     4x4x4 window is <=4 bricks and an x/y ray crosses <=4 bricks.
 //   room tables (tiny, L2 resident): per cell an 8-byte ray record with the
@@ -40,30 +40,12 @@
 #include <string>
 #include <vector>
 
-#include "voxnav.h"
+#include "vn_common.h"
 
 namespace {
 
-// ----------------------------------------------------------------------------
-// errors
-// ----------------------------------------------------------------------------
-thread_local std::string g_last_error;
-
-int fail(int code, const char *fmt, ...) {
-    char buf[512];
-    va_list ap;
-    va_start(ap, fmt);
-    vsnprintf(buf, sizeof(buf), fmt, ap);
-    va_end(ap);
-    g_last_error = buf;
-    return code;
-}
-
-#define VN_HIP(expr)                                                                        \
-    do {                                                                                    \
-        hipError_t e_ = (expr);                                                             \
-        if (e_ != hipSuccess) return fail(VN_ERR_HIP, "%s: %s", #expr, hipGetErrorString(e_)); \
-    } while (0)
+using vn_detail::fail;
+using vn_detail::g_last_error;
 
 constexpr int MT_N = 624;
 constexpr int MT_C = 8;  // MT words captured by the streaming seed (draws 0..7)

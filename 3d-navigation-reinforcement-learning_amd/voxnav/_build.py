@@ -18,8 +18,8 @@ CSRC = PROJECT / "csrc"
 INCLUDE = REPO / "include"
 LIBDIR = PKG / "_lib"
 LIB = LIBDIR / "libvoxnav.so"
-SOURCES = [CSRC / "voxnav_env.hip"]
-HEADERS = [INCLUDE / "voxnav.h"]
+SOURCES = [CSRC / "voxnav_env.hip", CSRC / "voxnav_collect.hip"]
+HEADERS = [INCLUDE / "voxnav.h", CSRC / "vn_common.h"]
 ARCH = os.environ.get("VOXNAV_ARCH", "gfx950")
 
 # -ffp-contract=off: the reward (f64) and obs quotients must follow the

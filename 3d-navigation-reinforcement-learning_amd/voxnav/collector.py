@@ -1,0 +1,269 @@
+"""On-device PPO rollout collector (policy in the loop) around BatchedGridEnv.
+
+Restates sb3_contrib ``RecurrentPPO.collect_rollouts`` (and SB3
+``OnPolicyAlgorithm.collect_rollouts`` for the feed-forward policy), which
+train/Grid_Train.py reaches through ``model.learn`` (:228) with
+``n_steps=2048, gamma=0.99, gae_lambda=0.95`` (:84-85), for N agents on one
+GPU with nothing crossing PCIe per step except one 4-byte count:
+
+per step t
+  1. policy forward on obs[t] (states already zeroed for agents whose
+     previous step ended an episode): library GEMMs (x @ W_ih^T for both
+     LSTMs at once, h @ W_hh^T, the Tanh MLPs) and the HIP kernels
+     ``vn_lstm_cell`` (gates -> h, c; states stored into the buffer) and
+     ``vn_policy_head`` (logits, value, Categorical draw, log-prob)
+  2. ``BatchedGridEnv.step_into`` -> obs[t+1], reward[t], terminated,
+     truncated, terminal_obs (SB3 auto-reset inside the env kernel)
+  3. ``vn_collect_compact`` -> ordered indices of the truncated agents
+     (SB3: ``done and info["TimeLimit.truncated"]``); their terminal values
+     V(terminal_obs; critic state after step t) are computed on the gathered
+     rows and added as ``reward += gamma * V`` (``vn_collect_bootstrap``)
+  4. ``vn_episode_start`` -> episode_starts[t+1] = done, zero the (h, c) of
+     those agents (``_process_sequence``'s ``(1 - episode_start)`` mask)
+
+after T steps: V(obs[T]) under the current critic states, then the GAE scan
+(``vn_gae``) -> advantages, returns.
+
+Build-defined (documented in DESIGN.md): the Categorical draw uses a
+counter-based Philox stream keyed by (sample_seed, global agent id, global
+step) instead of torch's global generator, so a rollout is reproducible and
+independent of how agents are sharded over GPUs.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from dataclasses import dataclass
+from typing import Optional
+
+import torch
+
+from . import _native
+from .env import OBS_DIM, BatchedGridEnv
+from .policy import ActorCriticPolicy, RecurrentActorCriticPolicy
+
+
+def _p(t: Optional[torch.Tensor]):
+    return None if t is None else C.c_void_p(t.data_ptr())
+
+
+@dataclass
+class RolloutBuffer:
+    """SB3 (Recurrent)RolloutBuffer fields, [T, N]-major, on the GPU.
+
+    ``obs[t]`` is the observation the policy acted on at step t;
+    ``episode_starts[t]`` is SB3's ``_last_episode_starts`` at step t;
+    ``lstm_h / lstm_c [T, 2, N, H]`` are the (actor, critic) states entering
+    step t, before the episode-start mask (SB3 stores ``_last_lstm_states``).
+    """
+    obs: torch.Tensor
+    actions: torch.Tensor
+    rewards: torch.Tensor
+    episode_starts: torch.Tensor
+    values: torch.Tensor
+    log_probs: torch.Tensor
+    advantages: torch.Tensor
+    returns: torch.Tensor
+    lstm_h: Optional[torch.Tensor] = None
+    lstm_c: Optional[torch.Tensor] = None
+    last_values: Optional[torch.Tensor] = None
+    dones: Optional[torch.Tensor] = None
+
+
+class _Weights:
+    """The policy's parameters laid out for the collector's GEMMs/kernels."""
+
+    def __init__(self, policy, device):
+        f = lambda t: t.detach().to(device=device, dtype=torch.float32).contiguous()  # noqa: E731
+        self.recurrent = bool(getattr(policy, "recurrent", False))
+        if self.recurrent:
+            la, lc = policy.lstm_actor, policy.lstm_critic
+            if la.num_layers != 1 or lc.num_layers != 1:
+                raise NotImplementedError("one LSTM layer (Grid_Train's n_lstm_layers=1)")
+            self.H = la.hidden_size
+            self.w_ih_cat = torch.cat([f(la.weight_ih_l0), f(lc.weight_ih_l0)], 0)      # [2*4H, 80]
+            self.w_hh = [f(la.weight_hh_l0), f(lc.weight_hh_l0)]                       # [4H, H]
+            self.w_ih_vf = f(lc.weight_ih_l0)
+            self.b_ih = torch.stack([f(la.bias_ih_l0), f(lc.bias_ih_l0)])               # [2, 4H]
+            self.b_hh = torch.stack([f(la.bias_hh_l0), f(lc.bias_hh_l0)])
+        ext = policy.mlp_extractor
+        self.pi = [(f(m.weight), f(m.bias)) for m in ext.linears("pi")]
+        self.vf = [(f(m.weight), f(m.bias)) for m in ext.linears("vf")]
+        self.wa, self.ba = f(policy.action_net.weight), f(policy.action_net.bias)
+        self.wv, self.bv = f(policy.value_net.weight).reshape(-1), f(policy.value_net.bias)
+        self.A = self.wa.shape[0]
+        self.P = self.wa.shape[1]
+        if self.wv.shape[0] != self.P:
+            raise NotImplementedError("pi and vf latents must have the same width")
+
+
+def _mlp(layers, x):
+    for w, b in layers:
+        x = torch.addmm(b, x, w.t())
+        x.tanh_()
+    return x
+
+
+class RolloutCollector:
+    """``collect()`` fills a RolloutBuffer of ``n_steps`` x ``env.num_agents``.
+
+    ``policy``: ``RecurrentActorCriticPolicy`` (PPO-LSTM, Grid_Train) or
+    ``ActorCriticPolicy`` (PPO-MLP).  Its parameters are read at
+    construction and again by ``sync_weights()`` (after a learner update).
+    """
+
+    def __init__(self, env: BatchedGridEnv, policy, n_steps: int = 128, gamma: float = 0.99, gae_lambda: float = 0.95,
+                 sample_seed: int = 42, deterministic: bool = False, store_lstm_states: bool = True,
+                 reset_seed: int = 42):
+        if not isinstance(policy, (ActorCriticPolicy, RecurrentActorCriticPolicy)):
+            raise TypeError("policy must be an ActorCriticPolicy or RecurrentActorCriticPolicy")
+        if getattr(policy, "obs_dim", OBS_DIM) != OBS_DIM:
+            raise ValueError("policy obs_dim must be 80")
+        self.env = env
+        self.lib = env.lib
+        self.device = env.device
+        self.policy = policy
+        self.n_steps = int(n_steps)
+        self.gamma = float(gamma)
+        self.gae_lambda = float(gae_lambda)
+        self.sample_seed = int(sample_seed)
+        self.deterministic = bool(deterministic)
+        self.N = env.num_agents
+        self.t_global = 0
+        self.sync_weights()
+        T, N, dev = self.n_steps, self.N, self.device
+        z = lambda *s, dt=torch.float32: torch.zeros(s, dtype=dt, device=dev)  # noqa: E731
+        self._obs = z(T + 1, N, OBS_DIM)
+        self._starts = z(T + 1, N)
+        self.actions = z(T, N, dt=torch.int32)
+        self.rewards = z(T, N)
+        self.values = z(T, N)
+        self.log_probs = z(T, N)
+        self._term = z(N, dt=torch.uint8)
+        self._trunc = z(N, dt=torch.uint8)
+        self._tobs = z(N, OBS_DIM)
+        self._boot_idx = z(N, dt=torch.int32)
+        self._boot_cnt = z(1, dt=torch.int32)
+        self._boot_cnt_host = torch.zeros(1, dtype=torch.int32, pin_memory=True)
+        self._last_values = z(N)
+        self.recurrent = self.w.recurrent
+        if self.recurrent:
+            H = self.w.H
+            self.h = z(2, N, H)
+            self.c = z(2, N, H)
+            self._gx = z(N, 2 * 4 * H)
+            self._gh = z(2, N, 4 * H)
+            self.store = bool(store_lstm_states)
+            self._hs = z(T + 1, 2, N, H) if self.store else None
+            self._cs = z(T + 1, 2, N, H) if self.store else None
+        # learn() start: reset every env, episode_starts = ones, zero states
+        self._obs[0] = env.reset(seed=reset_seed)
+        self._starts[0].fill_(1.0)
+        self._carry = False
+
+    def sync_weights(self):
+        self.w = _Weights(self.policy, self.device)
+
+    def _stream(self):
+        return C.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
+
+    # -------------------------------------------------------------- policy
+    def _forward(self, obs: torch.Tensor, t: int):
+        """Policy step on obs [N, 80] into actions/values/log_probs[t]."""
+        w, lib, N = self.w, self.lib, self.N
+        if self.recurrent:
+            H = w.H
+            torch.mm(obs, w.w_ih_cat.t(), out=self._gx)
+            torch.mm(self.h[0], w.w_hh[0].t(), out=self._gh[0])
+            torch.mm(self.h[1], w.w_hh[1].t(), out=self._gh[1])
+            hs = self._hs[t + 1] if self.store else None
+            cs = self._cs[t + 1] if self.store else None
+            _native.check(lib.vn_lstm_cell(_p(self._gx), 8 * H, _p(self._gh), _p(w.b_ih), _p(w.b_hh), _p(self.h),
+                                           _p(self.c), _p(hs), _p(cs), 2, N, H, self._stream()), "vn_lstm_cell")
+            x_pi, x_vf = self.h[0], self.h[1]
+        else:
+            x_pi = x_vf = obs
+        lat_pi = _mlp(w.pi, x_pi)
+        lat_vf = _mlp(w.vf, x_vf)
+        _native.check(lib.vn_policy_head(_p(lat_pi), _p(lat_vf), N, w.P, _p(w.wa), _p(w.ba), w.A, _p(w.wv), _p(w.bv),
+                                         self.sample_seed, self.t_global, self.env.agent_id_base,
+                                         int(self.deterministic), _p(self.actions[t]), _p(self.values[t]),
+                                         _p(self.log_probs[t]), self._stream()), "vn_policy_head")
+
+    def _critic(self, obs: torch.Tensor, h: Optional[torch.Tensor], c: Optional[torch.Tensor], out: torch.Tensor):
+        """predict_values: one critic step from state (h, c) [M, H] (consumed), value -> out [M]."""
+        w, M = self.w, obs.shape[0]
+        if self.recurrent:
+            H = w.H
+            gx = torch.mm(obs, w.w_ih_vf.t())
+            gh = torch.mm(h, w.w_hh[1].t())
+            _native.check(self.lib.vn_lstm_cell(_p(gx), 4 * H, _p(gh), _p(w.b_ih[1]), _p(w.b_hh[1]), _p(h), _p(c),
+                                                None, None, 1, M, H, self._stream()), "vn_lstm_cell")
+            x = h
+        else:
+            x = obs
+        lat = _mlp(w.vf, x)
+        _native.check(self.lib.vn_policy_head(None, _p(lat), M, w.P, None, None, 0, _p(w.wv), _p(w.bv), 0, 0, 0, 0,
+                                              None, _p(out), None, self._stream()), "vn_policy_head")
+
+    # -------------------------------------------------------------- rollout
+    @torch.no_grad()
+    def collect(self) -> RolloutBuffer:
+        """One rollout of n_steps.  The returned buffer views the collector's
+        storage: it stays valid until the next ``collect()``."""
+        T, N, lib = self.n_steps, self.N, self.lib
+        s = self._stream
+        if self._carry:
+            self._carry_over()
+        for t in range(T):
+            self._forward(self._obs[t], t)
+            self.env.step_into(self.actions[t], self._obs[t + 1], self.rewards[t], self._term, self._trunc,
+                               self._tobs)
+            _native.check(lib.vn_collect_compact(_p(self._term), _p(self._trunc), N, _p(self._boot_idx),
+                                                 _p(self._boot_cnt), s()), "vn_collect_compact")
+            self._boot_cnt_host.copy_(self._boot_cnt, non_blocking=True)
+            torch.cuda.current_stream(self.device).synchronize()
+            M = int(self._boot_cnt_host[0])
+            if M:
+                idx = self._boot_idx[:M].long()
+                tv = torch.empty(M, dtype=torch.float32, device=self.device)
+                if self.recurrent:
+                    self._critic(self._tobs.index_select(0, idx), self.h[1].index_select(0, idx),
+                                 self.c[1].index_select(0, idx), tv)
+                else:
+                    self._critic(self._tobs.index_select(0, idx), None, None, tv)
+                _native.check(lib.vn_collect_bootstrap(_p(self._boot_idx), _p(tv), M, self.gamma,
+                                                       _p(self.rewards[t]), s()), "vn_collect_bootstrap")
+            _native.check(lib.vn_episode_start(_p(self._term), _p(self._trunc), N, _p(self._starts[t + 1]),
+                                               _p(self.h) if self.recurrent else None,
+                                               _p(self.c) if self.recurrent else None,
+                                               2 if self.recurrent else 0, self.w.H if self.recurrent else 0, s()),
+                          "vn_episode_start")
+            self.t_global += 1
+        # V(last obs) under the current (masked) critic state
+        if self.recurrent:
+            self._critic(self._obs[T], self.h[1].clone(), self.c[1].clone(), self._last_values)
+        else:
+            self._critic(self._obs[T], None, None, self._last_values)
+        adv = torch.empty((T, N), dtype=torch.float32, device=self.device)
+        ret = torch.empty((T, N), dtype=torch.float32, device=self.device)
+        _native.check(lib.vn_gae(_p(self.rewards), _p(self.values), _p(self._starts), _p(self._last_values),
+                                 _p(self._starts[T]), T, N, self.gamma, self.gae_lambda, _p(adv), _p(ret), s()),
+                      "vn_gae")
+        self._carry = True
+        hs = self._hs[:T] if self.recurrent and self.store else None
+        cs = self._cs[:T] if self.recurrent and self.store else None
+        return RolloutBuffer(obs=self._obs[:T], actions=self.actions, rewards=self.rewards,
+                             episode_starts=self._starts[:T], values=self.values, log_probs=self.log_probs,
+                             advantages=adv, returns=ret, lstm_h=hs, lstm_c=cs, last_values=self._last_values,
+                             dones=self._starts[T])
+
+    def _carry_over(self):
+        # the previous rollout's last obs / episode starts / lstm states become
+        # this rollout's first (_last_obs, _last_episode_starts, _last_lstm_states)
+        T = self.n_steps
+        self._obs[0].copy_(self._obs[T])
+        self._starts[0].copy_(self._starts[T])
+        if self.recurrent and self.store:
+            self._hs[0].copy_(self._hs[T])
+            self._cs[0].copy_(self._cs[T])
+        self._carry = False

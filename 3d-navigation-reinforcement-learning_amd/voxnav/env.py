@@ -169,6 +169,26 @@ class BatchedGridEnv:
                                        self._stream()), "vn_step")
         return StepResult(obs, rew, te.bool(), tr.bool(), tob)
 
+    def step_into(self, actions: torch.Tensor, obs: torch.Tensor, reward: torch.Tensor, terminated: torch.Tensor,
+                  truncated: torch.Tensor, terminal_obs: Optional[torch.Tensor] = None):
+        """``step`` writing into caller-owned device buffers (no allocation):
+        actions i32 [N], obs f32 [N, 80], reward f32 (or f64) [N],
+        terminated / truncated u8 [N], terminal_obs f32 [N, 80] or None."""
+        if not self._was_reset:
+            raise RuntimeError("call reset() before step()")
+        N = self.num_agents
+        for name, t, dt, shape in (("actions", actions, torch.int32, (N,)), ("obs", obs, torch.float32, (N, OBS_DIM)),
+                                   ("terminated", terminated, torch.uint8, (N,)),
+                                   ("truncated", truncated, torch.uint8, (N,))):
+            if t.dtype != dt or tuple(t.shape) != shape or not t.is_contiguous() or t.device != self.device:
+                raise ValueError(f"{name}: expected contiguous {dt} {shape} on {self.device}")
+        if reward.dtype not in (torch.float32, torch.float64) or tuple(reward.shape) != (N,) or not reward.is_contiguous():
+            raise ValueError("reward: expected contiguous f32/f64 [N]")
+        f64 = reward.dtype == torch.float64
+        _native.check(self.lib.vn_step(self._h, _ptr(actions), _ptr(obs), None if f64 else _ptr(reward),
+                                       _ptr(reward) if f64 else None, _ptr(terminated), _ptr(truncated),
+                                       _ptr(terminal_obs), self._stream()), "vn_step")
+
     def step_random(self, k_steps: int, policy_seed: int = 42, t0: Optional[int] = None, record_actions: bool = False,
                     reward_f64: bool = False, out: Optional[Rollout] = None) -> Rollout:
         """k fused steps under the build's Philox uniform random policy."""
@@ -201,7 +221,7 @@ class BatchedGridEnv:
         return {f: s[:, i] for i, f in enumerate(_native.STATE_FIELDS)}
 
     def belief(self) -> torch.Tensor:
-        """int8 [N, pad_w, pad_d, pad_h]; counts saturate at 127; -128 outside the room."""
+        """int8 [N, pad_w, pad_d, pad_h]; counts saturate at 63; -128 outside the room."""
         i = self.info
         out = torch.empty((self.num_agents, i.pad_w, i.pad_d, i.pad_h), dtype=torch.int8, device=self.device)
         _native.check(self.lib.vn_export_belief(self._h, _ptr(out), self._stream()), "vn_export_belief")

@@ -52,6 +52,11 @@ def parse():
     ap.add_argument("--single-step-check", type=int, default=1,
                     help="also time the drop-in one-step-per-launch call (vn_step_random k=1)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline sample budget (0 = skip)")
+    ap.add_argument("--collector", default="lstm", choices=["lstm", "mlp", "none"],
+                    help="also time the policy-in-the-loop rollout collector (PPO-LSTM / PPO-MLP)")
+    ap.add_argument("--collector-rooms", default="P3_training", help="reference room set for the collector leg")
+    ap.add_argument("--collector-T", type=int, default=128, help="rollout length (n_steps) of the collector leg")
+    ap.add_argument("--collector-rollouts", type=int, default=2, help="timed rollouts of the collector leg")
     ap.add_argument("--json-out", default=None)
     return ap.parse_args()
 
@@ -84,6 +89,71 @@ def cpu_baseline(room_whd, L, seconds):
     return {"value": steps / el, "unit": "env-steps/s", "cores": threads, "kind": "port",
             "sample": f"{N} agents x {steps // N} steps of the same workload ({el:.1f} s) through "
                       f"oracle/voxnav_oracle.c (C restatement of envs/CubicEnv.py, OpenMP over agents)"}
+
+
+def lstm_flops_per_agent_step(obs=80, H=256, arch=(256, 256, 128), A=6) -> int:
+    """PPO-LSTM forward: x@W_ih for 2 LSTMs, h@W_hh for 2,
+    the two Tanh MLPs and the heads, 2 FLOP per MAC."""
+    macs = 2 * obs * 4 * H + 2 * H * 4 * H
+    d = H
+    for w in arch:
+        macs += 2 * d * w
+        d = w
+    macs += d * (A + 1)
+    return 2 * macs
+
+
+def mlp_flops_per_agent_step(obs=80, arch=(256, 256, 128), A=6) -> int:
+    macs, d = 0, obs
+    for w in arch:
+        macs += 2 * d * w
+        d = w
+    macs += d * (A + 1)
+    return 2 * macs
+
+
+def collector_leg(args, torch, dist, dev, rank, world, N):
+    """Policy-in-the-loop rollouts (RecurrentPPO.collect_rollouts + GAE) on
+    the GPU: BASELINE.json config C4 shape (P3_training rooms, PPO-LSTM,
+    seq 128) at N agents per GPU.  One untimed rollout, then timed ones."""
+    from voxnav.collector import RolloutCollector
+    from voxnav.env import BatchedGridEnv
+    from voxnav.policy import ActorCriticPolicy, RecurrentActorCriticPolicy
+    from voxnav.rooms import load_archive_set
+    rooms = load_archive_set(args.collector_rooms)
+    torch.manual_seed(42)
+    pol = (RecurrentActorCriticPolicy() if args.collector == "lstm" else ActorCriticPolicy()).to(dev)
+    env = BatchedGridEnv(num_agents=N, rooms=rooms, local_map_length=args.L, autoreset=True, device=dev,
+                         agent_id_base=rank * N, seed_stride=N * world)
+    col = RolloutCollector(env, pol, n_steps=args.collector_T, sample_seed=42, reset_seed=42)
+    col.collect()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(args.collector_rollouts):
+        buf = col.collect()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([el], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t[0].item())
+    assert torch.isfinite(buf.advantages).all().item()
+    steps = args.collector_T * args.collector_rollouts
+    fl = lstm_flops_per_agent_step() if args.collector == "lstm" else mlp_flops_per_agent_step()
+    tflops = fl * N * steps / el / 1e12
+    name = ("PPO-LSTM (MlpLstmPolicy: actor+critic LSTM 256, pi/vf [256,256,128] Tanh)" if args.collector == "lstm"
+            else "PPO-MLP (MlpPolicy: pi/vf [256,256,128] Tanh)")
+    return {"value": round(N * world * steps / el, 1), "unit": "env-steps/s", "policy": name, "dtype": "f32",
+            "rooms": args.collector_rooms, "agents_per_gpu": N, "rollout_steps": args.collector_T,
+            "timed_rollouts": args.collector_rollouts, "ms_per_step": round(el * 1e3 / steps, 4),
+            "includes": "policy forward, Categorical draw, env step + auto-reset, truncation bootstrap, "
+                        "LSTM-state buffer stores, last values, GAE",
+            "policy_flops_per_agent_step": fl, "policy_tflops": round(tflops, 2),
+            "policy_frac_of_f32_peak": round(tflops / 157.3, 4)}
 
 
 def main():
@@ -144,6 +214,9 @@ def main():
         _, _, st1, el1, km1 = run(1, min(args.steps, 100), 10)
         single = {"value": round(N * world * st1 / el1, 1), "steps": st1, "kernel_avg_us": round(km1 * 1e3, 3)}
     out, warm_steps, steps_timed, elapsed, kern_ms = run(F, args.steps, args.warmup)
+    coll = None
+    if args.collector != "none":
+        coll = collector_leg(args, torch, dist, dev, rank, world, N)
 
     # sanity: the trajectory buffer holds real observations
     assert torch.isfinite(out.obs).all().item()
@@ -181,6 +254,8 @@ def main():
         }
         if single is not None:
             rec["drop_in_single_step"] = single   # vn_step-shaped call: one env step per launch
+        if coll is not None:
+            rec["collector"] = coll               # policy in the loop
         if world == 1 and args.cpu_seconds > 0:
             rec["cpu_baseline"] = cpu_baseline((W, D, H), args.L, args.cpu_seconds)
         line = json.dumps(rec)

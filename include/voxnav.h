@@ -127,8 +127,9 @@ int vn_step_random(VnEnv *env, uint64_t policy_seed, uint64_t t0, int32_t k_step
  * x, y, z, facing, last_action, step_count, visited_count, bump_count,
  * done, last_bump, near_wall, was_near_wall, cells_insight_down, room,
  * max_steps, next_seed.
- * belief_out: device i8 [N][pad_w][pad_d][pad_h] dense x-major; visit
- * counts saturate at 127, cells outside the agent's room read -128.
+ * belief_out: device i8 [N][pad_w][pad_d][pad_h] dense x-major, the
+ * reference's internal_grid values (-2 wall, -1 unknown, 0 free, n visits;
+ * visit counts saturate at 63), cells outside the agent's room read -128.
  */
 int vn_export_state(VnEnv *env, int64_t *state_out, void *stream);
 int vn_export_belief(VnEnv *env, int8_t *belief_out, void *stream);
@@ -141,6 +142,68 @@ int vn_export_belief(VnEnv *env, int8_t *belief_out, void *stream);
 int vn_gae(const float *rewards, const float *values, const float *episode_starts, const float *last_values,
            const float *dones, int32_t T, int32_t N, double gamma, double gae_lambda, float *advantages,
            float *returns, void *stream);
+
+/* ------------------------------------------------------------------------
+ * Rollout collector (sb3_contrib RecurrentPPO.collect_rollouts, reached
+ * from model.learn at train/Grid_Train.py:228; policy MlpLstmPolicy with
+ * net_arch pi/vf=[256,256,128], lstm_hidden_size=256, :68-80, :196-204).
+ * The GEMMs of the policy forward are library GEMMs issued by the caller;
+ * these entry points are everything in between.  All device f32 unless
+ * stated, stream-ordered.
+ * ---------------------------------------------------------------------- */
+
+/*
+ * One LSTM step for n_lstm independent LSTMs over N agents (torch nn.LSTM
+ * gate order i, f, g, o; RecurrentActorCriticPolicy._process_sequence):
+ *   pre = gx + gh + b_ih + b_hh;  c = f*c + i*g;  h = o*tanh(c)
+ *   gx       element (b, n, j) at gx[n*gx_row_stride + b*4H + j]  (x @ W_ih^T
+ *            for all LSTMs in one GEMM)
+ *   gh       [n_lstm][N][4H] (h @ W_hh^T) or NULL when the state is zero
+ *   b_ih, b_hh [n_lstm][4H];  h (out), c (in/out) [n_lstm][N][H]
+ *   h_store, c_store  [n_lstm][N][H] copies for the rollout buffer, or NULL
+ * H must be a multiple of 4.
+ */
+int vn_lstm_cell(const float *gx, int64_t gx_row_stride, const float *gh, const float *b_ih, const float *b_hh,
+                 float *h, float *c, float *h_store, float *c_store, int32_t n_lstm, int32_t N, int32_t H,
+                 void *stream);
+
+/*
+ * Action and value heads + Categorical draw (ActorCriticPolicy action_net /
+ * value_net and distribution.get_actions / log_prob).
+ *   latent_pi [N][P] (NULL: value only), latent_vf [N][P] (NULL: no value)
+ *   w_action [n_actions][P], b_action [n_actions], w_value [P], b_value [1]
+ *   actions (i32 [N]): Philox4x32-10(key=sample_seed, ctr=(agent_id_base+n,
+ *   t | 2^63)) word 0 -> u = (w >> 8) / 2^24, first a with u < cdf[a]
+ *   (argmax of the logits when deterministic); log_probs = logit - logsumexp.
+ * n_actions <= 8, P a multiple of 4.
+ */
+int vn_policy_head(const float *latent_pi, const float *latent_vf, int32_t N, int32_t P, const float *w_action,
+                   const float *b_action, int32_t n_actions, const float *w_value, const float *b_value,
+                   uint64_t sample_seed, uint64_t t, int64_t agent_id_base, int32_t deterministic, int32_t *actions,
+                   float *values, float *log_probs, void *stream);
+
+/*
+ * Ordered indices of the agents whose step was a time-limit truncation
+ * (SB3 VecEnv: done and info["TimeLimit.truncated"] = truncated and not
+ * terminated) -> boot_idx (device i32 [N]) and boot_count (device i32 [1]).
+ */
+int vn_collect_compact(const uint8_t *terminated, const uint8_t *truncated, int32_t N, int32_t *boot_idx,
+                       int32_t *boot_count, void *stream);
+
+/*
+ * Truncation bootstrap: rewards[boot_idx[i]] += gamma * terminal_values[i]
+ * for i < M (f32, two roundings, as collect_rollouts' numpy update).
+ */
+int vn_collect_bootstrap(const int32_t *boot_idx, const float *terminal_values, int32_t M, double gamma,
+                         float *rewards, void *stream);
+
+/*
+ * episode_starts[n] = terminated[n] | truncated[n] (f32 0/1, may be NULL)
+ * and, for those agents, zero the LSTM state rows h, c [n_lstm][N][H]
+ * (n_lstm = 0: no recurrent state).
+ */
+int vn_episode_start(const uint8_t *terminated, const uint8_t *truncated, int32_t N, float *episode_starts,
+                     float *h, float *c, int32_t n_lstm, int32_t H, void *stream);
 
 #ifdef __cplusplus
 }

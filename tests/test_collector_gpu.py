@@ -1,0 +1,192 @@
+"""Parity of the on-device rollout collector (voxnav.collector) on the GPU.
+
+Env outputs (obs bytes, terminated/truncated, f32 rewards before the
+bootstrap) are bit-exact against the C oracle replaying the collector's
+actions; the float policy quantities are compared with the float64 oracle
+(oracle/collector_oracle.py) within stated tolerances:
+
+  values, log-probs, LSTM states       |gpu - f64| <= 1e-4 + 1e-4 |f64|
+  bootstrapped rewards                  |gpu - f64| <= 1e-4 + 1e-5 |f64|
+  advantages / returns (f64 GAE)        |gpu - f64| <= 2e-3 + 1e-4 |f64|
+  sampled actions                       equal, or u within 1e-5 of a cdf
+                                        boundary (f32 vs f64 rounding)
+and the GAE kernel bit-exact against the f32 oracle on the GPU's own
+rewards/values.  The kernels alone are compared with the plain-PyTorch f32
+policy (voxnav.policy.forward_torch) at 2e-5.
+"""
+import numpy as np
+import pytest
+
+from helpers import box_text
+
+torch = pytest.importorskip("torch")
+pytestmark = pytest.mark.gpu
+
+BOXES = [(8, 8, 4), (6, 6, 4), (7, 5, 5), (5, 5, 4)]     # 72 / 32 / 45 / 18 free cells
+
+
+@pytest.fixture(scope="module")
+def voxnav():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    import voxnav
+    voxnav.load_library()
+    return voxnav
+
+
+def _rooms():
+    from voxnav.rooms import RoomSet, parse_room
+    from oracle.oracle import parse_room_text
+    texts = [(f"box{w}x{d}x{h}.txt", box_text(w, d, h)) for (w, d, h) in BOXES]
+    prod = RoomSet([parse_room(t, n) for n, t in texts], use_room_draw=True, source="test-boxes")
+    orc = [parse_room_text(t, n) for n, t in texts]
+    return prod, orc
+
+
+def _close(a, b, atol, rtol, what):
+    a = np.asarray(a, np.float64)
+    b = np.asarray(b, np.float64)
+    bad = np.abs(a - b) > atol + rtol * np.abs(b)
+    assert not bad.any(), f"{what}: {bad.sum()} of {bad.size} out of tolerance, max err {np.abs(a - b).max():.3g}"
+
+
+def _policy(kind):
+    from voxnav.policy import ActorCriticPolicy, RecurrentActorCriticPolicy
+    torch.manual_seed(7)
+    pol = RecurrentActorCriticPolicy() if kind == "lstm" else ActorCriticPolicy()
+    # larger head weights than SB3's 0.01 init so the draws are not ~uniform
+    with torch.no_grad():
+        pol.action_net.weight.mul_(100.0)
+        pol.action_net.bias.uniform_(-0.5, 0.5)
+        pol.value_net.bias.fill_(0.3)
+    return pol
+
+
+@pytest.mark.parametrize("kind,T,rollouts", [("lstm", 48, 2), ("mlp", 80, 1)])
+def test_collector_matches_oracle(voxnav, kind, T, rollouts):
+    from oracle import collector_oracle as co
+    from oracle.oracle import OracleEnv, gae as gae32
+    from voxnav.collector import RolloutCollector
+    from voxnav.env import BatchedGridEnv
+    from voxnav.policy import numpy_weights
+    N, L = 64, 4
+    prod, orooms = _rooms()
+    pol = _policy(kind)
+    env = BatchedGridEnv(num_agents=N, rooms=prod, local_map_length=L, device="cuda:0")
+    col = RolloutCollector(env, pol.to("cuda:0"), n_steps=T, sample_seed=1234, reset_seed=42)
+    orc = co.PolicyOracle(numpy_weights(pol))
+    oenv = OracleEnv(orooms, n_agents=N, local_map_length=L)
+    seeds = 42 + np.arange(N)
+    # reset observations
+    ref = OracleEnv(orooms, n_agents=N, local_map_length=L)
+    obs0 = np.stack([ref.reset(i, int(seeds[i])) for i in range(N)])
+    assert col._obs[0].cpu().numpy().tobytes() == obs0.tobytes()
+    starts0 = np.ones(N, np.float32)
+    h = c = None
+    total_boot = 0
+    for r in range(rollouts):
+        buf = col.collect()
+        torch.cuda.synchronize()
+        acts = buf.actions.cpu().numpy()
+        rr = oenv.run_random(seeds, 0, T, t0=r * T, seed_stride=N, initial_reset=(r == 0), actions=acts,
+                             terminal_obs=True)
+        gobs = buf.obs.cpu().numpy()
+        assert gobs[1:].tobytes() == rr["obs"][:-1].tobytes(), "env obs"
+        assert col._obs[T].cpu().numpy().tobytes() == rr["obs"][-1].tobytes()
+        out = co.collect(orc, rr, gobs[0], starts0, acts, gamma=0.99, h0=h, c0=c, sample_seed=1234, t0=r * T)
+        h, c, starts0 = out["h"], out["c"], out["dones"]
+        te, tr = rr["terminated"].astype(bool), rr["truncated"].astype(bool)
+        total_boot += int((tr & ~te).sum())
+        np.testing.assert_array_equal(buf.episode_starts.cpu().numpy(), out["episode_starts"])
+        np.testing.assert_array_equal(buf.dones.cpu().numpy(), out["dones"])
+        _close(buf.values.cpu(), out["values"], 1e-4, 1e-4, "values")
+        _close(buf.log_probs.cpu(), out["log_probs"], 1e-4, 1e-4, "log_probs")
+        _close(buf.rewards.cpu(), out["rewards"], 1e-4, 1e-5, "rewards")
+        _close(buf.last_values.cpu(), out["last_values"], 1e-4, 1e-4, "last_values")
+        # unbootstrapped rewards are the env's f32 rewards exactly
+        plain = ~(tr & ~te)
+        assert np.array_equal(buf.rewards.cpu().numpy()[plain], rr["reward"].astype(np.float32)[plain])
+        mism = acts != out["oracle_actions"]
+        assert np.all(out["margins"][mism] < 1e-5), f"{mism.sum()} action draws differ away from a cdf boundary"
+        assert mism.sum() <= 2
+        # GAE: bit-exact vs the f32 restatement on the GPU's own inputs; close to f64
+        a32, r32 = gae32(buf.rewards.cpu().numpy(), buf.values.cpu().numpy(), buf.episode_starts.cpu().numpy(),
+                         buf.last_values.cpu().numpy(), buf.dones.cpu().numpy())
+        assert buf.advantages.cpu().numpy().tobytes() == a32.tobytes()
+        assert buf.returns.cpu().numpy().tobytes() == r32.tobytes()
+        a64, r64 = co.gae64(out["rewards"].astype(np.float64), out["values"], out["episode_starts"],
+                            out["last_values"], out["dones"])
+        _close(buf.advantages.cpu(), a64, 2e-3, 1e-4, "advantages")
+        _close(buf.returns.cpu(), r64, 2e-3, 1e-4, "returns")
+        if kind == "lstm":
+            _close(col.h.cpu(), h, 1e-4, 1e-4, "h")
+            _close(col.c.cpu(), c, 1e-4, 1e-4, "c")
+            # stored states entering step t: zero at learn() start
+            if r == 0:
+                assert float(buf.lstm_h[0].abs().max()) == 0.0
+    assert total_boot > 0, "the test rooms must produce truncations inside the rollout"
+
+
+def test_kernels_match_torch_fp32(voxnav):
+    """vn_lstm_cell + vn_policy_head (through the collector's forward) vs nn.LSTM/nn.Linear."""
+    from voxnav.collector import RolloutCollector
+    from voxnav.env import BatchedGridEnv
+    N = 300
+    prod, _ = _rooms()
+    pol = _policy("lstm").to("cuda:0")
+    env = BatchedGridEnv(num_agents=N, rooms=prod, local_map_length=4, device="cuda:0")
+    col = RolloutCollector(env, pol, n_steps=4)
+    g = torch.Generator(device="cuda:0").manual_seed(5)
+    obs = torch.rand((N, 80), device="cuda:0", generator=g)
+    h = torch.randn((2, N, 256), device="cuda:0", generator=g) * 0.5
+    c = torch.randn((2, N, 256), device="cuda:0", generator=g) * 0.5
+    col.h.copy_(h)
+    col.c.copy_(c)
+    col._forward(obs, 0)
+    lg, v, h2, c2 = pol.forward_torch(obs, h, c)
+    lsm = torch.log_softmax(lg, 1)
+    a = col.actions[0].long()
+    _close(col.values[0].cpu(), v.cpu(), 2e-5, 2e-5, "values")
+    _close(col.log_probs[0].cpu(), lsm.gather(1, a[:, None])[:, 0].cpu(), 2e-5, 2e-5, "log_probs")
+    _close(col.h.cpu(), h2.cpu(), 2e-5, 2e-5, "h")
+    _close(col.c.cpu(), c2.cpu(), 2e-5, 2e-5, "c")
+    # deterministic mode = argmax of the logits
+    col.deterministic = True
+    col.h.copy_(h)
+    col.c.copy_(c)
+    col._forward(obs, 1)
+    assert torch.equal(col.actions[1].long(), lg.argmax(1))
+
+
+def test_compaction_and_episode_start(voxnav):
+    import ctypes as C
+    lib = voxnav.load_library()
+    rng = np.random.default_rng(11)
+    for N in (1, 63, 1000, 70001):
+        te = torch.from_numpy((rng.random(N) < 0.05).astype(np.uint8)).cuda()
+        tr = torch.from_numpy((rng.random(N) < 0.1).astype(np.uint8)).cuda()
+        idx = torch.full((N,), -1, dtype=torch.int32, device="cuda")
+        cnt = torch.zeros(1, dtype=torch.int32, device="cuda")
+        p = lambda t: C.c_void_p(t.data_ptr())  # noqa: E731
+        assert lib.vn_collect_compact(p(te), p(tr), N, p(idx), p(cnt), None) == 0
+        want = np.nonzero((tr.cpu().numpy() == 1) & (te.cpu().numpy() == 0))[0]
+        M = int(cnt.item())
+        assert M == len(want)
+        assert np.array_equal(idx[:M].cpu().numpy(), want)
+        H = 8
+        h = torch.ones((2, N, H), device="cuda")
+        c = torch.ones((2, N, H), device="cuda")
+        st = torch.full((N,), 7.0, device="cuda")
+        assert lib.vn_episode_start(p(te), p(tr), N, p(st), p(h), p(c), 2, H, None) == 0
+        done = (te | tr).bool().cpu().numpy()
+        assert np.array_equal(st.cpu().numpy(), done.astype(np.float32))
+        assert float(h[:, done].abs().sum()) == 0.0 and bool((h[:, ~done] == 1).all())
+        assert float(c[:, done].abs().sum()) == 0.0 and bool((c[:, ~done] == 1).all())
+        # bootstrap add: two f32 roundings
+        rew = torch.from_numpy(rng.standard_normal(N).astype(np.float32)).cuda()
+        tv = torch.from_numpy(rng.standard_normal(max(M, 1)).astype(np.float32)).cuda()
+        want_r = rew.cpu().numpy().copy()
+        gv = (np.float32(0.99) * tv.cpu().numpy()[:M]).astype(np.float32)
+        want_r[want] = (want_r[want] + gv).astype(np.float32)
+        assert lib.vn_collect_bootstrap(p(idx), p(tv), M, C.c_double(0.99), p(rew), None) == 0
+        assert rew.cpu().numpy().tobytes() == want_r.tobytes()
