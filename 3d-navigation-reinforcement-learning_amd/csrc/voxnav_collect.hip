@@ -233,20 +233,46 @@ __global__ __launch_bounds__(256) void policy_head_kernel(const float *__restric
 // Ordered compaction of the envs whose step was a time-limit truncation:
 // SB3 bootstraps `done and info["TimeLimit.truncated"]`, where the VecEnv
 // wrapper sets TimeLimit.truncated = truncated and not terminated.
-// One 1024-thread block; each thread owns a contiguous chunk; a block-wide
-// exclusive scan of the chunk counts keeps the agent order, so the gathered
-// batch (and its GEMM) is the same for every run.
+// One 1024-thread block; thread i owns the 16-byte-aligned chunks i,
+// i+1024, ... of the flag arrays (one uint4 load per array per chunk; the
+// flags are 0/1 bytes, so a chunk's boot mask is tr & ~te & 0x01 per byte).
+// A block-wide exclusive scan of the per-thread counts orders the output by
+// agent index, so the gathered batch (and its GEMM) is the same every run.
 // ----------------------------------------------------------------------------
+__device__ __forceinline__ uint4 boot_bytes(const uint8_t *__restrict__ term, const uint8_t *__restrict__ trunc,
+                                            int base, int N) {
+    uint4 m;
+    if (base + 16 <= N) {
+        const uint4 te = *reinterpret_cast<const uint4 *>(term + base);
+        const uint4 tr = *reinterpret_cast<const uint4 *>(trunc + base);
+        m.x = tr.x & ~te.x & 0x01010101u;
+        m.y = tr.y & ~te.y & 0x01010101u;
+        m.z = tr.z & ~te.z & 0x01010101u;
+        m.w = tr.w & ~te.w & 0x01010101u;
+    } else {
+        uint32_t w[4] = {0u, 0u, 0u, 0u};
+        for (int k = 0; k < 16 && base + k < N; ++k)
+            w[k >> 2] |= (uint32_t)((trunc[base + k] != 0) & (term[base + k] == 0)) << (8 * (k & 3));
+        m = make_uint4(w[0], w[1], w[2], w[3]);
+    }
+    return m;
+}
+
 __global__ __launch_bounds__(1024) void boot_compact_kernel(const uint8_t *__restrict__ term,
                                                             const uint8_t *__restrict__ trunc, int N,
                                                             int32_t *__restrict__ idx, int32_t *__restrict__ count) {
     __shared__ int wsum[16];
     const int tid = threadIdx.x;
-    const int chunk = (N + 1023) / 1024;
-    const int lo = min(N, tid * chunk), hi = min(N, lo + chunk);
+    const int nchunk = (N + 15) >> 4;
+    // thread tid owns chunks [c0, c1): contiguous, so the output order is
+    // the agent order after the scan
+    const int per = (nchunk + 1023) >> 10;
+    const int c0 = min(nchunk, tid * per), c1 = min(nchunk, c0 + per);
     int cnt = 0;
-    for (int i = lo; i < hi; ++i) cnt += (trunc[i] != 0) & (term[i] == 0);
-    // inclusive scan within the wave
+    for (int ch = c0; ch < c1; ++ch) {
+        const uint4 m = boot_bytes(term, trunc, ch << 4, N);
+        cnt += __popc(m.x) + __popc(m.y) + __popc(m.z) + __popc(m.w);
+    }
     const int lane = tid & 63, wv = tid >> 6;
     int inc = cnt;
 #pragma unroll
@@ -266,9 +292,21 @@ __global__ __launch_bounds__(1024) void boot_compact_kernel(const uint8_t *__res
         *count = run;
     }
     __syncthreads();
+    if (cnt == 0) return;
     int pos = wsum[wv] + inc - cnt;
-    for (int i = lo; i < hi; ++i)
-        if ((trunc[i] != 0) & (term[i] == 0)) idx[pos++] = i;
+    for (int ch = c0; ch < c1; ++ch) {
+        const uint4 m = boot_bytes(term, trunc, ch << 4, N);
+        const uint32_t w[4] = {m.x, m.y, m.z, m.w};
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            uint32_t b = w[q];
+            while (b) {
+                const int bit = __ffs(b) - 1;
+                idx[pos++] = (ch << 4) + q * 4 + (bit >> 3);
+                b &= b - 1;
+            }
+        }
+    }
 }
 
 // rewards[idx[i]] = rewards[idx[i]] + (gamma * v[i])   (two f32 roundings,
@@ -355,6 +393,8 @@ int vn_collect_compact(const uint8_t *terminated, const uint8_t *truncated, int3
                        int32_t *boot_count, void *stream) {
     if (!terminated || !truncated || !boot_idx || !boot_count) return fail(VN_ERR_INVALID, "NULL argument");
     if (N < 1) return fail(VN_ERR_INVALID, "N must be >= 1 (got %d)", N);
+    if (((uintptr_t)terminated | (uintptr_t)truncated) & 15)
+        return fail(VN_ERR_INVALID, "terminated / truncated must be 16-byte aligned");
     hipLaunchKernelGGL(boot_compact_kernel, dim3(1), dim3(1024), 0, (hipStream_t)stream, terminated, truncated,
                        (int)N, boot_idx, boot_count);
     VN_HIP(hipGetLastError());

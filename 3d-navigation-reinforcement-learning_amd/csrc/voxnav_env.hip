@@ -65,13 +65,14 @@ struct RoomDesc {          // 32 B, two uint4
     int32_t fixed_start;   // packed "Start position" or -1
     uint32_t bricks;       // ceil(W/4) | ceil(D/4)<<16
     uint32_t finish_visits;// smallest visited count with visited/total >= finish (f64)
-    uint32_t pad1;
+    int32_t fixed_goal;    // packed "Goal" (simpleEnv) or -1
 };
 
 struct Room {
     int W, D, H;
     uint32_t total_free, ray_off, start_off, finish_visits;
     int32_t fixed_start;
+    int32_t fixed_goal;
     int nbx, nby;
 };
 
@@ -123,6 +124,9 @@ struct Params {
     const int64_t *seeds;    // reset-only launches
     const uint8_t *mask;
     uint32_t ablate;         // diagnostics only (VOXNAV_ABLATE): skip parts of the step, results invalid
+    // simpleEnv variant
+    int variant, obs_dim, pd;
+    uint32_t *goal;          // per agent gx | gy<<8 | gz<<16
 };
 
 __device__ __forceinline__ Agent unpack(uint4 s) {
@@ -170,6 +174,7 @@ __device__ __forceinline__ Room load_room(const Params &p, int r) {
     R.nbx = b.y & 0xffff;
     R.nby = b.y >> 16;
     R.finish_visits = b.z;
+    R.fixed_goal = (int32_t)b.w;
     return R;
 }
 
@@ -811,6 +816,7 @@ __device__ __forceinline__ Room load_room_c(const EnvConst *ec, int r) {
     R.nbx = b.y & 0xffff;
     R.nby = b.y >> 16;
     R.finish_visits = b.z;
+    R.fixed_goal = (int32_t)b.w;
     return R;
 }
 
@@ -1060,6 +1066,243 @@ __global__ __launch_bounds__(BLOCK, VN_MIN_WAVES_PER_SIMD) void env_kernel(Param
     }
 }
 
+// ============================================================================
+// simpleEnv variant (envs/simpleEnv.py): walls are
+// the room file's `2` tokens, the belief map holds the reference's
+// internal_grid values as int8 (-1 unknown, 0 free, 1 visited, 2 wall),
+// dense per agent [pd-major: x][y][z] with z contiguous (PH bytes).  The
+// observation is 6 rays x L belief values + 6 distances + last_action
+// (obs_dim = 6L + 7).  One lane per agent, 64 agents per block; obs rows are
+// staged in LDS and written as one contiguous span per block.
+// ============================================================================
+
+// absolute ray directions of the relative moves (envs/simpleEnv.py:153-158,
+// :224-231) in the ray-record byte order 0:+x 1:-x 2:+y 3:-y 4:+z 5:-z
+__constant__ int8_t c_rel_dir[4][4] = {
+    {2, 0, 3, 1},   // forward  (N, E, S, W)
+    {0, 3, 1, 2},   // right
+    {3, 1, 2, 0},   // backward
+    {1, 2, 0, 3},   // left
+};
+__constant__ int8_t c_facing_of[4] = {1, 3, 0, 2};   // +x -> east(1), -x -> west(3), +y -> north(0), -y -> south(2)
+
+// MT draws of simpleEnv's load_room (:350, :410-426): room, start (drawn if
+// absent or on a wall), goal (drawn if absent or on a wall).  Returns
+// (start | room<<24, goal).
+__device__ __noinline__ uint2 simple_draw(const EnvConst *ec, uint32_t seed) {
+    MtStream mt;
+    mt.seed = seed;
+    mt.used = 0;
+    mt.err = ec->err;
+    mt_first_outputs(seed, mt.buf);
+    const int room = ec->use_room_draw ? (int)mt.below((uint32_t)ec->n_rooms) : 0;
+    const Room R = load_room_c(ec, room);
+    auto is_wall = [&](uint32_t c) {
+        const int x = c & 0xff, y = (c >> 8) & 0xff, z = (c >> 16) & 0xff;
+        return ((ec->rays[R.ray_off + (uint32_t)((x * R.D + y) * R.H + z)].y >> 16) & 1u) != 0u;
+    };
+    uint32_t s = R.fixed_start >= 0 ? (uint32_t)R.fixed_start : ec->starts[R.start_off + mt.below(R.total_free)];
+    if (is_wall(s)) s = ec->starts[R.start_off + mt.below(R.total_free)];
+    uint32_t gl = R.fixed_goal >= 0 ? (uint32_t)R.fixed_goal : ec->starts[R.start_off + mt.below(R.total_free)];
+    if (is_wall(gl)) gl = ec->starts[R.start_off + mt.below(R.total_free)];
+    return make_uint2((s & 0xffffffu) | ((uint32_t)room << 24), gl & 0xffffffu);
+}
+
+// _sense_direction (:301-337) along absolute direction d from the agent's
+// cell, using the cell's ray record (free run n to the first wall / edge).
+// Writes L obs values, returns the distance count * 0.25.
+__device__ __forceinline__ float simple_ray(int8_t *map, const Params &p, int cell, uint2 rec, int d, float *out) {
+    const uint32_t e8 = ((d < 4 ? rec.x : rec.y) >> (8 * (d & 3))) & 0xffu;
+    const int n = (int)(e8 & 0x7fu);
+    const bool at_wall = (e8 & 0x80u) != 0u;
+    const int L = p.L;
+    const int sx = p.pd * p.ph, sy = p.ph;
+    const int stride = d == 0 ? sx : d == 1 ? -sx : d == 2 ? sy : d == 3 ? -sy : d == 4 ? 1 : -1;
+    const int m = n < L ? n : L;
+    int c = cell;
+    for (int s = 0; s < m; ++s) {
+        c += stride;
+        int v = map[c];
+        if (v == -1) {           // unknown -> known free (:328-329)
+            map[c] = 0;
+            v = 0;
+        }
+        out[s] = (float)v;
+    }
+    if (n < L) {
+        if (at_wall) map[c + stride] = 2;   // first wall (:321-324)
+        else if (n >= 1) map[c] = 2;        // edge: the last in-room cell becomes a wall (:311-319)
+        out[n] = 2.0f;
+        for (int s = n + 1; s < L; ++s) out[s] = -1.0f;
+    }
+    return (float)((double)m * 0.25);       // round(count * cell_size, 2) (:337)
+}
+
+__device__ __forceinline__ void simple_observe(int8_t *map, const Params &p, const Agent &g, const Room &R,
+                                               float *row) {
+    const uint2 rec = p.rays[R.ray_off + (uint32_t)((g.x * R.D + g.y) * R.H + g.z)];
+    const int cell = (g.x * p.pd + g.y) * p.ph + g.z;
+    const int L = p.L;
+    const int dirs[6] = {c_rel_dir[0][g.facing], c_rel_dir[3][g.facing], c_rel_dir[1][g.facing],
+                         c_rel_dir[2][g.facing], 4, 5};   // forward, left, right, backward, up, down (:233)
+#pragma unroll
+    for (int k = 0; k < 6; ++k) row[6 * L + k] = simple_ray(map, p, cell, rec, dirs[k], row + k * L);
+    row[6 * L + 6] = (float)g.last_action;
+}
+
+// reset for the lanes with `need`: draws, the wave clears every resetting
+// agent's map rows x < W (all 64 lanes per agent, 8-byte stores), then each
+// agent marks its start cell visited and senses (reset + get_obs(), as the
+// reference's callers do, train/evaluate_grid.py:54-55).
+__device__ void simple_reset_wave(const Params &p, int8_t *map, bool need, uint32_t seed, Agent &g,
+                                  uint32_t &goal, Room &R, float *row, int lane, int block_agent0) {
+    uint2 drawn = make_uint2(0u, 0u);
+    if (need) drawn = simple_draw(p.envc, seed);
+    uint64_t m = __ballot(need);
+    while (m) {
+        const int src = __ffsll((unsigned long long)m) - 1;
+        m &= m - 1;
+        const int room = __shfl((int)(drawn.x >> 24), src);
+        const Room Rr = load_room(p, room);
+        uint64_t *base = reinterpret_cast<uint64_t *>(p.belief + (size_t)(block_agent0 + src) * p.agent_bytes);
+        const uint32_t words = (uint32_t)(Rr.W * p.pd * p.ph) >> 3;
+        for (uint32_t w = (uint32_t)lane; w < words; w += 64u) base[w] = ~0ull;   // -1 = unknown (:85)
+    }
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+    if (need) {
+        g.room = (int)(drawn.x >> 24);
+        R = load_room(p, g.room);
+        g.x = drawn.x & 0xff;
+        g.y = (drawn.x >> 8) & 0xff;
+        g.z = (drawn.x >> 16) & 0xff;
+        goal = drawn.y;
+        g.facing = 0;
+        g.last_action = 0;
+        g.done = g.last_bump = g.near_wall = g.was_near_wall = false;
+        g.step_count = 0;
+        g.visited = 1;
+        g.bumps = 0;
+        g.cid = 0;
+        g.move_mask = 0;
+        map[(g.x * p.pd + g.y) * p.ph + g.z] = 1;                              // :86
+        simple_observe(map, p, g, R, row);
+    }
+}
+
+template <bool RESET_ONLY>
+__global__ __launch_bounds__(64) void simple_kernel(Params p) {
+    extern __shared__ float sstage[];   // [64][obs_dim]
+    const int lane = threadIdx.x;
+    const int a0 = blockIdx.x * 64;
+    const int ai = a0 + lane;
+    const bool live = ai < p.N;
+    const int OD = p.obs_dim, L = p.L;
+    const int rows = min(64, p.N - a0);
+    float *row = sstage + lane * OD;
+    int8_t *map = p.belief + (size_t)(live ? ai : a0) * p.agent_bytes;
+    Agent g = unpack(live ? p.hot[ai] : make_uint4(0u, 0u, 0u, 0u));
+    uint32_t goal = live ? p.goal[ai] : 0u;
+    uint32_t next_seed = live ? p.next_seed[ai] : 0u;
+    Room R = load_room(p, g.room);
+
+    if (RESET_ONLY) {
+        const bool need = live && (!p.mask || p.mask[ai]);
+        const uint32_t seed = need ? (uint32_t)p.seeds[ai] : 0u;
+        simple_reset_wave(p, map, need, seed, g, goal, R, row, lane, a0);
+        if (need) {
+            float *o = p.obs + (size_t)ai * OD;
+            for (int k = 0; k < OD; ++k) o[k] = row[k];
+            p.hot[ai] = pack(g);
+            p.goal[ai] = goal;
+            p.next_seed[ai] = seed + p.seed_stride;   // modulo 2^32
+        }
+        return;
+    }
+
+    for (int k = 0; k < p.K; ++k) {
+        const uint64_t t = p.t0 + (uint64_t)k;
+        int a = 0;
+        if (live) {
+            if (p.actions) {
+                a = p.actions[(size_t)k * p.N + ai];
+            } else {
+                const uint4 w = philox4x32_10(p.policy_seed, p.gid_base + (uint64_t)ai, t >> 2);
+                const uint32_t word = (t & 3) == 0 ? w.x : (t & 3) == 1 ? w.y : (t & 3) == 2 ? w.z : w.w;
+                a = (int)(((uint64_t)word * 6u) >> 32);
+            }
+            if (p.actions_out) p.actions_out[(size_t)k * p.N + ai] = a;
+        }
+        bool trunc = false, term = false;
+        double r = 0.0;
+        if (live) {
+            // step (:109-150)
+            g.step_count += 1;
+            trunc = g.step_count >= R.total_free;                      // :111, max_steps = total_free (:409)
+            const int d = a < 4 ? c_rel_dir[a][g.facing] : (a == 4 ? 4 : 5);
+            if (a < 4) g.facing = c_facing_of[d];                        // :164-171
+            const uint2 rec = p.rays[R.ray_off + (uint32_t)((g.x * R.D + g.y) * R.H + g.z)];
+            const uint32_t e8 = ((d < 4 ? rec.x : rec.y) >> (8 * (d & 3))) & 0x7fu;
+            bool bumped = false, explored = false;
+            if (e8 >= 1u) {                                              // _mark_visited (:273-298)
+                g.x += d == 0 ? 1 : d == 1 ? -1 : 0;
+                g.y += d == 2 ? 1 : d == 3 ? -1 : 0;
+                g.z += d == 4 ? 1 : d == 5 ? -1 : 0;
+                int8_t *c = map + (g.x * p.pd + g.y) * p.ph + g.z;
+                const int v = *c;
+                if (v == 0 || v == -1) {
+                    *c = 1;
+                    g.visited += 1;
+                    explored = true;
+                }
+            } else {
+                bumped = true;
+            }
+            g.last_action = a;                                           // :137
+            simple_observe(map, p, g, R, row);                           // :139
+            // compute_reward (:189-217), f64 in the reference's order
+            r = -0.1;
+            if (bumped) {
+                g.bumps += 1;
+                r += -10.0;
+            }
+            if (a != 2 && a < 4) r += 0.05;                              // last_action == a here
+            const int gx = goal & 0xff, gy = (goal >> 8) & 0xff, gz = (goal >> 16) & 0xff;
+            if (g.x == gx && g.y == gy && g.z >= gz && g.z - gz < 5) {   // SPOT_GOAL_HEIGTH = 5 (:201-206)
+                g.done = true;
+                r += 100.0;
+            }
+            if (trunc) r += 0.0;                                         // r += -0
+            if (explored) r += 1.0;
+            term = g.done;
+            const size_t o = (size_t)k * p.N + ai;
+            if (p.reward) p.reward[o] = (float)r;
+            if (p.reward64) p.reward64[o] = r;
+            if (p.term) p.term[o] = term;
+            if (p.trunc) p.trunc[o] = trunc;
+            if ((term || trunc) && p.autoreset && p.terminal_obs) {
+                float *to = p.terminal_obs + o * OD;
+                for (int q = 0; q < OD; ++q) to[q] = row[q];
+            }
+        }
+        // SB3 VecEnv auto-reset
+        const bool need = live && p.autoreset && (term || trunc);
+        if (__ballot(need)) {
+            simple_reset_wave(p, map, need, next_seed, g, goal, R, row, lane, a0);
+            if (need) next_seed += p.seed_stride;
+        }
+        __syncthreads();
+        float *dst = p.obs + ((size_t)k * p.N + a0) * OD;
+        for (int q = lane; q < rows * OD; q += 64) dst[q] = sstage[q];
+        __syncthreads();
+    }
+    if (live) {
+        p.hot[ai] = pack(g);
+        p.goal[ai] = goal;
+        p.next_seed[ai] = next_seed;
+    }
+    (void)L;
+}
+
 // ----------------------------------------------------------------------------
 // exports (parity dumps)
 // ----------------------------------------------------------------------------
@@ -1073,6 +1316,10 @@ __global__ void export_state_kernel(Params p, int64_t *out) {
     o[5] = g.step_count; o[6] = g.visited; o[7] = g.bumps;
     o[8] = g.done; o[9] = g.last_bump; o[10] = g.near_wall; o[11] = g.was_near_wall;
     o[12] = g.cid; o[13] = g.room; o[14] = R.total_free; o[15] = p.next_seed[i];
+    if (p.variant == VN_VARIANT_SIMPLE) {
+        const uint32_t gl = p.goal[i];
+        o[9] = gl & 0xff; o[10] = (gl >> 8) & 0xff; o[11] = (gl >> 16) & 0xff; o[12] = 0;
+    }
 }
 
 __global__ void export_belief_kernel(Params p, int8_t *out, int pw, int pd) {
@@ -1085,7 +1332,9 @@ __global__ void export_belief_kernel(Params p, int8_t *out, int pw, int pd) {
     const Agent g = unpack(p.hot[i]);
     const Room R = load_room(p, g.room);
     int8_t v = -128;
-    if (x < R.W && y < R.D && z < R.H) {
+    if (x < R.W && y < R.D && z < R.H && p.variant == VN_VARIANT_SIMPLE) {
+        v = p.belief[(size_t)i * p.agent_bytes + (size_t)(x * p.pd + y) * p.ph + z];
+    } else if (x < R.W && y < R.D && z < R.H) {
         const uint32_t off = (uint32_t)((((((x >> 2) * p.nby + (y >> 2)) << 4) + ((x & 3) << 2) + (y & 3)) * p.ph) + z);
         const uint32_t b = (uint8_t)p.belief[(size_t)i * p.agent_bytes + off];
         v = (b & KNOWN) ? ((b & 0x40u) ? (int8_t)-2 : (int8_t)(b & 0x3fu)) : (int8_t)-1;
@@ -1149,7 +1398,9 @@ struct VnEnv {
     int8_t *d_belief = nullptr;
     int32_t *d_err = nullptr;
     EnvConst *d_envc = nullptr;
+    uint32_t *d_goal = nullptr;
     uint32_t ablate = 0;
+    int variant = 0, obs_dim = VN_OBS_DIM;
 };
 
 namespace {
@@ -1210,6 +1461,10 @@ Params base_params(VnEnv *e) {
     p.gid_base = (uint64_t)e->cfg.agent_id_base;
     p.K = 1;
     p.ablate = e->ablate;
+    p.variant = e->variant;
+    p.obs_dim = e->obs_dim;
+    p.pd = e->pd;
+    p.goal = e->d_goal;
     return p;
 }
 
@@ -1229,6 +1484,12 @@ int launch_ph(int L, dim3 grid, dim3 block, hipStream_t s, const Params &p) {
 
 template <bool RESET_ONLY>
 int launch_env(VnEnv *e, const Params &p, hipStream_t s) {
+    if (e->variant == VN_VARIANT_SIMPLE) {
+        const size_t lds = (size_t)64 * e->obs_dim * sizeof(float);
+        hipLaunchKernelGGL((simple_kernel<RESET_ONLY>), dim3((unsigned)((e->N + 63) / 64)), dim3(64), lds, s, p);
+        VN_HIP(hipGetLastError());
+        return VN_OK;
+    }
     const dim3 block(256);
     const dim3 grid((unsigned)(((size_t)e->N * GROUP + 255) / 256));
     const int L = e->cfg.local_map_length;
@@ -1248,6 +1509,7 @@ void free_env(VnEnv *e) {
     (void)hipFree(e->d_belief);
     (void)hipFree(e->d_err);
     (void)hipFree(e->d_envc);
+    (void)hipFree(e->d_goal);
     delete e;
 }
 
@@ -1268,6 +1530,9 @@ int vn_create(const VnRoomSet *rooms, int32_t n_agents, const VnConfig *cfg, int
     if (!rooms->whd || !rooms->walls) return fail(VN_ERR_INVALID, "rooms->whd / rooms->walls is NULL");
     if (cfg->local_map_length < 1 || cfg->local_map_length > VN_MAX_L)
         return fail(VN_ERR_INVALID, "local_map_length must be in 1..%d (got %d)", VN_MAX_L, cfg->local_map_length);
+    if (cfg->variant != VN_VARIANT_CUBIC && cfg->variant != VN_VARIANT_SIMPLE)
+        return fail(VN_ERR_INVALID, "variant must be %d (CubicEnv) or %d (simpleEnv), got %d", VN_VARIANT_CUBIC,
+                    VN_VARIANT_SIMPLE, cfg->variant);
 
     // ---- rooms -> descriptors, ray records, start lists ----
     const int nr = rooms->n_rooms;
@@ -1334,6 +1599,13 @@ int vn_create(const VnRoomSet *rooms, int32_t n_agents, const VnConfig *cfg, int
                 return fail(VN_ERR_ROOM, "room %d: start position (%d,%d,%d) outside the room", r, sx, sy, sz);
             fixed = sx | (sy << 8) | (sz << 16);
         }
+        int32_t fgoal = -1;
+        if (rooms->goal && rooms->goal[3 * r] >= 0) {
+            const int gx = rooms->goal[3 * r], gy = rooms->goal[3 * r + 1], gz = rooms->goal[3 * r + 2];
+            if (gx >= W || gy < 0 || gy >= D || gz < 0 || gz >= H)
+                return fail(VN_ERR_ROOM, "room %d: goal (%d,%d,%d) outside the room", r, gx, gy, gz);
+            fgoal = gx | (gy << 8) | (gz << 16);
+        }
         uint32_t *d = &desc[(size_t)r * 8];
         d[0] = (uint32_t)W | ((uint32_t)D << 8) | ((uint32_t)H << 16);
         d[1] = tf;
@@ -1348,6 +1620,7 @@ int vn_create(const VnRoomSet *rooms, int32_t n_agents, const VnConfig *cfg, int
             while (v < vmax && !((double)v / (double)tf >= fin)) ++v;
             d[6] = v;
         }
+        d[7] = (uint32_t)fgoal;
         maxW = W > maxW ? W : maxW;
         maxD = D > maxD ? D : maxD;
         maxH = H > maxH ? H : maxH;
@@ -1366,17 +1639,29 @@ int vn_create(const VnRoomSet *rooms, int32_t n_agents, const VnConfig *cfg, int
     // timing diagnostics only; every ablation keeps all addresses inside the
     // agent's room (bits: 1 column loads, 2 ray slots, 4 obs stores, 8 column stores)
     if (const char *ab = getenv("VOXNAV_ABLATE")) e->ablate = (uint32_t)strtoul(ab, nullptr, 0) & 0xfu;
+    e->variant = cfg->variant;
+    e->obs_dim = cfg->variant == VN_VARIANT_SIMPLE ? 6 * cfg->local_map_length + 7 : VN_OBS_DIM;
     e->nbx = (maxW + 3) / 4;
     e->nby = (maxD + 3) / 4;
-    e->pw = e->nbx * 4;
-    e->pd = e->nby * 4;
     e->ph = maxH <= 8 ? 8 : maxH <= 16 ? 16 : 32;   // whole column = one 8/16/32-byte access
-    e->map_bytes = (uint32_t)(e->nbx * e->nby * 16 * e->ph);
-    e->nwx = (e->pw + 63) / 64;
-    e->nwy = (e->pd + 63) / 64;
-    e->xp_off = e->map_bytes;                                        // rows (y, z): pd * ph * nwx words
-    e->yp_off = e->xp_off + (uint32_t)(e->pd * e->ph * e->nwx * 8);  // rows (x, z): pw * ph * nwy words
-    e->agent_bytes = (e->yp_off + (uint32_t)(e->pw * e->ph * e->nwy * 8) + 15u) & ~15u;
+    if (e->variant == VN_VARIANT_SIMPLE) {
+        // dense [pw][pd][ph] int8 map, no planes
+        e->pw = maxW;
+        e->pd = maxD;
+        e->map_bytes = (uint32_t)(e->pw * e->pd * e->ph);
+        e->nwx = e->nwy = 0;
+        e->xp_off = e->yp_off = e->map_bytes;
+        e->agent_bytes = (e->map_bytes + 15u) & ~15u;
+    } else {
+        e->pw = e->nbx * 4;
+        e->pd = e->nby * 4;
+        e->map_bytes = (uint32_t)(e->nbx * e->nby * 16 * e->ph);
+        e->nwx = (e->pw + 63) / 64;
+        e->nwy = (e->pd + 63) / 64;
+        e->xp_off = e->map_bytes;                                        // rows (y, z): pd * ph * nwx words
+        e->yp_off = e->xp_off + (uint32_t)(e->pd * e->ph * e->nwx * 8);  // rows (x, z): pw * ph * nwy words
+        e->agent_bytes = (e->yp_off + (uint32_t)(e->pw * e->ph * e->nwy * 8) + 15u) & ~15u;
+    }
 
     DeviceGuard dg(device);
     int rc = ensure_mt_table(device);
@@ -1417,6 +1702,7 @@ int vn_create(const VnRoomSet *rooms, int32_t n_agents, const VnConfig *cfg, int
     VN_ALLOC(e->d_belief, belief_bytes);
     VN_ALLOC(e->d_err, sizeof(int32_t));
     VN_ALLOC(e->d_envc, sizeof(EnvConst));
+    VN_ALLOC(e->d_goal, (size_t)n_agents * sizeof(uint32_t));
 #undef VN_ALLOC
     hipError_t he = hipSuccess;
     if (he == hipSuccess) he = hipMemcpy(e->d_rooms, desc.data(), desc.size() * sizeof(uint32_t), hipMemcpyHostToDevice);
@@ -1426,7 +1712,9 @@ int vn_create(const VnRoomSet *rooms, int32_t n_agents, const VnConfig *cfg, int
     if (he == hipSuccess) he = hipMemcpy(e->d_lut, lut, sizeof(lut), hipMemcpyHostToDevice);
     if (he == hipSuccess) he = hipMemset(e->d_hot, 0, (size_t)n_agents * sizeof(uint4));
     if (he == hipSuccess) he = hipMemset(e->d_seed, 0, (size_t)n_agents * sizeof(uint32_t));
-    if (he == hipSuccess) he = hipMemset(e->d_belief, 0, belief_bytes);   // 0x00 = unknown
+    // unknown: 0x00 in the CubicEnv byte encoding, -1 (0xFF) in the simpleEnv map
+    if (he == hipSuccess) he = hipMemset(e->d_belief, e->variant == VN_VARIANT_SIMPLE ? 0xFF : 0x00, belief_bytes);
+    if (he == hipSuccess) he = hipMemset(e->d_goal, 0, (size_t)n_agents * sizeof(uint32_t));
     if (he == hipSuccess) he = hipMemset(e->d_err, 0, sizeof(int32_t));
     if (he == hipSuccess) {
         EnvConst ec;
@@ -1469,6 +1757,8 @@ int vn_get_info(const VnEnv *env, VnInfo *info) {
     info->pad_h = env->ph;
     info->belief_bytes_per_agent = env->agent_bytes;
     info->device_bytes = (int64_t)env->device_bytes;
+    info->variant = env->variant;
+    info->obs_dim = env->obs_dim;
     return VN_OK;
 }
 

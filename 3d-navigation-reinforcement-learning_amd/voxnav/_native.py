@@ -12,6 +12,9 @@ import threading
 from . import _build
 
 VN_OBS_DIM = 80
+VN_VARIANT_CUBIC = 0
+VN_VARIANT_SIMPLE = 1
+VN_ABI_VERSION = 2
 VN_STATE_FIELDS = 16
 VN_MAX_L = 16
 STATE_FIELDS = (
@@ -22,13 +25,14 @@ STATE_FIELDS = (
 
 
 class VnRoomSet(C.Structure):
-    _fields_ = [("n_rooms", C.c_int32), ("whd", C.c_void_p), ("walls", C.c_void_p), ("fixed_start", C.c_void_p)]
+    _fields_ = [("n_rooms", C.c_int32), ("whd", C.c_void_p), ("walls", C.c_void_p), ("fixed_start", C.c_void_p),
+                ("goal", C.c_void_p)]
 
 
 class VnConfig(C.Structure):
     _fields_ = [
         ("local_map_length", C.c_int32), ("use_room_draw", C.c_int32), ("autoreset", C.c_int32),
-        ("reserved0", C.c_int32), ("crash_penalty", C.c_double), ("finish_percentage", C.c_double),
+        ("variant", C.c_int32), ("crash_penalty", C.c_double), ("finish_percentage", C.c_double),
         ("agent_id_base", C.c_int64), ("seed_stride", C.c_int64),
     ]
 
@@ -38,6 +42,7 @@ class VnInfo(C.Structure):
         ("n_agents", C.c_int32), ("n_rooms", C.c_int32), ("local_map_length", C.c_int32),
         ("pad_w", C.c_int32), ("pad_d", C.c_int32), ("pad_h", C.c_int32),
         ("belief_bytes_per_agent", C.c_int64), ("device_bytes", C.c_int64),
+        ("variant", C.c_int32), ("obs_dim", C.c_int32),
     ]
 
 
@@ -76,7 +81,7 @@ def _bind(lib):
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
-    if lib.vn_abi_version() != 1:
+    if lib.vn_abi_version() != VN_ABI_VERSION:
         raise VoxnavError("libvoxnav ABI version mismatch")
     return lib
 

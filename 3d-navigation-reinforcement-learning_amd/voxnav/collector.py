@@ -116,8 +116,8 @@ class RolloutCollector:
                  reset_seed: int = 42):
         if not isinstance(policy, (ActorCriticPolicy, RecurrentActorCriticPolicy)):
             raise TypeError("policy must be an ActorCriticPolicy or RecurrentActorCriticPolicy")
-        if getattr(policy, "obs_dim", OBS_DIM) != OBS_DIM:
-            raise ValueError("policy obs_dim must be 80")
+        if getattr(policy, "obs_dim", OBS_DIM) != env.obs_dim:
+            raise ValueError(f"policy obs_dim {policy.obs_dim} != env obs_dim {env.obs_dim}")
         self.env = env
         self.lib = env.lib
         self.device = env.device
@@ -132,7 +132,7 @@ class RolloutCollector:
         self.sync_weights()
         T, N, dev = self.n_steps, self.N, self.device
         z = lambda *s, dt=torch.float32: torch.zeros(s, dtype=dt, device=dev)  # noqa: E731
-        self._obs = z(T + 1, N, OBS_DIM)
+        self._obs = z(T + 1, N, env.obs_dim)
         self._starts = z(T + 1, N)
         self.actions = z(T, N, dt=torch.int32)
         self.rewards = z(T, N)
@@ -140,7 +140,7 @@ class RolloutCollector:
         self.log_probs = z(T, N)
         self._term = z(N, dt=torch.uint8)
         self._trunc = z(N, dt=torch.uint8)
-        self._tobs = z(N, OBS_DIM)
+        self._tobs = z(N, env.obs_dim)
         self._boot_idx = z(N, dt=torch.int32)
         self._boot_cnt = z(1, dt=torch.int32)
         self._boot_cnt_host = torch.zeros(1, dtype=torch.int32, pin_memory=True)

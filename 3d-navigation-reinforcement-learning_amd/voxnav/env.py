@@ -33,19 +33,30 @@ SEED_LIMIT = 2 ** 32       # np.random.seed range (envs/CubicEnv.py:80)
 
 
 class StepResult(NamedTuple):
-    obs: torch.Tensor            # f32 [N, 80]  (post-reset obs for finished agents)
+    obs: torch.Tensor            # f32 [N, obs_dim]  (post-reset obs for finished agents)
     reward: torch.Tensor         # f32 [N]  (or f64 with reward_f64=True)
     terminated: torch.Tensor     # bool [N]
     truncated: torch.Tensor      # bool [N]
-    terminal_obs: Optional[torch.Tensor]  # f32 [N, 80], rows valid where terminated|truncated
+    terminal_obs: Optional[torch.Tensor]  # f32 [N, obs_dim], rows valid where terminated|truncated
 
 
 class Rollout(NamedTuple):
-    obs: torch.Tensor            # f32 [K, N, 80]
+    obs: torch.Tensor            # f32 [K, N, obs_dim]
     reward: torch.Tensor         # f32 [K, N]
     terminated: torch.Tensor     # bool [K, N]
     truncated: torch.Tensor      # bool [K, N]
     actions: Optional[torch.Tensor]  # i32 [K, N]
+
+
+def _variant_code(v) -> int:
+    if isinstance(v, str):
+        try:
+            return {"cubic": _native.VN_VARIANT_CUBIC, "simple": _native.VN_VARIANT_SIMPLE}[v.lower()]
+        except KeyError:
+            raise ValueError(f"variant must be 'cubic' or 'simple', got {v!r}") from None
+    if int(v) not in (_native.VN_VARIANT_CUBIC, _native.VN_VARIANT_SIMPLE):
+        raise ValueError(f"variant must be 0 (cubic) or 1 (simple), got {v!r}")
+    return int(v)
 
 
 def _ptr(t: Optional[torch.Tensor]):
@@ -63,14 +74,16 @@ class BatchedGridEnv:
     ``room_path`` (or an explicit ``rooms`` RoomSet), ``width/depth/height``
     for the ctor box used when no room path is given, ``local_map_length``
     and ``crash_penalty``.  ``num_agents`` is the batch, ``autoreset`` the
-    VecEnv behaviour.
+    VecEnv behaviour.  ``variant="simple"`` selects the goal-seeking
+    envs/simpleEnv.py GridAgent (obs 6L+7) instead
+    of envs/CubicEnv.py.
     """
 
     def __init__(self, num_agents: int = 1, room_path=None, rooms: Optional[RoomSet] = None,
                  local_map_length: int = 4, crash_penalty: float = -2.0, width: int = 20, depth: int = 20,
                  height: int = 12, autoreset: bool = True, device: Union[int, str, torch.device, None] = None,
                  agent_id_base: int = 0, seed_stride: Optional[int] = None,
-                 finish_percentage: float = FINISH_PERCENTAGE, lib=None):
+                 finish_percentage: float = FINISH_PERCENTAGE, variant: Union[int, str] = "cubic", lib=None):
         if not torch.cuda.is_available():
             raise _native.VoxnavError("BatchedGridEnv needs a ROCm GPU (torch.cuda.is_available() is False)")
         self.lib = lib if lib is not None else _native.load()
@@ -89,10 +102,13 @@ class BatchedGridEnv:
         self.device = dev
         self.agent_id_base = int(agent_id_base)
         self.seed_stride = int(seed_stride) if seed_stride is not None else self.num_agents
-        whd, walls, fs = self.room_set.pack()
-        rs = _native.VnRoomSet(len(self.room_set), whd.ctypes.data, walls.ctypes.data, fs.ctypes.data)
-        cfg = _native.VnConfig(self.local_map_length, int(self.room_set.use_room_draw), int(self.autoreset), 0,
-                               self.crash_penalty, float(finish_percentage), self.agent_id_base, self.seed_stride)
+        self.variant = _variant_code(variant)
+        whd, walls, fs, gl = self.room_set.pack(self.variant)
+        rs = _native.VnRoomSet(len(self.room_set), whd.ctypes.data, walls.ctypes.data, fs.ctypes.data,
+                               gl.ctypes.data)
+        cfg = _native.VnConfig(self.local_map_length, int(self.room_set.use_room_draw), int(self.autoreset),
+                               self.variant, self.crash_penalty, float(finish_percentage), self.agent_id_base,
+                               self.seed_stride)
         h = C.c_void_p()
         with torch.cuda.device(self.device):
             _native.check(self.lib.vn_create(C.byref(rs), self.num_agents, C.byref(cfg), self.device.index,
@@ -101,7 +117,9 @@ class BatchedGridEnv:
         info = _native.VnInfo()
         _native.check(self.lib.vn_get_info(self._h, C.byref(info)), "vn_get_info")
         self.info = info
-        self.total_free_cells = np.asarray([r.total_free_cells for r in self.room_set.rooms], dtype=np.int64)
+        self.obs_dim = int(info.obs_dim)
+        self.total_free_cells = np.asarray([r.total_free_cells_for(self.variant) for r in self.room_set.rooms],
+                                           dtype=np.int64)
         self._was_reset = False
         self._t = 0   # global step counter for the random policy stream
 
@@ -140,12 +158,12 @@ class BatchedGridEnv:
     def reset(self, seed=None, mask: Optional[torch.Tensor] = None, out: Optional[torch.Tensor] = None):
         """GridAgent.reset(seed) for all agents (or those with mask[i]).
 
-        Returns obs f32 [N, 80] (rows of unmasked agents are left as in
+        Returns obs f32 [N, obs_dim] (rows of unmasked agents are left as in
         ``out`` / zero).
         """
         seeds = self._seeds_tensor(seed)
         if out is None:
-            out = torch.zeros((self.num_agents, OBS_DIM), dtype=torch.float32, device=self.device)
+            out = torch.zeros((self.num_agents, self.obs_dim), dtype=torch.float32, device=self.device)
         m = None
         if mask is not None:
             m = mask.to(device=self.device, dtype=torch.uint8).contiguous()
@@ -159,11 +177,11 @@ class BatchedGridEnv:
             raise RuntimeError("call reset() before step()")
         N = self.num_agents
         a = torch.as_tensor(actions, device=self.device).to(torch.int32).reshape(N).contiguous()
-        obs = torch.empty((N, OBS_DIM), dtype=torch.float32, device=self.device)
+        obs = torch.empty((N, self.obs_dim), dtype=torch.float32, device=self.device)
         rew = torch.empty(N, dtype=torch.float64 if reward_f64 else torch.float32, device=self.device)
         te = torch.empty(N, dtype=torch.uint8, device=self.device)
         tr = torch.empty(N, dtype=torch.uint8, device=self.device)
-        tob = torch.zeros((N, OBS_DIM), dtype=torch.float32, device=self.device) if (terminal_obs and self.autoreset) else None
+        tob = torch.zeros((N, self.obs_dim), dtype=torch.float32, device=self.device) if (terminal_obs and self.autoreset) else None
         _native.check(self.lib.vn_step(self._h, _ptr(a), _ptr(obs), None if reward_f64 else _ptr(rew),
                                        _ptr(rew) if reward_f64 else None, _ptr(te), _ptr(tr), _ptr(tob),
                                        self._stream()), "vn_step")
@@ -172,12 +190,12 @@ class BatchedGridEnv:
     def step_into(self, actions: torch.Tensor, obs: torch.Tensor, reward: torch.Tensor, terminated: torch.Tensor,
                   truncated: torch.Tensor, terminal_obs: Optional[torch.Tensor] = None):
         """``step`` writing into caller-owned device buffers (no allocation):
-        actions i32 [N], obs f32 [N, 80], reward f32 (or f64) [N],
-        terminated / truncated u8 [N], terminal_obs f32 [N, 80] or None."""
+        actions i32 [N], obs f32 [N, obs_dim], reward f32 (or f64) [N],
+        terminated / truncated u8 [N], terminal_obs f32 [N, obs_dim] or None."""
         if not self._was_reset:
             raise RuntimeError("call reset() before step()")
         N = self.num_agents
-        for name, t, dt, shape in (("actions", actions, torch.int32, (N,)), ("obs", obs, torch.float32, (N, OBS_DIM)),
+        for name, t, dt, shape in (("actions", actions, torch.int32, (N,)), ("obs", obs, torch.float32, (N, self.obs_dim)),
                                    ("terminated", terminated, torch.uint8, (N,)),
                                    ("truncated", truncated, torch.uint8, (N,))):
             if t.dtype != dt or tuple(t.shape) != shape or not t.is_contiguous() or t.device != self.device:
@@ -198,7 +216,7 @@ class BatchedGridEnv:
         if t0 is None:
             t0 = self._t
         if out is None:
-            obs = torch.empty((K, N, OBS_DIM), dtype=torch.float32, device=self.device)
+            obs = torch.empty((K, N, self.obs_dim), dtype=torch.float32, device=self.device)
             rew = torch.empty((K, N), dtype=torch.float64 if reward_f64 else torch.float32, device=self.device)
             te = torch.empty((K, N), dtype=torch.uint8, device=self.device)
             tr = torch.empty((K, N), dtype=torch.uint8, device=self.device)
@@ -221,7 +239,9 @@ class BatchedGridEnv:
         return {f: s[:, i] for i, f in enumerate(_native.STATE_FIELDS)}
 
     def belief(self) -> torch.Tensor:
-        """int8 [N, pad_w, pad_d, pad_h]; counts saturate at 63; -128 outside the room."""
+        """int8 [N, pad_w, pad_d, pad_h], the reference's internal_grid values
+        (CubicEnv: counts saturate at 63; simpleEnv: -1/0/1/2); -128 outside
+        the agent's room."""
         i = self.info
         out = torch.empty((self.num_agents, i.pad_w, i.pad_d, i.pad_h), dtype=torch.int8, device=self.device)
         _native.check(self.lib.vn_export_belief(self._h, _ptr(out), self._stream()), "vn_export_belief")

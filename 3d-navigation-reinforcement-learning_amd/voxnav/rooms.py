@@ -10,6 +10,8 @@ The text grammar is the reference's (README.md:9-19, parser
     Goal=x,y,z            -> goal (optional; used by the simpleEnv variant)
 
 Quirks kept on purpose: any value other than 2 (or an explicit -2) is free;
+the simpleEnv variant (envs/simpleEnv.py:282, :381) keeps the raw values,
+so there only 2 is a wall and a -2 token is free (``Room.walls_for``);
 a row with the wrong width raises ``ValueError`` (:435-436); a row past D or
 a layer index outside [-H, H) raises ``IndexError`` like the reference's
 numpy assignment (:437); ``Layer z=-2`` writes layer H-2
@@ -34,14 +36,29 @@ REPO_ROOT = Path(__file__).resolve().parents[2]
 REFERENCE_ROOM_ARCHIVE = REPO_ROOT / "rooms" / "reference_rooms.tar.xz"
 
 
+VARIANT_CUBIC = 0    # envs/CubicEnv.py
+VARIANT_SIMPLE = 1   # envs/simpleEnv.py
+
+
 @dataclass
 class Room:
-    """One parsed room: walls[x, y, z] is True where the reference grid is -2."""
+    """One parsed room: walls[x, y, z] is True where the CubicEnv grid is -2
+    (file value 2 or -2); ``minus2`` marks the cells written as -2, which
+    are free in the simpleEnv variant."""
 
     name: str
     walls: np.ndarray
     start: Optional[Tuple[int, int, int]] = None
     goal: Optional[Tuple[int, int, int]] = None
+    minus2: Optional[np.ndarray] = None
+
+    def walls_for(self, variant: int = VARIANT_CUBIC) -> np.ndarray:
+        if variant == VARIANT_SIMPLE and self.minus2 is not None:
+            return self.walls & ~self.minus2
+        return self.walls
+
+    def total_free_cells_for(self, variant: int = VARIANT_CUBIC) -> int:
+        return int((~self.walls_for(variant)[1:-1, 1:-1, 1:-1]).sum())
 
     @property
     def shape(self) -> Tuple[int, int, int]:
@@ -65,6 +82,7 @@ class Room:
 
 def parse_room(text: str, name: str = "<room>") -> Room:
     walls = None
+    minus2 = None
     start = goal = None
     layer = None
     row = 0
@@ -83,6 +101,7 @@ def parse_room(text: str, name: str = "<room>") -> Room:
             dims = line.split("=")[1].split(",")
             W, D, H = int(dims[0]), int(dims[1]), int(dims[2])
             walls = np.zeros((W, D, H), dtype=bool)
+            minus2 = np.zeros((W, D, H), dtype=bool)
             continue
         if line.startswith("Layer"):
             layer = int(line.split("=")[1])
@@ -100,10 +119,11 @@ def parse_room(text: str, name: str = "<room>") -> Room:
         if row >= D:
             raise IndexError(f"{name}: row {row} is out of bounds for depth {D}")
         walls[:, row, layer % H] = [v in (2, -2) for v in vals]
+        minus2[:, row, layer % H] = [v == -2 for v in vals]
         row += 1
     if walls is None:
         raise ValueError(f"{name}: no 'Size=' line")
-    return Room(name=name, walls=walls, start=start, goal=goal)
+    return Room(name=name, walls=walls, start=start, goal=goal, minus2=minus2 if minus2.any() else None)
 
 
 def load_room_file(path: Union[str, Path]) -> Room:
@@ -149,7 +169,7 @@ class RoomSet:
     rooms: List[Room]
     use_room_draw: bool = True
     source: str = ""
-    _packed: Optional[tuple] = field(default=None, repr=False)
+    _packed: dict = field(default_factory=dict, repr=False)
 
     def __len__(self):
         return len(self.rooms)
@@ -158,14 +178,17 @@ class RoomSet:
     def max_shape(self):
         return tuple(int(max(r.shape[i] for r in self.rooms)) for i in range(3))
 
-    def pack(self):
-        """(whd int32 [n,3], walls uint8 concat, fixed_start int32 [n,3]) for vn_create."""
-        if self._packed is None:
+    def pack(self, variant: int = VARIANT_CUBIC):
+        """(whd int32 [n,3], walls uint8 concat, fixed_start int32 [n,3],
+        goal int32 [n,3]) for vn_create; walls of the given env variant."""
+        if variant not in self._packed:
             whd = np.asarray([r.shape for r in self.rooms], dtype=np.int32)
-            walls = np.concatenate([np.ascontiguousarray(r.walls, dtype=np.uint8).reshape(-1) for r in self.rooms])
+            walls = np.concatenate([np.ascontiguousarray(r.walls_for(variant), dtype=np.uint8).reshape(-1)
+                                    for r in self.rooms])
             fs = np.asarray([r.start if r.start is not None else (-1, -1, -1) for r in self.rooms], dtype=np.int32)
-            self._packed = (np.ascontiguousarray(whd), np.ascontiguousarray(walls), np.ascontiguousarray(fs))
-        return self._packed
+            gl = np.asarray([r.goal if r.goal is not None else (-1, -1, -1) for r in self.rooms], dtype=np.int32)
+            self._packed[variant] = tuple(np.ascontiguousarray(a) for a in (whd, walls, fs, gl))
+        return self._packed[variant]
 
 
 def load_room_dir(room_path: Union[str, Path]) -> RoomSet:

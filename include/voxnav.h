@@ -27,8 +27,11 @@
 extern "C" {
 #endif
 
-#define VN_ABI_VERSION 1
+#define VN_ABI_VERSION 2
 #define VN_OBS_DIM 80            /* envs/CubicEnv.py:58-62, :295-311 */
+#define VN_VARIANT_CUBIC 0       /* envs/CubicEnv.py  (obs 80)                   */
+#define VN_VARIANT_SIMPLE 1      /* envs/simpleEnv.py (obs 6L + 7, goal reward)   */
+#define VN_MAX_OBS_DIM 103       /* 6 * VN_MAX_L + 7                              */
 #define VN_STATE_FIELDS 16
 #define VN_MAX_L 16              /* largest supported local_map_length */
 #define VN_MAX_W 255
@@ -55,8 +58,12 @@ typedef struct VnEnv VnEnv;
 typedef struct VnRoomSet {
     int32_t n_rooms;
     const int32_t *whd;          /* [n_rooms][3]  W, D, H                       */
-    const uint8_t *walls;        /* concat of W*D*H bytes, index (x*D+y)*H+z    */
+    const uint8_t *walls;        /* concat of W*D*H bytes, index (x*D+y)*H+z;
+                                    CubicEnv: value -2 after its 2 -> -2 mapping
+                                    (:434), simpleEnv: file value 2 (:282)      */
     const int32_t *fixed_start;  /* [n_rooms][3] or NULL; -1 = draw a start     */
+    const int32_t *goal;         /* [n_rooms][3] or NULL; "Goal=" line, -1 =
+                                    draw one (simpleEnv :419-426)               */
 } VnRoomSet;
 
 /* GridAgent ctor kwargs (envs/CubicEnv.py:17-29) + batching knobs. */
@@ -64,7 +71,7 @@ typedef struct VnConfig {
     int32_t local_map_length;    /* L (ctor default 4; Grid_Train uses 10)      */
     int32_t use_room_draw;       /* 1: room_path given -> random.choice(rooms)  */
     int32_t autoreset;           /* SB3 VecEnv auto-reset inside vn_step        */
-    int32_t reserved0;
+    int32_t variant;             /* VN_VARIANT_CUBIC / VN_VARIANT_SIMPLE        */
     double crash_penalty;        /* ctor default -2.0                           */
     double finish_percentage;    /* FINISH_PERCENTAGE = 0.84 (CubicEnv.py:12)   */
     int64_t agent_id_base;       /* global id of this shard's agent 0           */
@@ -78,6 +85,8 @@ typedef struct VnInfo {
     int32_t pad_w, pad_d, pad_h; /* belief map padding (max room dims, PH%4==0) */
     int64_t belief_bytes_per_agent;
     int64_t device_bytes;        /* total HBM owned by the env                  */
+    int32_t variant;
+    int32_t obs_dim;             /* floats per observation row                  */
 } VnInfo;
 
 const char *vn_last_error(void);
@@ -92,21 +101,27 @@ int vn_get_info(const VnEnv *env, VnInfo *info);
  * GridAgent.reset(seed) for every agent with mask[i] != 0 (mask NULL = all)
  * (envs/CubicEnv.py:77-108, draws :407/:462).  seeds: device int64 [N],
  * each in [0, 2^32) (the reference also calls np.random.seed(seed), :80).
- * obs: device f32 [N][80]; rows of unmasked agents are left untouched.
+ * obs: device f32 [N][obs_dim]; rows of unmasked agents are left untouched.
+ * simpleEnv variant (envs/simpleEnv.py:79-107): its reset neither seeds nor
+ * returns an observation; the build seeds the draws with random.seed(seed)
+ * and returns get_obs() after the reset (what train/evaluate_grid.py:54-55
+ * does), so obs is that first observation.
  */
 int vn_reset(VnEnv *env, const int64_t *seeds, const uint8_t *mask, float *obs, void *stream);
 
 /*
- * GridAgent.step(action) for all N agents (envs/CubicEnv.py:110-132),
+ * GridAgent.step(action) for all N agents (envs/CubicEnv.py:110-132;
+ * simpleEnv variant: envs/simpleEnv.py:109-150),
  * followed, when cfg.autoreset, by the SB3 VecEnv auto-reset of every agent
  * whose step ended the episode (terminated or truncated).
  *   actions       device i32 [N], each in 0..5
- *   obs           device f32 [N][80]  (post-reset obs for finished agents)
+ *   obs           device f32 [N][obs_dim] (post-reset obs for finished agents;
+ *                 obs_dim = 80, or 6L+7 for the simpleEnv variant)
  *   reward        device f32 [N]      (may be NULL)  -- f64 reward rounded
  *   reward64      device f64 [N]      (may be NULL)  -- exact f64 reward
  *   terminated    device u8  [N]      (may be NULL)
  *   truncated     device u8  [N]      (may be NULL)
- *   terminal_obs  device f32 [N][80]  (may be NULL) written only for agents
+ *   terminal_obs  device f32 [N][obs_dim] (may be NULL) written only for agents
  *                 that finished an episode in this step
  */
 int vn_step(VnEnv *env, const int32_t *actions, float *obs, float *reward, double *reward64,
@@ -126,9 +141,11 @@ int vn_step_random(VnEnv *env, uint64_t policy_seed, uint64_t t0, int32_t k_step
  * Parity dumps.  state_out: device i64 [N][16] in the field order
  * x, y, z, facing, last_action, step_count, visited_count, bump_count,
  * done, last_bump, near_wall, was_near_wall, cells_insight_down, room,
- * max_steps, next_seed.
+ * max_steps, next_seed.  simpleEnv variant: fields 9..11 are the goal
+ * (gx, gy, gz) and 12 is 0 (it has no last_bump / near-wall state).
  * belief_out: device i8 [N][pad_w][pad_d][pad_h] dense x-major, the
- * reference's internal_grid values (-2 wall, -1 unknown, 0 free, n visits;
+ * reference's internal_grid values (CubicEnv: -2 wall, -1 unknown, 0 free,
+ * n visits; simpleEnv: -1 unknown, 0 free, 1 visited, 2 wall;
  * visit counts saturate at 63), cells outside the agent's room read -128.
  */
 int vn_export_state(VnEnv *env, int64_t *state_out, void *stream);
@@ -186,6 +203,7 @@ int vn_policy_head(const float *latent_pi, const float *latent_vf, int32_t N, in
  * Ordered indices of the agents whose step was a time-limit truncation
  * (SB3 VecEnv: done and info["TimeLimit.truncated"] = truncated and not
  * terminated) -> boot_idx (device i32 [N]) and boot_count (device i32 [1]).
+ * terminated / truncated must be 16-byte aligned.
  */
 int vn_collect_compact(const uint8_t *terminated, const uint8_t *truncated, int32_t N, int32_t *boot_idx,
                        int32_t *boot_count, void *stream);

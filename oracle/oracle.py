@@ -47,9 +47,10 @@ STATE_FIELDS = (
 @dataclass
 class OracleRoom:
     name: str
-    grid: np.ndarray                 # int64 [W, D, H], walls == -2
+    grid: np.ndarray                 # int64 [W, D, H], walls == -2  (CubicEnv's self.grid)
     start: Optional[tuple] = None    # "Start position" line, if any
     goal: Optional[tuple] = None     # "Goal" line, if any
+    tokens: Optional[np.ndarray] = None   # raw file values (simpleEnv's self.grid, walls == 2)
 
     @property
     def whd(self):
@@ -58,6 +59,15 @@ class OracleRoom:
     @property
     def walls(self) -> np.ndarray:
         return (self.grid == -2).astype(np.uint8)
+
+    @property
+    def simple_walls(self) -> np.ndarray:
+        """simpleEnv walls: file value 2 only; a -2 token is free there (envs/simpleEnv.py:282, :381)."""
+        t = self.tokens if self.tokens is not None else np.where(self.grid == -2, 2, self.grid)
+        return (t == 2).astype(np.uint8)
+
+    def walls_for(self, variant: int) -> np.ndarray:
+        return self.simple_walls if variant else self.walls
 
     def interior_free(self):
         """(total_free_cells, start list) -- envs/CubicEnv.py:450-457."""
@@ -74,6 +84,7 @@ class OracleRoom:
 def parse_room_text(text: str, name: str = "<room>") -> OracleRoom:
     """Restates load_room's text branch, envs/CubicEnv.py:408-438."""
     grid = None
+    tokens = None
     start = goal = None
     row = 0
     z = None
@@ -89,17 +100,19 @@ def parse_room_text(text: str, name: str = "<room>") -> OracleRoom:
             d = line.split("=")[1].split(",")
             W, D, H = int(d[0]), int(d[1]), int(d[2])
             grid = np.zeros((W, D, H), dtype=np.int64)
+            tokens = np.zeros((W, D, H), dtype=np.int64)
         elif line.startswith("Layer"):
             z = int(line.split("=")[1])
             row = 0
         else:
-            vals = [int(v) for v in line.split()]
-            vals = [v if v != 2 else -2 for v in vals]
+            raw = [int(v) for v in line.split()]
+            vals = [v if v != 2 else -2 for v in raw]
             if len(vals) != grid.shape[0]:
                 raise ValueError(f"Line '{line}' has {len(vals)} values, but width is {grid.shape[0]}")
             grid[:, row, z] = vals          # numpy indexing: negative z wraps, row >= D raises
+            tokens[:, row, z] = raw         # simpleEnv keeps the raw values (envs/simpleEnv.py:381)
             row += 1
-    return OracleRoom(name=name, grid=grid, start=start, goal=goal)
+    return OracleRoom(name=name, grid=grid, start=start, goal=goal, tokens=tokens)
 
 
 def parse_room_file(path) -> OracleRoom:
@@ -145,6 +158,10 @@ def lib():
         P = c.c_void_p
         L.or_create.restype = P
         L.or_create.argtypes = [c.c_int, P, P, P, c.c_int, c.c_int, c.c_double, c.c_int]
+        L.or_create2.restype = P
+        L.or_create2.argtypes = [c.c_int, P, P, P, P, c.c_int, c.c_int, c.c_double, c.c_int, c.c_int]
+        L.or_obs_dim.argtypes = [P]
+        L.or_obs_dim.restype = c.c_int
         L.or_destroy.argtypes = [P]
         L.or_reset.argtypes = [P, c.c_int, c.c_int64, P]
         L.or_reset.restype = c.c_int
@@ -174,20 +191,26 @@ def _ptr(a: Optional[np.ndarray]):
 
 
 class OracleEnv:
-    """N independent CubicEnv agents on the CPU (restated semantics)."""
+    """N independent CubicEnv (variant 0) or simpleEnv (variant 1) agents on
+    the CPU (restated semantics)."""
 
     def __init__(self, rooms: Sequence[OracleRoom], n_agents: int = 1, local_map_length: int = 4,
-                 crash_penalty: float = -2.0, use_room_draw: bool = True):
+                 crash_penalty: float = -2.0, use_room_draw: bool = True, variant: int = 0):
         self.rooms = list(rooms)
         self.n_agents = int(n_agents)
         self.L = int(local_map_length)
+        self.variant = int(variant)
         whd = np.array([r.whd for r in self.rooms], dtype=np.int32).reshape(-1)
-        walls = np.concatenate([r.walls.reshape(-1) for r in self.rooms]).astype(np.uint8)
+        walls = np.concatenate([r.walls_for(self.variant).reshape(-1) for r in self.rooms]).astype(np.uint8)
         fs = np.array([r.start if r.start is not None else (-1, -1, -1) for r in self.rooms],
                       dtype=np.int32).reshape(-1)
-        self._keep = (whd, walls, fs)
-        self._h = lib().or_create(len(self.rooms), _ptr(whd), _ptr(walls), _ptr(fs), int(bool(use_room_draw)),
-                                  self.L, float(crash_penalty), self.n_agents)
+        gl = np.array([r.goal if r.goal is not None else (-1, -1, -1) for r in self.rooms],
+                      dtype=np.int32).reshape(-1)
+        self._keep = (whd, walls, fs, gl)
+        self._h = lib().or_create2(len(self.rooms), _ptr(whd), _ptr(walls), _ptr(fs), _ptr(gl),
+                                   int(bool(use_room_draw)), self.L, float(crash_penalty), self.n_agents,
+                                   self.variant)
+        self.obs_dim = int(lib().or_obs_dim(self._h))
 
     def __del__(self):
         h = getattr(self, "_h", None)
@@ -196,12 +219,12 @@ class OracleEnv:
             self._h = None
 
     def reset(self, agent: int, seed: int) -> np.ndarray:
-        obs = np.zeros(OBS_DIM, np.float32)
+        obs = np.zeros(self.obs_dim, np.float32)
         lib().or_reset(self._h, agent, int(seed), _ptr(obs))
         return obs
 
     def step(self, agent: int, action: int):
-        obs = np.zeros(OBS_DIM, np.float32)
+        obs = np.zeros(self.obs_dim, np.float32)
         r = np.zeros(1, np.float64)
         te = np.zeros(1, np.uint8)
         tr = np.zeros(1, np.uint8)
@@ -235,14 +258,14 @@ class OracleEnv:
         seeds = np.ascontiguousarray(np.asarray(seeds, dtype=np.int64).reshape(N))
         stride = N if seed_stride is None else int(seed_stride)
         if record:
-            obs = np.zeros((K, N, OBS_DIM), np.float32)
+            obs = np.zeros((K, N, self.obs_dim), np.float32)
             rew = np.zeros((K, N), np.float64)
             te = np.zeros((K, N), np.uint8)
             tr = np.zeros((K, N), np.uint8)
             act = np.zeros((K, N), np.int32)
         else:
             obs = rew = te = tr = act = None
-        tob = np.zeros((K, N, OBS_DIM), np.float32) if terminal_obs else None
+        tob = np.zeros((K, N, self.obs_dim), np.float32) if terminal_obs else None
         ain = None if actions is None else np.ascontiguousarray(np.asarray(actions, np.int32).reshape(K, N))
         resets = lib().or_run_random(self._h, _ptr(seeds), int(bool(initial_reset)), stride, int(gid_base),
                                      int(policy_seed), int(t0), int(K), int(bool(autoreset)), _ptr(obs),

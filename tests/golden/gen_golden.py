@@ -120,6 +120,42 @@ def explorer_action(env):
     raise AssertionError(d)
 
 
+def seek_action(env):
+    """Goal-seeking BFS (simpleEnv golden vectors only): shortest path over
+    the true free cells (simpleEnv walls are 2) to the goal or one of the 4
+    cells above it (envs/simpleEnv.py:201-206)."""
+    W, D, H = env.width, env.depth, env.height
+    targets = {(env.gx, env.gy, env.gz + i) for i in range(5)}
+    start = (env.x, env.y, env.z)
+    prev = {start: None}
+    q = deque([start])
+    goal = None
+    while q:
+        c = q.popleft()
+        if c in targets and c != start:
+            goal = c
+            break
+        for d in ((1, 0, 0), (-1, 0, 0), (0, 1, 0), (0, -1, 0), (0, 0, 1), (0, 0, -1)):
+            n = (c[0] + d[0], c[1] + d[1], c[2] + d[2])
+            if 0 <= n[0] < W and 0 <= n[1] < D and 0 <= n[2] < H and n not in prev and env.grid[n] != 2:
+                prev[n] = c
+                q.append(n)
+    if goal is None:
+        return 0
+    c = goal
+    while prev[c] != start:
+        c = prev[c]
+    d = (c[0] - start[0], c[1] - start[1], c[2] - start[2])
+    if d == (0, 0, 1):
+        return 4
+    if d == (0, 0, -1):
+        return 5
+    for a in range(4):
+        if _DIRS[a][env.facing] == d:
+            return a
+    raise AssertionError(d)
+
+
 def run_trajectory(env, seeds, steps, policy, policy_seed, eps, full_dumps=(), simple=False):
     """Step `env`, resetting (seed from `seeds`, in order) at start and after
     every terminated/truncated step (SB3 VecEnv auto-reset order)."""
@@ -149,6 +185,8 @@ def run_trajectory(env, seeds, steps, policy, policy_seed, eps, full_dumps=(), s
         for t in range(steps):
             if policy == "random" or coin.random() < eps:
                 a = random_action(policy_seed, 0, t)
+            elif policy == "seek":
+                a = seek_action(env)
             else:
                 a = explorer_action(env)
             obs, r, term, trunc, _ = env.step(a)
@@ -209,6 +247,8 @@ def write_box_room(dirpath: Path, W, D, H):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--quick", action="store_true")
+    ap.add_argument("--only", choices=["all", "simple"], default="all",
+                    help="'simple': regenerate only the simpleEnv trajectories (section 4)")
     args = ap.parse_args()
     if not (REF / "envs" / "CubicEnv.py").exists():
         raise SystemExit(f"reference not found at {REF}")
@@ -234,58 +274,59 @@ def main():
             env.rooms = sorted(env.rooms)      # glob order is unspecified (envs/CubicEnv.py:66)
         return env
 
-    # ---------------- 1. parsed-room fixtures (all room files) -------------
-    names, dims, free, hashes, bfree = [], [], [], [], []
-    with contextlib.redirect_stdout(io.StringIO()):
-        for p in sorted(rooms.glob("P*/*.txt")):
-            env = make_env(room_path=None)
-            env.rooms = [p]
-            env.reset(seed=0)
-            g = env.grid
-            names.append(str(p.relative_to(rooms)))
-            dims.append(g.shape)
-            free.append(env.total_free_cells)
-            hashes.append(grid_hash(g))
-            bnd = np.ones(g.shape, bool)
-            bnd[1:-1, 1:-1, 1:-1] = False
-            bfree.append(int(((g != -2) & bnd).sum()))
-    np.savez_compressed(OUT / "rooms_parsed.npz", names=np.asarray(names), whd=np.asarray(dims, np.int32),
-                        total_free=np.asarray(free, np.int64), grid_hash=np.asarray(hashes, np.uint64),
-                        boundary_free=np.asarray(bfree, np.int64))
-    print(f"rooms_parsed: {len(names)} files")
-
-    # ---------------- 2. reset tables --------------------------------------
-    n_seeds = 300 if args.quick else 2000
-    # the reference also calls np.random.seed(seed) (envs/CubicEnv.py:80): seeds must lie in [0, 2**32)
-    seed_list = list(range(n_seeds)) + [2 ** 32 - 1, 2 ** 31 + 5, 2 ** 31 - 1, 4000000000, 99991]
-    reset_sets = {"P1_training": rooms / "P1_training", "P2_training": rooms / "P2_training",
-                  "P3_training": rooms / "P3_training", "P2_evaluate": rooms / "P2_evaluate"}
-    for tag, d in reset_sets.items():
-        env = make_env(room_path=d, L=10)
-        room_hashes = []
+    if args.only == "all":
+        # ---------------- 1. parsed-room fixtures (all room files) -------------
+        names, dims, free, hashes, bfree = [], [], [], [], []
         with contextlib.redirect_stdout(io.StringIO()):
-            for p in env.rooms:
-                e2 = make_env(room_path=None)
-                e2.rooms = [p]
-                e2.reset(seed=0)
-                room_hashes.append(grid_hash(e2.grid))
-            rows = []
+            for p in sorted(rooms.glob("P*/*.txt")):
+                env = make_env(room_path=None)
+                env.rooms = [p]
+                env.reset(seed=0)
+                g = env.grid
+                names.append(str(p.relative_to(rooms)))
+                dims.append(g.shape)
+                free.append(env.total_free_cells)
+                hashes.append(grid_hash(g))
+                bnd = np.ones(g.shape, bool)
+                bnd[1:-1, 1:-1, 1:-1] = False
+                bfree.append(int(((g != -2) & bnd).sum()))
+        np.savez_compressed(OUT / "rooms_parsed.npz", names=np.asarray(names), whd=np.asarray(dims, np.int32),
+                            total_free=np.asarray(free, np.int64), grid_hash=np.asarray(hashes, np.uint64),
+                            boundary_free=np.asarray(bfree, np.int64))
+        print(f"rooms_parsed: {len(names)} files")
+
+        # ---------------- 2. reset tables --------------------------------------
+        n_seeds = 300 if args.quick else 2000
+        # the reference also calls np.random.seed(seed) (envs/CubicEnv.py:80): seeds must lie in [0, 2**32)
+        seed_list = list(range(n_seeds)) + [2 ** 32 - 1, 2 ** 31 + 5, 2 ** 31 - 1, 4000000000, 99991]
+        reset_sets = {"P1_training": rooms / "P1_training", "P2_training": rooms / "P2_training",
+                      "P3_training": rooms / "P3_training", "P2_evaluate": rooms / "P2_evaluate"}
+        for tag, d in reset_sets.items():
+            env = make_env(room_path=d, L=10)
+            room_hashes = []
+            with contextlib.redirect_stdout(io.StringIO()):
+                for p in env.rooms:
+                    e2 = make_env(room_path=None)
+                    e2.rooms = [p]
+                    e2.reset(seed=0)
+                    room_hashes.append(grid_hash(e2.grid))
+                rows = []
+                for s in seed_list:
+                    env.reset(seed=s)
+                    ri = room_hashes.index(grid_hash(env.grid))
+                    rows.append((ri, env.x, env.y, env.z))
+            np.savez_compressed(OUT / f"reset_table_{tag}.npz", seeds=np.asarray(seed_list, np.int64),
+                                draws=np.asarray(rows, np.int32), room_names=np.asarray([p.name for p in env.rooms]))
+            print(f"reset_table_{tag}: {len(rows)} seeds")
+        # box (room_path=None): a single start draw, no room draw
+        env = make_env(room_path=None, L=10, whd=(32, 32, 8))
+        rows = []
+        with contextlib.redirect_stdout(io.StringIO()):
             for s in seed_list:
                 env.reset(seed=s)
-                ri = room_hashes.index(grid_hash(env.grid))
-                rows.append((ri, env.x, env.y, env.z))
-        np.savez_compressed(OUT / f"reset_table_{tag}.npz", seeds=np.asarray(seed_list, np.int64),
-                            draws=np.asarray(rows, np.int32), room_names=np.asarray([p.name for p in env.rooms]))
-        print(f"reset_table_{tag}: {len(rows)} seeds")
-    # box (room_path=None): a single start draw, no room draw
-    env = make_env(room_path=None, L=10, whd=(32, 32, 8))
-    rows = []
-    with contextlib.redirect_stdout(io.StringIO()):
-        for s in seed_list:
-            env.reset(seed=s)
-            rows.append((0, env.x, env.y, env.z))
-    np.savez_compressed(OUT / "reset_table_box32x32x8.npz", seeds=np.asarray(seed_list, np.int64),
-                        draws=np.asarray(rows, np.int32), room_names=np.asarray(["<ctor box>"]))
+                rows.append((0, env.x, env.y, env.z))
+        np.savez_compressed(OUT / "reset_table_box32x32x8.npz", seeds=np.asarray(seed_list, np.int64),
+                            draws=np.asarray(rows, np.int32), room_names=np.asarray(["<ctor box>"]))
 
     # ---------------- 3. trajectories --------------------------------------
     box_dir = tmp / "boxes"
@@ -326,7 +367,7 @@ def main():
         return rooms / arg, None
 
     rng_dump = lambda n: tuple(sorted({0, n // 3, n // 2, n - 1}))  # noqa: E731
-    for i, (name, src, L, steps, policy, eps) in enumerate(scen):
+    for i, (name, src, L, steps, policy, eps) in enumerate(scen if args.only == "all" else []):
         rp, whd = resolve(src)
         env = make_env(room_path=rp, L=L, whd=whd)
         seeds = [42 + 1000 * i + 7 * k for k in range(64)]
@@ -338,16 +379,25 @@ def main():
               f"term={int(t['terminated'].sum())} trunc={int(t['truncated'].sum())}")
 
     # ---------------- 4. simpleEnv (goal-seeking variant) --------------------
-    for i, (name, src, L, steps) in enumerate([
-        ("P2_training_L4", "set:P2_training", 4, S(600)),
-        ("maze8x8s22_L4", "file:P2_training/maze_8x8_seed22.txt", 4, S(400)),
+    # (the reference's reset does not seed `random`; the build seeds it with
+    #  random.seed(seed) before every reset and calls get_obs() after it)
+    for i, (name, src, L, steps, policy, eps) in enumerate([
+        ("P2_training_L4", "set:P2_training", 4, S(600), "random", 0.0),
+        ("maze8x8s22_L4", "file:P2_training/maze_8x8_seed22.txt", 4, S(400), "random", 0.0),
+        ("box8x8x4_L4_random", "box:8x8x4", 4, S(400), "random", 0.0),
+        ("maze8x8s22_L10_seek", "file:P2_training/maze_8x8_seed22.txt", 10, S(900), "seek", 0.25),
+        ("kitchen2_L10_seek", "file:P3_training/kitchen2.txt", 10, S(700), "seek", 0.2),
+        ("P3_training_L10_seek", "set:P3_training", 10, S(1200), "seek", 0.15),
+        ("P2_training_L4_seek", "set:P2_training", 4, S(1000), "seek", 0.3),
     ]):
         rp, _ = resolve(src)
         env = make_env(room_path=rp, L=L, cls=simple.GridAgent)
         seeds = [77 + 31 * k for k in range(64)]
-        t = run_trajectory(env, seeds, steps, "random", policy_seed=5000 + i, eps=0.0, simple=True)
-        np.savez_compressed(OUT / f"simple_{name}.npz", **t, L=np.int64(L), room_source=np.asarray(src))
-        print(f"simple_{name}: {len(t['actions'])} steps")
+        t = run_trajectory(env, seeds, steps, policy, policy_seed=5000 + i, eps=eps, simple=True)
+        np.savez_compressed(OUT / f"simple_{name}.npz", **t, L=np.int64(L), room_source=np.asarray(src),
+                            policy=np.asarray(policy))
+        print(f"simple_{name}: {len(t['actions'])} steps, {len(t['reset_at'])} episodes, "
+              f"term={int(t['terminated'].sum())} trunc={int(t['truncated'].sum())}")
     shutil.rmtree(tmp, ignore_errors=True)
 
 

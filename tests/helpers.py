@@ -66,11 +66,16 @@ def source_texts(src: str):
     raise ValueError(src)
 
 
-def oracle_env(src: str, L: int, n_agents: int = 1, crash_penalty: float = -2.0):
+def oracle_env(src: str, L: int, n_agents: int = 1, crash_penalty: float = -2.0, variant: int = 0):
     from oracle.oracle import OracleEnv, parse_room_text, walled_box
     texts, draw, whd = source_texts(src)
     rooms = [walled_box(*whd)] if whd else [parse_room_text(t, n) for n, t in texts]
-    return OracleEnv(rooms, n_agents=n_agents, local_map_length=L, crash_penalty=crash_penalty, use_room_draw=draw)
+    return OracleEnv(rooms, n_agents=n_agents, local_map_length=L, crash_penalty=crash_penalty, use_room_draw=draw,
+                     variant=variant)
+
+
+def simple_golden_trajectories():
+    return sorted(GOLDEN.glob("simple_*.npz"))
 
 
 def product_room_set(src: str):

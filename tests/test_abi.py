@@ -21,7 +21,7 @@ def test_library_loads_and_exports_header_symbols():
     for name in decl:
         assert hasattr(lib, name), name
     assert set(decl) == set(_native.EXPORTED_SYMBOLS)
-    assert lib.vn_abi_version() == 1
+    assert lib.vn_abi_version() == _native.VN_ABI_VERSION == 2
     out = subprocess.run(["nm", "-D", "--defined-only", str(_native._build.LIB)], capture_output=True, text=True)
     exported = set(re.findall(r" T (vn_\w+)", out.stdout))
     assert set(decl) <= exported
@@ -44,7 +44,10 @@ def test_errors_cross_the_boundary_as_codes():
     import numpy as np
     whd = np.array([4, 4, 4], np.int32)
     walls = np.zeros(64, np.uint8)
-    rs = _native.VnRoomSet(1, whd.ctypes.data, walls.ctypes.data, None)
+    rs = _native.VnRoomSet(1, whd.ctypes.data, walls.ctypes.data, None, None)
     rc = lib.vn_create(ctypes.byref(rs), 4, ctypes.byref(cfg), 0, ctypes.byref(h))
     assert rc == -1 and b"local_map_length" in lib.vn_last_error()
     assert lib.vn_step(None, None, None, None, None, None, None, None, None) == -1
+    bad = _native.VnConfig(4, 1, 1, 7, -2.0, 0.84, 0, 0)  # unknown variant
+    rc = lib.vn_create(ctypes.byref(rs), 4, ctypes.byref(bad), 0, ctypes.byref(h))
+    assert rc == -1 and b"variant" in lib.vn_last_error()

@@ -13,6 +13,7 @@ import numpy as np
 import pytest
 
 from helpers import (GOLDEN, STATE13, archive_texts, golden_trajectories, grid_hash, load_golden, oracle_env,
+                     simple_golden_trajectories,
                      set_members)
 from oracle import oracle as O
 
@@ -143,3 +144,54 @@ def test_oracle_gae_known_answer():
     np.testing.assert_array_equal(adv[:, 0], np.array([0.6875, 0.25, 2.0], np.float32))
     np.testing.assert_array_equal(adv[:, 1], np.array([0.0, 1.0, 0.0], np.float32))
     np.testing.assert_array_equal(ret, adv + v)
+
+
+SIMPLE_STATE = ("x", "y", "z", "facing", "last_action", "step_count", "visited_count", "bump_count", "done")
+
+
+def simple_state_row(env, agent=0):
+    st = env.state(agent)
+    return [st[f] for f in SIMPLE_STATE]
+
+
+def simple_reset_row(env, agent=0):
+    st = env.state(agent)
+    # for the simpleEnv variant, state fields 9..11 hold the goal (gx, gy, gz)
+    return [st["x"], st["y"], st["z"], st["last_bump"], st["near_wall"], st["was_near_wall"]]
+
+
+def replay_simple_oracle(d, env):
+    """Replay a golden simpleEnv trajectory (envs/simpleEnv.py, reset seeded
+    with random.seed(seed) then get_obs(), as tests/golden/gen_golden.py ran it)."""
+    seeds = list(d["seeds"])
+    si = 0
+    obs = env.reset(0, int(seeds[si]))
+    si += 1
+    assert obs.tobytes() == d["reset_obs"][0].tobytes()
+    assert simple_reset_row(env) == list(d["reset_state"][0])
+    ri = 1
+    for t, a in enumerate(d["actions"]):
+        obs, r, te, tr = env.step(0, int(a))
+        assert obs.tobytes() == d["obs"][t].tobytes(), f"obs mismatch at step {t}"
+        assert r == float(d["reward"][t]), f"reward mismatch at step {t}: {r!r} vs {d['reward'][t]!r}"
+        assert (te, tr) == (bool(d["terminated"][t]), bool(d["truncated"][t])), t
+        assert simple_state_row(env) == list(d["state"][t]), f"state mismatch at step {t}"
+        assert grid_hash(env.belief(0)) == int(d["belief_hash"][t]), f"belief mismatch at step {t}"
+        if te or tr:
+            obs = env.reset(0, int(seeds[si]))
+            si += 1
+            assert obs.tobytes() == d["reset_obs"][ri].tobytes()
+            assert simple_reset_row(env) == list(d["reset_state"][ri])
+            ri += 1
+    assert si == len(seeds)
+
+
+@pytest.mark.parametrize("path", simple_golden_trajectories(), ids=lambda p: p.stem)
+def test_oracle_replays_simple_golden(path):
+    d = load_golden(path)
+    env = oracle_env(str(d["room_source"]), int(d["L"]), variant=1)
+    assert env.obs_dim == 6 * int(d["L"]) + 7
+    replay_simple_oracle(d, env)
+    # the room the golden ran in is the one the oracle parsed (raw tokens, walls == 2)
+    st = env.state(0)
+    assert grid_hash(env.rooms[st["room"]].tokens) in {int(h) for h in d["room_hash"]}

@@ -63,7 +63,7 @@ def test_text_round_trip_and_box():
 
 def test_pack_layout():
     rs = R.load_archive_set("P2_training")
-    whd, walls, fs = rs.pack()
+    whd, walls, fs, gl = rs.pack()
     assert whd.shape == (25, 3) and walls.dtype == np.uint8
     assert walls.size == int(np.prod(whd, axis=1).sum())
     off = 0
@@ -72,3 +72,28 @@ def test_pack_layout():
         assert (walls[off:off + n].reshape(tuple(s)) == r.walls).all()
         off += n
     assert (fs == -1).all()
+
+
+def test_simple_variant_walls_match_oracle_tokens():
+    """simpleEnv keeps raw file values: only 2 is a wall, -2 is free
+    (envs/simpleEnv.py:282, :381); checked on every reference room file."""
+    from helpers import archive_texts
+    from oracle.oracle import parse_room_text
+    n_minus2 = 0
+    for rel, text in archive_texts().items():
+        if not rel.endswith(".txt"):
+            continue
+        r = R.parse_room(text, rel)
+        o = parse_room_text(text, rel)
+        assert (r.walls_for(R.VARIANT_SIMPLE) == o.simple_walls.astype(bool)).all(), rel
+        assert (r.walls_for(R.VARIANT_CUBIC) == o.walls.astype(bool)).all(), rel
+        n_minus2 += r.minus2 is not None
+    assert n_minus2 >= 1     # kitchen2.txt
+
+
+def test_pack_goal_and_variant_walls():
+    text = R.room_to_text(R.box_room(6, 5, 4)).replace("Size=6,5,4\n", "Size=6,5,4\nGoal=2,3,1\n")
+    room = R.parse_room(text)
+    rs = R.RoomSet([room])
+    whd, walls, fs, gl = rs.pack(R.VARIANT_SIMPLE)
+    assert tuple(gl[0]) == (2, 3, 1) and (fs == -1).all()
