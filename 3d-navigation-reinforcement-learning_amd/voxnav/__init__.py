@@ -7,14 +7,17 @@ include/voxnav.h.  Public API:
 
   rooms.*             room-file parser / room sets / synthetic boxes
   BatchedGridEnv      N agents per GPU, torch tensors in/out, SB3 auto-reset
-  GridAgent           the reference's single-env gymnasium API
+  GridAgent           the reference's single-env gymnasium API (CubicEnv)
+  SimpleGridAgent     the same for the goal-seeking simpleEnv variant
+  RolloutCollector    on-device PPO rollout collection (policy in the loop)
   compute_gae         GAE advantage/return scan kernel
   sharding            multi-GPU agent sharding helpers
 """
 from . import rooms  # noqa: F401
 from ._native import VoxnavError, load as load_library  # noqa: F401
 
-__all__ = ["rooms", "BatchedGridEnv", "GridAgent", "compute_gae", "VoxnavError", "load_library"]
+__all__ = ["rooms", "BatchedGridEnv", "GridAgent", "SimpleGridAgent", "RolloutCollector", "compute_gae",
+           "VoxnavError", "load_library"]
 
 
 def __getattr__(name):
@@ -25,6 +28,12 @@ def __getattr__(name):
     if name == "GridAgent":
         from .gym_api import GridAgent
         return GridAgent
+    if name == "SimpleGridAgent":
+        from .gym_api import SimpleGridAgent
+        return SimpleGridAgent
+    if name == "RolloutCollector":
+        from .collector import RolloutCollector
+        return RolloutCollector
     if name == "compute_gae":
         from .gae import compute_gae
         return compute_gae

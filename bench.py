@@ -52,6 +52,8 @@ def parse():
     ap.add_argument("--single-step-check", type=int, default=1,
                     help="also time the drop-in one-step-per-launch call (vn_step_random k=1)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline sample budget (0 = skip)")
+    ap.add_argument("--simple", type=int, default=1,
+                    help="also time the simpleEnv variant (envs/simpleEnv.py) on the same agents/room, L=4")
     ap.add_argument("--collector", default="lstm", choices=["lstm", "mlp", "none"],
                     help="also time the policy-in-the-loop rollout collector (PPO-LSTM / PPO-MLP)")
     ap.add_argument("--collector-rooms", default="P3_training", help="reference room set for the collector leg")
@@ -89,6 +91,12 @@ def cpu_baseline(room_whd, L, seconds):
     return {"value": steps / el, "unit": "env-steps/s", "cores": threads, "kind": "port",
             "sample": f"{N} agents x {steps // N} steps of the same workload ({el:.1f} s) through "
                       f"oracle/voxnav_oracle.c (C restatement of envs/CubicEnv.py, OpenMP over agents)"}
+
+
+def simple_bytes_per_step(L: int) -> int:
+    """simpleEnv variant: action 1 + ray cells 6L + state 2*16 + goal 4 +
+    obs 4*(6L+7) + reward 4 + flags 2."""
+    return 1 + 6 * L + 32 + 4 + 4 * (6 * L + 7) + 4 + 2
 
 
 def lstm_flops_per_agent_step(obs=80, H=256, arch=(256, 256, 128), A=6) -> int:
@@ -179,8 +187,9 @@ def main():
                          autoreset=True, device=dev, agent_id_base=rank * N, seed_stride=N * world)
     env.reset(seed=42)
     from voxnav.env import Rollout
-    def run(F, steps, warmup):
-        out = Rollout(torch.empty((F, N, 80), dtype=torch.float32, device=dev),
+
+    def run(F, steps, warmup, env=env):
+        out = Rollout(torch.empty((F, N, env.obs_dim), dtype=torch.float32, device=dev),
                       torch.empty((F, N), dtype=torch.float32, device=dev),
                       torch.empty((F, N), dtype=torch.uint8, device=dev),
                       torch.empty((F, N), dtype=torch.uint8, device=dev), None)
@@ -214,6 +223,22 @@ def main():
         _, _, st1, el1, km1 = run(1, min(args.steps, 100), 10)
         single = {"value": round(N * world * st1 / el1, 1), "steps": st1, "kernel_avg_us": round(km1 * 1e3, 3)}
     out, warm_steps, steps_timed, elapsed, kern_ms = run(F, args.steps, args.warmup)
+    simple = None
+    if args.simple:
+        senv = BatchedGridEnv(num_agents=N, rooms=single_room_set(box_room(W, D, H)), local_map_length=4,
+                              autoreset=True, device=dev, agent_id_base=rank * N, seed_stride=N * world,
+                              variant="simple")
+        senv.reset(seed=42)
+        _, _, st_s, el_s, km_s = run(F, args.steps, args.warmup, env=senv)
+        sb = simple_bytes_per_step(4)
+        sach = sb * N * F / (km_s * 1e-3) / 1e9
+        simple = {"value": round(N * world * st_s / el_s, 1), "unit": "env-steps/s", "variant": "envs/simpleEnv.py",
+                  "room": f"{W}x{D}x{H}", "local_map_length": 4, "steps": st_s, "steps_per_launch": F,
+                  "kernel_avg_us": round(km_s * 1e3, 3),
+                  "roofline": {"bound": "hbm", "achieved": round(sach, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                               "frac": round(sach / HBM_PEAK_GBS, 5), "algorithmic_bytes_per_env_step": sb}}
+        senv.close()
+        del senv
     coll = None
     if args.collector != "none":
         coll = collector_leg(args, torch, dist, dev, rank, world, N)
@@ -254,6 +279,8 @@ def main():
         }
         if single is not None:
             rec["drop_in_single_step"] = single   # vn_step-shaped call: one env step per launch
+        if simple is not None:
+            rec["simple_env"] = simple            # goal-seeking variant
         if coll is not None:
             rec["collector"] = coll               # policy in the loop
         if world == 1 and args.cpu_seconds > 0:

@@ -8,7 +8,7 @@ set -u
 cd "${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-BARGS="${BENCH_ARGS:-} --single-step-check 0 --collector none"
+BARGS="${BENCH_ARGS:-} --single-step-check 0 --collector none --simple 0"
 TAG=${TAG:-r01}
 step() {
   local name=$1 t=$2; shift 2

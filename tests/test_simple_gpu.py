@@ -153,3 +153,23 @@ def test_simple_sharding_and_fusion_invariance(voxnav):
     steps = [single.step_random(1, policy_seed=5, t0=k) for k in range(K)]
     assert torch.equal(torch.cat([s.obs for s in steps], 0), a.obs)
     assert torch.equal(torch.cat([s.reward for s in steps], 0), a.reward)
+
+
+def test_simple_gridagent_facade_matches_golden(voxnav):
+    from voxnav.gym_api import SimpleGridAgent
+    d = load_golden(sorted(p for p in simple_golden_trajectories() if "kitchen2" in p.name)[0])
+    ag = SimpleGridAgent(local_map_length=int(d["L"]), rooms=product_room_set(str(d["room_source"])).rooms)
+    assert ag.reset(seed=int(d["seeds"][0])) is None          # the reference's reset returns None
+    assert ag.get_obs().tobytes() == d["reset_obs"][0].tobytes()
+    assert ag.observation_space.shape == (6 * int(d["L"]) + 7,)
+    assert (ag.gx, ag.gy, ag.gz) == tuple(int(v) for v in d["reset_state"][0][3:])
+    si = 1
+    for t, a in enumerate(d["actions"][:200]):
+        obs, r, te, tr, info = ag.step(int(a))
+        assert isinstance(r, np.float64) and r == d["reward"][t]
+        assert obs.tobytes() == d["obs"][t].tobytes()
+        assert (ag.visited_count, ag.bump_count, ag.done) == (d["state"][t][6], d["state"][t][7], bool(d["state"][t][8]))
+        if te or tr:
+            ag.reset(seed=int(d["seeds"][si]))
+            si += 1
+    ag.close()
