@@ -2,6 +2,7 @@
 """Interleaved A/B timing of library variants in ONE process (same device,
 same state), e.g.  python scripts/ab.py --variants base:path.so,lb4:other.so"""
 import argparse
+import os
 import json
 import sys
 import time
@@ -23,35 +24,44 @@ def main():
     ap.add_argument("--steps", type=int, default=256)
     ap.add_argument("--rounds", type=int, default=5)
     a = ap.parse_args()
-    libs = {}
+    libs, ablate = {}, {}
     for v in a.variants.split(","):
-        name, path = v.split(":", 1)
+        parts = v.split(":")
+        name, path = parts[0], parts[1]
+        ablate[name] = parts[2] if len(parts) > 2 else "0"     # VOXNAV_ABLATE bits (diagnostics)
         libs[name] = _native.load_variant(REPO / path if not path.startswith("/") else path)
     cfgs = [c.split(":") for c in a.configs.split(",")]
-    envs, outs = {}, {}
-    for name, lib in libs.items():
+    # One env alive at a time, created and destroyed per measurement, so every
+    # variant gets the same device allocations (HBM placement shifts the
+    # throughput of the same code by 10-15 % between allocations).
+    outs = {}
+    for c in cfgs:
+        n, F = int(c[0]), int(c[3])
+        outs[tuple(c)] = Rollout(torch.empty((F, n, 80), device="cuda:0"), torch.empty((F, n), device="cuda:0"),
+                                 torch.empty((F, n), dtype=torch.uint8, device="cuda:0"),
+                                 torch.empty((F, n), dtype=torch.uint8, device="cuda:0"), None)
+    res = {(name, tuple(c)): [] for name in libs for c in cfgs}
+    for r in range(a.rounds):
         for c in cfgs:
             n, room, L, F = int(c[0]), c[1], int(c[2]), int(c[3])
             rs = load_archive_set(room) if room.startswith("P") else single_room_set(box_room(*map(int, room.split("x"))))
-            e = BatchedGridEnv(num_agents=n, rooms=rs, local_map_length=L, autoreset=True, device="cuda:0", lib=lib)
-            e.reset(seed=42)
-            envs[(name, tuple(c))] = e
-            outs[(name, tuple(c))] = Rollout(torch.empty((F, n, 80), device="cuda:0"), torch.empty((F, n), device="cuda:0"),
-                                              torch.empty((F, n), dtype=torch.uint8, device="cuda:0"),
-                                              torch.empty((F, n), dtype=torch.uint8, device="cuda:0"), None)
-    res = {k: [] for k in envs}
-    for r in range(a.rounds):
-        for k, e in envs.items():
-            F = int(k[1][3])
-            o = outs[k]
-            for _ in range(2):
-                e.step_random(F, out=o)
-            torch.cuda.synchronize()
-            t0 = time.perf_counter()
-            for _ in range(max(1, a.steps // F)):
-                e.step_random(F, out=o)
-            torch.cuda.synchronize()
-            res[k].append(e.num_agents * max(1, a.steps // F) * F / (time.perf_counter() - t0))
+            names = list(libs) if r % 2 == 0 else list(libs)[::-1]
+            for name in names:
+                os.environ["VOXNAV_ABLATE"] = ablate[name]
+                e = BatchedGridEnv(num_agents=n, rooms=rs, local_map_length=L, autoreset=True, device="cuda:0",
+                                   lib=libs[name])
+                e.reset(seed=42)
+                o = outs[tuple(c)]
+                for _ in range(max(2, 64 // F)):
+                    e.step_random(F, out=o)
+                torch.cuda.synchronize()
+                t0 = time.perf_counter()
+                for _ in range(max(1, a.steps // F)):
+                    e.step_random(F, out=o)
+                torch.cuda.synchronize()
+                res[(name, tuple(c))].append(n * max(1, a.steps // F) * F / (time.perf_counter() - t0))
+                e.close()
+                del e
     for k, v in res.items():
         v = sorted(v)
         print(json.dumps({"variant": k[0], "config": ":".join(k[1]), "Gsteps_median": round(v[len(v) // 2] / 1e9, 3),
