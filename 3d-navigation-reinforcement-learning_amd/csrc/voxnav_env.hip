@@ -814,7 +814,7 @@ __device__ __forceinline__ int sense_observe(const Params &p, int8_t *map, uint6
                 const uint64_t nv = pn[w] | pm[w];
                 if (pofs + w == 0) pc_.w[0] = nv;
                 else if (pofs + w == 1) pc_.w[1] = nv;
-                if (!(p.ablate & 2u)) prow[pw0 + w] = nv;
+                if (!(p.ablate & 32u)) prow[pw0 + w] = nv;
             }
         }
         const int sh = pa - pw0 * 64;      // 0..63
@@ -829,8 +829,8 @@ __device__ __forceinline__ int sense_observe(const Params &p, int8_t *map, uint6
         const uint32_t ryh = (uint32_t)__shfl((int)(uint32_t)(rel >> 32), 1, GROUP);
         const int pax = __shfl(pa, 0, GROUP), pay = __shfl(pa, 1, GROUP);
         const uint64_t lane_sel = 0x1111111111111111ull << q;
-        uint64_t mx = (p.ablate & 2u) ? 0ull : (((uint64_t)rxh << 32) | rxl) & lane_sel;
-        uint64_t my = (p.ablate & 2u) ? 0ull : (((uint64_t)ryh << 32) | ryl) & lane_sel;
+        uint64_t mx = (p.ablate & 32u) ? 0ull : (((uint64_t)rxh << 32) | rxl) & lane_sel;
+        uint64_t my = (p.ablate & 32u) ? 0ull : (((uint64_t)ryh << 32) | ryl) & lane_sel;
         while (mx) {
             const int pos = pax + __ffsll((unsigned long long)mx) - 1;
             mx &= mx - 1;
@@ -1742,8 +1742,9 @@ int vn_create(const VnRoomSet *rooms, int32_t n_agents, const VnConfig *cfg, int
     e->total_free = total_free;
     // timing diagnostics only; every ablation keeps all addresses inside the
     // agent's room (bits: 1 entering-column loads, 2 plane rows and blind marks,
-    // 4 obs rows, 8 column write-backs, 16 obs flush to HBM)
-    if (const char *ab = getenv("VOXNAV_ABLATE")) e->ablate = (uint32_t)strtoul(ab, nullptr, 0) & 0x1fu;
+    // 4 obs rows, 8 column write-backs, 16 obs flush to HBM, 32 plane word writes
+    // and blind marks; 2 skips the plane row loads)
+    if (const char *ab = getenv("VOXNAV_ABLATE")) e->ablate = (uint32_t)strtoul(ab, nullptr, 0) & 0x3fu;
     e->variant = cfg->variant;
     e->obs_dim = cfg->variant == VN_VARIANT_SIMPLE ? 6 * cfg->local_map_length + 7 : VN_OBS_DIM;
     e->nbx = (maxW + 3) / 4;
