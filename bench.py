@@ -11,7 +11,10 @@ random.choice over the one-room set), local_map_length L=10
 timed region; every step writes the full obs [N,80] f32, reward, terminated
 and truncated tensors.
 
-One "step" = one batched env step of all agents on the GPU.  ``--fuse F``
+One "step" = one batched env step of all agents on the GPU; the default
+timed window is 5,408 steps, one full episode of the 32x32x8 box
+(episodes truncate at total_free_cells = 5,400 steps), so the number is the
+episode-average throughput rather than one phase of it.  ``--fuse F``
 advances F steps per kernel launch (obs written for every step into a
 [F, N, 80] trajectory buffer, i.e. the rollout-buffer shape); F=1 is the
 drop-in VecEnv.step call.
@@ -43,7 +46,10 @@ def algorithmic_bytes_per_step(L: int) -> int:
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=256)
+    # 5408 = one whole 5,400-step episode of the 32x32x8 box (every agent
+    # starts at t=0): the timed window covers every phase of an episode,
+    # early exploration, steady state and the auto-reset
+    ap.add_argument("--steps", type=int, default=5408)
     ap.add_argument("--warmup", type=int, default=32)
     ap.add_argument("--agents", type=int, default=65536, help="agents per GPU")
     ap.add_argument("--room", default="32x32x8", help="WxDxH of the walled-box room")

@@ -17,12 +17,12 @@ step() {
   echo "[$name] rc=$rc"; grep -h '"metric"' "gpurun_out/${TAG}_$name.log" | cut -c1-200
   [ $rc -eq 0 ] || exit $rc
 }
-step trace 400 rocprofv3 --kernel-trace --stats -d gpurun_out/${TAG}_trace -o trace --output-format csv -- python3 bench.py --steps 640 --warmup 64 --cpu-seconds 0 $BARGS
+step trace 400 rocprofv3 --kernel-trace --stats -d gpurun_out/${TAG}_trace -o trace --output-format csv -- python3 bench.py --steps 5408 --warmup 32 --cpu-seconds 0 $BARGS
 step trace_f1 400 rocprofv3 --kernel-trace --stats -d gpurun_out/${TAG}_trace_f1 -o trace --output-format csv -- python3 bench.py --steps 200 --warmup 20 --cpu-seconds 0 $BARGS --fuse 1
-step fetch 400 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/${TAG}_fetch -o fetch --output-format csv -- python3 bench.py --steps 64 --warmup 16 --cpu-seconds 0 $BARGS
-step write 400 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/${TAG}_write -o write --output-format csv -- python3 bench.py --steps 64 --warmup 16 --cpu-seconds 0 $BARGS
-step l2 400 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum -d gpurun_out/${TAG}_l2 -o l2 --output-format csv -- python3 bench.py --steps 64 --warmup 16 --cpu-seconds 0 $BARGS
-step sq 400 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_LDS SQ_INSTS_BRANCH SQ_INSTS_SMEM -d gpurun_out/${TAG}_sq -o sq --output-format csv -- python3 bench.py --steps 64 --warmup 16 --cpu-seconds 0 $BARGS
-step sqw 400 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU -d gpurun_out/${TAG}_sqw -o sqw --output-format csv -- python3 bench.py --steps 64 --warmup 16 --cpu-seconds 0 $BARGS
-step tcp 400 rocprofv3 --pmc TCP_TCC_READ_REQ_sum TCP_PENDING_STALL_CYCLES_sum -d gpurun_out/${TAG}_tcp -o tcp --output-format csv -- python3 bench.py --steps 64 --warmup 16 --cpu-seconds 0 $BARGS
+step fetch 400 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/${TAG}_fetch -o fetch --output-format csv -- python3 bench.py --steps 5408 --warmup 32 --cpu-seconds 0 $BARGS
+step write 400 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/${TAG}_write -o write --output-format csv -- python3 bench.py --steps 5408 --warmup 32 --cpu-seconds 0 $BARGS
+step l2 400 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum -d gpurun_out/${TAG}_l2 -o l2 --output-format csv -- python3 bench.py --steps 5408 --warmup 32 --cpu-seconds 0 $BARGS
+step sq 400 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_LDS SQ_INSTS_BRANCH SQ_INSTS_SMEM -d gpurun_out/${TAG}_sq -o sq --output-format csv -- python3 bench.py --steps 5408 --warmup 32 --cpu-seconds 0 $BARGS
+step sqw 400 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU -d gpurun_out/${TAG}_sqw -o sqw --output-format csv -- python3 bench.py --steps 5408 --warmup 32 --cpu-seconds 0 $BARGS
+step tcp 400 rocprofv3 --pmc TCP_TCC_READ_REQ_sum TCP_PENDING_STALL_CYCLES_sum -d gpurun_out/${TAG}_tcp -o tcp --output-format csv -- python3 bench.py --steps 5408 --warmup 32 --cpu-seconds 0 $BARGS
 exit 0
