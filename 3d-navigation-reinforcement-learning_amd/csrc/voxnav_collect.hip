@@ -39,6 +39,26 @@ namespace {
 
 __device__ __forceinline__ float sigm(float x) { return 1.0f / (1.0f + expf(-x)); }
 
+// bf16 (stored as uint16_t) <-> f32; f32 -> bf16 rounds to nearest even
+// (torch's rounding; the values here are finite)
+__device__ __forceinline__ float bf2f(uint32_t b) { return __uint_as_float(b << 16); }
+__device__ __forceinline__ uint32_t f2bf(float f) {
+    const uint32_t u = __float_as_uint(f);
+    return (u + 0x7FFFu + ((u >> 16) & 1u)) >> 16;
+}
+
+template <typename T>
+__device__ __forceinline__ float4 load4(const T *p);
+template <>
+__device__ __forceinline__ float4 load4<float>(const float *p) {
+    return *reinterpret_cast<const float4 *>(p);
+}
+template <>
+__device__ __forceinline__ float4 load4<uint16_t>(const uint16_t *p) {
+    const uint2 v = *reinterpret_cast<const uint2 *>(p);
+    return make_float4(bf2f(v.x & 0xffffu), bf2f(v.x >> 16), bf2f(v.y & 0xffffu), bf2f(v.y >> 16));
+}
+
 // Philox4x32-10 (same rounds as the env's random policy); the sampler's
 // counter is (global agent id, t | 2^63) so it never collides with the
 // env's random-policy stream (gid, t / 4) under the same key.
@@ -69,12 +89,16 @@ __device__ __forceinline__ uint32_t philox_word0(uint64_t key, uint64_t gid, uin
 //   gx  element (b, n, j) at gx[n*gx_row + b*4H + j]   (one GEMM for all LSTMs)
 //   gh  [B][N][4H] or NULL (state was zero)
 //   h, c, h_store, c_store  [B][N][H]
+// T = float, or uint16_t for bf16 gate pre-activations (the bf16 policy
+// path, which also writes h in bf16 for the next GEMMs into h_bf).
 // ----------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void lstm_cell_kernel(const float *__restrict__ gx, int64_t gx_row,
-                                                        const float *__restrict__ gh, const float *__restrict__ b_ih,
+template <typename T>
+__global__ __launch_bounds__(256) void lstm_cell_kernel(const T *__restrict__ gx, int64_t gx_row,
+                                                        const T *__restrict__ gh, const float *__restrict__ b_ih,
                                                         const float *__restrict__ b_hh, float *__restrict__ h,
-                                                        float *__restrict__ c, float *__restrict__ h_store,
-                                                        float *__restrict__ c_store, int B, int N, int H) {
+                                                        float *__restrict__ c, uint16_t *__restrict__ h_bf,
+                                                        float *__restrict__ h_store, float *__restrict__ c_store,
+                                                        int B, int N, int H) {
     const int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const int H4 = H >> 2;
     const int64_t per_b = (int64_t)N * H4;
@@ -84,19 +108,19 @@ __global__ __launch_bounds__(256) void lstm_cell_kernel(const float *__restrict_
     const int64_t n = r / H4;
     const int j = (int)(r - n * H4) * 4;
     const int G = 4 * H;
-    const float *px = gx + n * gx_row + (int64_t)b * G + j;
-    const float *ph = gh ? gh + ((int64_t)b * N + n) * G + j : nullptr;
+    const T *px = gx + n * gx_row + (int64_t)b * G + j;
+    const T *ph = gh ? gh + ((int64_t)b * N + n) * G + j : nullptr;
     const float *pbi = b_ih + (int64_t)b * G + j;
     const float *pbh = b_hh + (int64_t)b * G + j;
     float4 pre[4];
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
-        const float4 x = *reinterpret_cast<const float4 *>(px + k * H);
+        const float4 x = load4<T>(px + k * H);
         const float4 bi = *reinterpret_cast<const float4 *>(pbi + k * H);
         const float4 bh = *reinterpret_cast<const float4 *>(pbh + k * H);
         float4 s = x;
         if (ph) {
-            const float4 y = *reinterpret_cast<const float4 *>(ph + k * H);
+            const float4 y = load4<T>(ph + k * H);
             s.x += y.x; s.y += y.y; s.z += y.z; s.w += y.w;
         }
         s.x += bi.x; s.y += bi.y; s.z += bi.z; s.w += bi.w;
@@ -118,6 +142,9 @@ __global__ __launch_bounds__(256) void lstm_cell_kernel(const float *__restrict_
 #undef VN_CELL
     *reinterpret_cast<float4 *>(c + so) = cv;
     *reinterpret_cast<float4 *>(h + so) = hv;
+    if (h_bf)
+        *reinterpret_cast<uint2 *>(h_bf + so) =
+            make_uint2(f2bf(hv.x) | (f2bf(hv.y) << 16), f2bf(hv.z) | (f2bf(hv.w) << 16));
     if (h_store) *reinterpret_cast<float4 *>(h_store + so) = hv;
     if (c_store) *reinterpret_cast<float4 *>(c_store + so) = cv;
 }
@@ -135,8 +162,9 @@ __global__ __launch_bounds__(256) void lstm_cell_kernel(const float *__restrict_
 // ----------------------------------------------------------------------------
 constexpr int HEAD_MAX_A = 8;
 
-__global__ __launch_bounds__(256) void policy_head_kernel(const float *__restrict__ lat_pi,
-                                                          const float *__restrict__ lat_vf, int N, int P,
+template <typename T>
+__global__ __launch_bounds__(256) void policy_head_kernel(const T *__restrict__ lat_pi,
+                                                          const T *__restrict__ lat_vf, int N, int P,
                                                           const float *__restrict__ wa, const float *__restrict__ ba,
                                                           int A, const float *__restrict__ wv,
                                                           const float *__restrict__ bv, uint64_t seed, uint64_t t,
@@ -158,7 +186,7 @@ __global__ __launch_bounds__(256) void policy_head_kernel(const float *__restric
     if (live) {
         for (int k = l * 4; k < P; k += 64) {
             if (lat_pi) {
-                const float4 x = *reinterpret_cast<const float4 *>(lat_pi + n * P + k);
+                const float4 x = load4<T>(lat_pi + n * P + k);
 #pragma unroll
                 for (int a = 0; a < HEAD_MAX_A; ++a) {
                     if (a < A) {
@@ -171,7 +199,7 @@ __global__ __launch_bounds__(256) void policy_head_kernel(const float *__restric
                 }
             }
             if (lat_vf) {
-                const float4 x = *reinterpret_cast<const float4 *>(lat_vf + n * P + k);
+                const float4 x = load4<T>(lat_vf + n * P + k);
                 const float *w = sw + A * P + k;
                 acc[HEAD_MAX_A] += x.x * w[0];
                 acc[HEAD_MAX_A] += x.y * w[1];
@@ -326,7 +354,8 @@ __global__ __launch_bounds__(256) void bootstrap_kernel(const int32_t *__restric
 __global__ __launch_bounds__(256) void episode_start_kernel(const uint8_t *__restrict__ term,
                                                             const uint8_t *__restrict__ trunc, int N,
                                                             float *__restrict__ starts, float *__restrict__ h,
-                                                            float *__restrict__ c, int B, int H) {
+                                                            float *__restrict__ c, uint16_t *__restrict__ h_bf,
+                                                            int B, int H) {
     const int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const int H4 = H >> 2;
     if (B == 0) {
@@ -346,6 +375,7 @@ __global__ __launch_bounds__(256) void episode_start_kernel(const uint8_t *__res
         const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
         *reinterpret_cast<float4 *>(h + so) = z;
         *reinterpret_cast<float4 *>(c + so) = z;
+        if (h_bf) *reinterpret_cast<uint2 *>(h_bf + so) = make_uint2(0u, 0u);
     }
 }
 
@@ -355,24 +385,30 @@ unsigned blocks_for(int64_t threads, int per_block = 256) { return (unsigned)((t
 
 extern "C" {
 
-int vn_lstm_cell(const float *gx, int64_t gx_row_stride, const float *gh, const float *b_ih, const float *b_hh,
-                 float *h, float *c, float *h_store, float *c_store, int32_t n_lstm, int32_t N, int32_t H,
-                 void *stream) {
+}  // extern "C"
+
+namespace {
+
+template <typename T>
+int lstm_cell_launch(const T *gx, int64_t gx_row_stride, const T *gh, const float *b_ih, const float *b_hh, float *h,
+                     float *c, uint16_t *h_bf, float *h_store, float *c_store, int32_t n_lstm, int32_t N, int32_t H,
+                     void *stream) {
     if (!gx || !b_ih || !b_hh || !h || !c) return fail(VN_ERR_INVALID, "NULL argument");
     if (n_lstm < 1 || N < 1 || H < 4 || (H & 3)) return fail(VN_ERR_INVALID, "bad sizes n_lstm=%d N=%d H=%d", n_lstm, N, H);
     if (gx_row_stride < (int64_t)n_lstm * 4 * H || (gx_row_stride & 3))
         return fail(VN_ERR_INVALID, "gx_row_stride %lld too small / unaligned", (long long)gx_row_stride);
     const int64_t threads = (int64_t)n_lstm * N * (H / 4);
-    hipLaunchKernelGGL(lstm_cell_kernel, dim3(blocks_for(threads)), dim3(256), 0, (hipStream_t)stream, gx,
-                       gx_row_stride, gh, b_ih, b_hh, h, c, h_store, c_store, (int)n_lstm, (int)N, (int)H);
+    hipLaunchKernelGGL(lstm_cell_kernel<T>, dim3(blocks_for(threads)), dim3(256), 0, (hipStream_t)stream, gx,
+                       gx_row_stride, gh, b_ih, b_hh, h, c, h_bf, h_store, c_store, (int)n_lstm, (int)N, (int)H);
     VN_HIP(hipGetLastError());
     return VN_OK;
 }
 
-int vn_policy_head(const float *latent_pi, const float *latent_vf, int32_t N, int32_t P, const float *w_action,
-                   const float *b_action, int32_t n_actions, const float *w_value, const float *b_value,
-                   uint64_t sample_seed, uint64_t t, int64_t agent_id_base, int32_t deterministic, int32_t *actions,
-                   float *values, float *log_probs, void *stream) {
+template <typename T>
+int policy_head_launch(const T *latent_pi, const T *latent_vf, int32_t N, int32_t P, const float *w_action,
+                       const float *b_action, int32_t n_actions, const float *w_value, const float *b_value,
+                       uint64_t sample_seed, uint64_t t, int64_t agent_id_base, int32_t deterministic,
+                       int32_t *actions, float *values, float *log_probs, void *stream) {
     if (!latent_pi && !latent_vf) return fail(VN_ERR_INVALID, "latent_pi and latent_vf are both NULL");
     if (latent_pi && (!w_action || !b_action || !actions || !log_probs))
         return fail(VN_ERR_INVALID, "NULL action-head argument");
@@ -382,11 +418,46 @@ int vn_policy_head(const float *latent_pi, const float *latent_vf, int32_t N, in
         return fail(VN_ERR_INVALID, "n_actions must be in 1..%d (got %d)", HEAD_MAX_A, n_actions);
     const int A = latent_pi ? n_actions : 0;
     const size_t lds = (size_t)(A + 1) * P * sizeof(float);
-    hipLaunchKernelGGL(policy_head_kernel, dim3(blocks_for(N, 16)), dim3(256), lds, (hipStream_t)stream, latent_pi,
-                       latent_vf, (int)N, (int)P, w_action, b_action, A, w_value, b_value, sample_seed, t,
+    hipLaunchKernelGGL(policy_head_kernel<T>, dim3(blocks_for(N, 16)), dim3(256), lds, (hipStream_t)stream,
+                       latent_pi, latent_vf, (int)N, (int)P, w_action, b_action, A, w_value, b_value, sample_seed, t,
                        agent_id_base, (int)deterministic, actions, values, log_probs);
     VN_HIP(hipGetLastError());
     return VN_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int vn_lstm_cell(const float *gx, int64_t gx_row_stride, const float *gh, const float *b_ih, const float *b_hh,
+                 float *h, float *c, float *h_store, float *c_store, int32_t n_lstm, int32_t N, int32_t H,
+                 void *stream) {
+    return lstm_cell_launch<float>(gx, gx_row_stride, gh, b_ih, b_hh, h, c, nullptr, h_store, c_store, n_lstm, N, H,
+                                   stream);
+}
+
+int vn_lstm_cell_bf16(const uint16_t *gx, int64_t gx_row_stride, const uint16_t *gh, const float *b_ih,
+                      const float *b_hh, float *h, float *c, uint16_t *h_bf16, float *h_store, float *c_store,
+                      int32_t n_lstm, int32_t N, int32_t H, void *stream) {
+    return lstm_cell_launch<uint16_t>(gx, gx_row_stride, gh, b_ih, b_hh, h, c, h_bf16, h_store, c_store, n_lstm, N,
+                                      H, stream);
+}
+
+int vn_policy_head(const float *latent_pi, const float *latent_vf, int32_t N, int32_t P, const float *w_action,
+                   const float *b_action, int32_t n_actions, const float *w_value, const float *b_value,
+                   uint64_t sample_seed, uint64_t t, int64_t agent_id_base, int32_t deterministic, int32_t *actions,
+                   float *values, float *log_probs, void *stream) {
+    return policy_head_launch<float>(latent_pi, latent_vf, N, P, w_action, b_action, n_actions, w_value, b_value,
+                                     sample_seed, t, agent_id_base, deterministic, actions, values, log_probs, stream);
+}
+
+int vn_policy_head_bf16(const uint16_t *latent_pi, const uint16_t *latent_vf, int32_t N, int32_t P,
+                        const float *w_action, const float *b_action, int32_t n_actions, const float *w_value,
+                        const float *b_value, uint64_t sample_seed, uint64_t t, int64_t agent_id_base,
+                        int32_t deterministic, int32_t *actions, float *values, float *log_probs, void *stream) {
+    return policy_head_launch<uint16_t>(latent_pi, latent_vf, N, P, w_action, b_action, n_actions, w_value, b_value,
+                                        sample_seed, t, agent_id_base, deterministic, actions, values, log_probs,
+                                        stream);
 }
 
 int vn_collect_compact(const uint8_t *terminated, const uint8_t *truncated, int32_t N, int32_t *boot_idx,
@@ -413,14 +484,14 @@ int vn_collect_bootstrap(const int32_t *boot_idx, const float *terminal_values, 
 }
 
 int vn_episode_start(const uint8_t *terminated, const uint8_t *truncated, int32_t N, float *episode_starts,
-                     float *h, float *c, int32_t n_lstm, int32_t H, void *stream) {
+                     float *h, float *c, uint16_t *h_bf16, int32_t n_lstm, int32_t H, void *stream) {
     if (!terminated || !truncated) return fail(VN_ERR_INVALID, "NULL argument");
     if (N < 1 || n_lstm < 0) return fail(VN_ERR_INVALID, "bad sizes N=%d n_lstm=%d", N, n_lstm);
     if (n_lstm > 0 && (!h || !c || H < 4 || (H & 3))) return fail(VN_ERR_INVALID, "bad LSTM state arguments");
     if (n_lstm == 0 && !episode_starts) return VN_OK;
     const int64_t threads = n_lstm ? (int64_t)n_lstm * N * (H / 4) : (int64_t)N;
     hipLaunchKernelGGL(episode_start_kernel, dim3(blocks_for(threads)), dim3(256), 0, (hipStream_t)stream,
-                       terminated, truncated, (int)N, episode_starts, h, c, (int)n_lstm, (int)H);
+                       terminated, truncated, (int)N, episode_starts, h, c, h_bf16, (int)n_lstm, (int)H);
     VN_HIP(hipGetLastError());
     return VN_OK;
 }

@@ -24,6 +24,11 @@ per step t
 after T steps: V(obs[T]) under the current critic states, then the GAE scan
 (``vn_gae``) -> advantages, returns.
 
+``policy_dtype="bf16"`` runs the policy GEMMs in bf16 (f32 accumulation,
+bf16 activations; LSTM cell state, heads, sampling and everything after
+them stay f32) -- the reference's SB3 policy is f32, which stays the
+default.
+
 Build-defined (documented in DESIGN.md): the Categorical draw uses a
 counter-based Philox stream keyed by (sample_seed, global agent id, global
 step) instead of torch's global generator, so a rollout is reproducible and
@@ -70,24 +75,30 @@ class RolloutBuffer:
 
 
 class _Weights:
-    """The policy's parameters laid out for the collector's GEMMs/kernels."""
+    """The policy's parameters laid out for the collector's GEMMs/kernels.
 
-    def __init__(self, policy, device):
+    GEMM operands (weights, MLP biases) are in ``dtype`` (f32, or bf16 for
+    the bf16 policy path); LSTM biases and the head weights stay f32 (they
+    are applied inside the HIP kernels in f32)."""
+
+    def __init__(self, policy, device, dtype=torch.float32):
         f = lambda t: t.detach().to(device=device, dtype=torch.float32).contiguous()  # noqa: E731
+        g = lambda t: t.detach().to(device=device, dtype=dtype).contiguous()  # noqa: E731
+        self.dtype = dtype
         self.recurrent = bool(getattr(policy, "recurrent", False))
         if self.recurrent:
             la, lc = policy.lstm_actor, policy.lstm_critic
             if la.num_layers != 1 or lc.num_layers != 1:
                 raise NotImplementedError("one LSTM layer (Grid_Train's n_lstm_layers=1)")
             self.H = la.hidden_size
-            self.w_ih_cat = torch.cat([f(la.weight_ih_l0), f(lc.weight_ih_l0)], 0)      # [2*4H, 80]
-            self.w_hh = [f(la.weight_hh_l0), f(lc.weight_hh_l0)]                       # [4H, H]
-            self.w_ih_vf = f(lc.weight_ih_l0)
+            self.w_ih_cat = torch.cat([g(la.weight_ih_l0), g(lc.weight_ih_l0)], 0)      # [2*4H, 80]
+            self.w_hh = [g(la.weight_hh_l0), g(lc.weight_hh_l0)]                       # [4H, H]
+            self.w_ih_vf = g(lc.weight_ih_l0)
             self.b_ih = torch.stack([f(la.bias_ih_l0), f(lc.bias_ih_l0)])               # [2, 4H]
             self.b_hh = torch.stack([f(la.bias_hh_l0), f(lc.bias_hh_l0)])
         ext = policy.mlp_extractor
-        self.pi = [(f(m.weight), f(m.bias)) for m in ext.linears("pi")]
-        self.vf = [(f(m.weight), f(m.bias)) for m in ext.linears("vf")]
+        self.pi = [(g(m.weight), g(m.bias)) for m in ext.linears("pi")]
+        self.vf = [(g(m.weight), g(m.bias)) for m in ext.linears("vf")]
         self.wa, self.ba = f(policy.action_net.weight), f(policy.action_net.bias)
         self.wv, self.bv = f(policy.value_net.weight).reshape(-1), f(policy.value_net.bias)
         self.A = self.wa.shape[0]
@@ -113,7 +124,7 @@ class RolloutCollector:
 
     def __init__(self, env: BatchedGridEnv, policy, n_steps: int = 128, gamma: float = 0.99, gae_lambda: float = 0.95,
                  sample_seed: int = 42, deterministic: bool = False, store_lstm_states: bool = True,
-                 reset_seed: int = 42):
+                 reset_seed: int = 42, policy_dtype: str = "f32"):
         if not isinstance(policy, (ActorCriticPolicy, RecurrentActorCriticPolicy)):
             raise TypeError("policy must be an ActorCriticPolicy or RecurrentActorCriticPolicy")
         if getattr(policy, "obs_dim", OBS_DIM) != env.obs_dim:
@@ -129,6 +140,10 @@ class RolloutCollector:
         self.deterministic = bool(deterministic)
         self.N = env.num_agents
         self.t_global = 0
+        if policy_dtype not in ("f32", "bf16"):
+            raise ValueError("policy_dtype must be 'f32' (the reference's) or 'bf16'")
+        self.bf16 = policy_dtype == "bf16"
+        self.cdt = torch.bfloat16 if self.bf16 else torch.float32
         self.sync_weights()
         T, N, dev = self.n_steps, self.N, self.device
         z = lambda *s, dt=torch.float32: torch.zeros(s, dtype=dt, device=dev)  # noqa: E731
@@ -150,8 +165,9 @@ class RolloutCollector:
             H = self.w.H
             self.h = z(2, N, H)
             self.c = z(2, N, H)
-            self._gx = z(N, 2 * 4 * H)
-            self._gh = z(2, N, 4 * H)
+            self._gx = z(N, 2 * 4 * H, dt=self.cdt)
+            self._gh = z(2, N, 4 * H, dt=self.cdt)
+            self.h_bf = z(2, N, H, dt=torch.bfloat16) if self.bf16 else None   # GEMM copy of h
             self.store = bool(store_lstm_states)
             self._hs = z(T + 1, 2, N, H) if self.store else None
             self._cs = z(T + 1, 2, N, H) if self.store else None
@@ -161,49 +177,63 @@ class RolloutCollector:
         self._carry = False
 
     def sync_weights(self):
-        self.w = _Weights(self.policy, self.device)
+        self.w = _Weights(self.policy, self.device, self.cdt)
 
     def _stream(self):
         return C.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
 
     # -------------------------------------------------------------- policy
+    def _cell(self, gx, gx_row, gh, b_ih, b_hh, h, c, h_bf, hs, cs, nl, M):
+        if self.bf16:
+            _native.check(self.lib.vn_lstm_cell_bf16(_p(gx), gx_row, _p(gh), _p(b_ih), _p(b_hh), _p(h), _p(c),
+                                                     _p(h_bf), _p(hs), _p(cs), nl, M, self.w.H, self._stream()),
+                          "vn_lstm_cell_bf16")
+        else:
+            _native.check(self.lib.vn_lstm_cell(_p(gx), gx_row, _p(gh), _p(b_ih), _p(b_hh), _p(h), _p(c), _p(hs),
+                                                _p(cs), nl, M, self.w.H, self._stream()), "vn_lstm_cell")
+
+    def _head(self, lat_pi, lat_vf, M, t, actions, values, log_probs):
+        w = self.w
+        fn = self.lib.vn_policy_head_bf16 if self.bf16 else self.lib.vn_policy_head
+        pi = lat_pi is not None
+        _native.check(fn(_p(lat_pi), _p(lat_vf), M, w.P, _p(w.wa) if pi else None, _p(w.ba) if pi else None,
+                         w.A if pi else 0, _p(w.wv), _p(w.bv), self.sample_seed if pi else 0, t if pi else 0,
+                         self.env.agent_id_base if pi else 0, int(self.deterministic) if pi else 0, _p(actions),
+                         _p(values), _p(log_probs), self._stream()), "vn_policy_head")
+
     def _forward(self, obs: torch.Tensor, t: int):
         """Policy step on obs [N, 80] into actions/values/log_probs[t]."""
-        w, lib, N = self.w, self.lib, self.N
+        w, N = self.w, self.N
+        x = obs if not self.bf16 else obs.to(self.cdt)
         if self.recurrent:
             H = w.H
-            torch.mm(obs, w.w_ih_cat.t(), out=self._gx)
-            torch.mm(self.h[0], w.w_hh[0].t(), out=self._gh[0])
-            torch.mm(self.h[1], w.w_hh[1].t(), out=self._gh[1])
+            hin = self.h_bf if self.bf16 else self.h
+            torch.mm(x, w.w_ih_cat.t(), out=self._gx)
+            torch.mm(hin[0], w.w_hh[0].t(), out=self._gh[0])
+            torch.mm(hin[1], w.w_hh[1].t(), out=self._gh[1])
             hs = self._hs[t + 1] if self.store else None
             cs = self._cs[t + 1] if self.store else None
-            _native.check(lib.vn_lstm_cell(_p(self._gx), 8 * H, _p(self._gh), _p(w.b_ih), _p(w.b_hh), _p(self.h),
-                                           _p(self.c), _p(hs), _p(cs), 2, N, H, self._stream()), "vn_lstm_cell")
-            x_pi, x_vf = self.h[0], self.h[1]
+            self._cell(self._gx, 8 * H, self._gh, w.b_ih, w.b_hh, self.h, self.c, self.h_bf, hs, cs, 2, N)
+            x_pi, x_vf = (self.h_bf[0], self.h_bf[1]) if self.bf16 else (self.h[0], self.h[1])
         else:
-            x_pi = x_vf = obs
+            x_pi = x_vf = x
         lat_pi = _mlp(w.pi, x_pi)
         lat_vf = _mlp(w.vf, x_vf)
-        _native.check(lib.vn_policy_head(_p(lat_pi), _p(lat_vf), N, w.P, _p(w.wa), _p(w.ba), w.A, _p(w.wv), _p(w.bv),
-                                         self.sample_seed, self.t_global, self.env.agent_id_base,
-                                         int(self.deterministic), _p(self.actions[t]), _p(self.values[t]),
-                                         _p(self.log_probs[t]), self._stream()), "vn_policy_head")
+        self._head(lat_pi, lat_vf, N, self.t_global, self.actions[t], self.values[t], self.log_probs[t])
 
     def _critic(self, obs: torch.Tensor, h: Optional[torch.Tensor], c: Optional[torch.Tensor], out: torch.Tensor):
         """predict_values: one critic step from state (h, c) [M, H] (consumed), value -> out [M]."""
         w, M = self.w, obs.shape[0]
+        x = obs if not self.bf16 else obs.to(self.cdt)
         if self.recurrent:
             H = w.H
-            gx = torch.mm(obs, w.w_ih_vf.t())
-            gh = torch.mm(h, w.w_hh[1].t())
-            _native.check(self.lib.vn_lstm_cell(_p(gx), 4 * H, _p(gh), _p(w.b_ih[1]), _p(w.b_hh[1]), _p(h), _p(c),
-                                                None, None, 1, M, H, self._stream()), "vn_lstm_cell")
-            x = h
-        else:
-            x = obs
+            gx = torch.mm(x, w.w_ih_vf.t())
+            gh = torch.mm(h if not self.bf16 else h.to(self.cdt), w.w_hh[1].t())
+            h_bf = torch.empty((M, H), dtype=torch.bfloat16, device=self.device) if self.bf16 else None
+            self._cell(gx, 4 * H, gh, w.b_ih[1], w.b_hh[1], h, c, h_bf, None, None, 1, M)
+            x = h_bf if self.bf16 else h
         lat = _mlp(w.vf, x)
-        _native.check(self.lib.vn_policy_head(None, _p(lat), M, w.P, None, None, 0, _p(w.wv), _p(w.bv), 0, 0, 0, 0,
-                                              None, _p(out), None, self._stream()), "vn_policy_head")
+        self._head(None, lat, M, 0, None, out, None)
 
     # -------------------------------------------------------------- rollout
     @torch.no_grad()
@@ -236,6 +266,7 @@ class RolloutCollector:
             _native.check(lib.vn_episode_start(_p(self._term), _p(self._trunc), N, _p(self._starts[t + 1]),
                                                _p(self.h) if self.recurrent else None,
                                                _p(self.c) if self.recurrent else None,
+                                               _p(self.h_bf) if self.recurrent else None,
                                                2 if self.recurrent else 0, self.w.H if self.recurrent else 0, s()),
                           "vn_episode_start")
             self.t_global += 1

@@ -65,6 +65,8 @@ def parse():
     ap.add_argument("--collector-rooms", default="P3_training", help="reference room set for the collector leg")
     ap.add_argument("--collector-T", type=int, default=128, help="rollout length (n_steps) of the collector leg")
     ap.add_argument("--collector-rollouts", type=int, default=2, help="timed rollouts of the collector leg")
+    ap.add_argument("--collector-bf16", type=int, default=1,
+                    help="also time the collector with bf16 policy GEMMs (the reference's policy is f32)")
     ap.add_argument("--json-out", default=None)
     return ap.parse_args()
 
@@ -126,7 +128,7 @@ def mlp_flops_per_agent_step(obs=80, arch=(256, 256, 128), A=6) -> int:
     return 2 * macs
 
 
-def collector_leg(args, torch, dist, dev, rank, world, N):
+def collector_leg(args, torch, dist, dev, rank, world, N, dtype="f32"):
     """Policy-in-the-loop rollouts (RecurrentPPO.collect_rollouts + GAE) on
     the GPU: BASELINE.json config C4 shape (P3_training rooms, PPO-LSTM,
     seq 128) at N agents per GPU.  One untimed rollout, then timed ones."""
@@ -139,7 +141,7 @@ def collector_leg(args, torch, dist, dev, rank, world, N):
     pol = (RecurrentActorCriticPolicy() if args.collector == "lstm" else ActorCriticPolicy()).to(dev)
     env = BatchedGridEnv(num_agents=N, rooms=rooms, local_map_length=args.L, autoreset=True, device=dev,
                          agent_id_base=rank * N, seed_stride=N * world)
-    col = RolloutCollector(env, pol, n_steps=args.collector_T, sample_seed=42, reset_seed=42)
+    col = RolloutCollector(env, pol, n_steps=args.collector_T, sample_seed=42, reset_seed=42, policy_dtype=dtype)
     col.collect()
     if world > 1:
         dist.barrier()
@@ -161,13 +163,16 @@ def collector_leg(args, torch, dist, dev, rank, world, N):
     tflops = fl * N * steps / el / 1e12
     name = ("PPO-LSTM (MlpLstmPolicy: actor+critic LSTM 256, pi/vf [256,256,128] Tanh)" if args.collector == "lstm"
             else "PPO-MLP (MlpPolicy: pi/vf [256,256,128] Tanh)")
-    return {"value": round(N * world * steps / el, 1), "unit": "env-steps/s", "policy": name, "dtype": "f32",
+    peak = 157.3 if dtype == "f32" else 2500.0     # dense MFMA peak for the GEMM dtype (MI355X_MICROARCH.md)
+    env.close()
+    del col, env
+    return {"value": round(N * world * steps / el, 1), "unit": "env-steps/s", "policy": name, "dtype": dtype,
             "rooms": args.collector_rooms, "agents_per_gpu": N, "rollout_steps": args.collector_T,
             "timed_rollouts": args.collector_rollouts, "ms_per_step": round(el * 1e3 / steps, 4),
             "includes": "policy forward, Categorical draw, env step + auto-reset, truncation bootstrap, "
                         "LSTM-state buffer stores, last values, GAE",
             "policy_flops_per_agent_step": fl, "policy_tflops": round(tflops, 2),
-            "policy_frac_of_f32_peak": round(tflops / 157.3, 4)}
+            "policy_frac_of_mfma_peak": round(tflops / peak, 4), "mfma_peak_tflops": peak}
 
 
 def main():
@@ -245,9 +250,11 @@ def main():
                                "frac": round(sach / HBM_PEAK_GBS, 5), "algorithmic_bytes_per_env_step": sb}}
         senv.close()
         del senv
-    coll = None
+    coll = coll_bf = None
     if args.collector != "none":
         coll = collector_leg(args, torch, dist, dev, rank, world, N)
+        if args.collector_bf16:
+            coll_bf = collector_leg(args, torch, dist, dev, rank, world, N, dtype="bf16")
 
     # sanity: the trajectory buffer holds real observations
     assert torch.isfinite(out.obs).all().item()
@@ -287,6 +294,8 @@ def main():
             rec["drop_in_single_step"] = single   # vn_step-shaped call: one env step per launch
         if simple is not None:
             rec["simple_env"] = simple            # goal-seeking variant
+        if coll_bf is not None:
+            rec["collector_bf16"] = coll_bf
         if coll is not None:
             rec["collector"] = coll               # policy in the loop
         if world == 1 and args.cpu_seconds > 0:

@@ -184,6 +184,13 @@ int vn_lstm_cell(const float *gx, int64_t gx_row_stride, const float *gh, const 
                  float *h, float *c, float *h_store, float *c_store, int32_t n_lstm, int32_t N, int32_t H,
                  void *stream);
 
+/* vn_lstm_cell with bf16 gate pre-activations (uint16_t storage) from bf16
+ * GEMMs; the cell math and the (h, c) state stay f32, and h is also written
+ * in bf16 to h_bf16 [n_lstm][N][H] (the next GEMMs' input), or NULL. */
+int vn_lstm_cell_bf16(const uint16_t *gx, int64_t gx_row_stride, const uint16_t *gh, const float *b_ih,
+                      const float *b_hh, float *h, float *c, uint16_t *h_bf16, float *h_store, float *c_store,
+                      int32_t n_lstm, int32_t N, int32_t H, void *stream);
+
 /*
  * Action and value heads + Categorical draw (ActorCriticPolicy action_net /
  * value_net and distribution.get_actions / log_prob).
@@ -198,6 +205,12 @@ int vn_policy_head(const float *latent_pi, const float *latent_vf, int32_t N, in
                    const float *b_action, int32_t n_actions, const float *w_value, const float *b_value,
                    uint64_t sample_seed, uint64_t t, int64_t agent_id_base, int32_t deterministic, int32_t *actions,
                    float *values, float *log_probs, void *stream);
+
+/* vn_policy_head with bf16 latents (uint16_t storage); math in f32. */
+int vn_policy_head_bf16(const uint16_t *latent_pi, const uint16_t *latent_vf, int32_t N, int32_t P,
+                        const float *w_action, const float *b_action, int32_t n_actions, const float *w_value,
+                        const float *b_value, uint64_t sample_seed, uint64_t t, int64_t agent_id_base,
+                        int32_t deterministic, int32_t *actions, float *values, float *log_probs, void *stream);
 
 /*
  * Ordered indices of the agents whose step was a time-limit truncation
@@ -217,11 +230,11 @@ int vn_collect_bootstrap(const int32_t *boot_idx, const float *terminal_values, 
 
 /*
  * episode_starts[n] = terminated[n] | truncated[n] (f32 0/1, may be NULL)
- * and, for those agents, zero the LSTM state rows h, c [n_lstm][N][H]
- * (n_lstm = 0: no recurrent state).
+ * and, for those agents, zero the LSTM state rows h, c [n_lstm][N][H] and
+ * the bf16 copy h_bf16 (may be NULL) (n_lstm = 0: no recurrent state).
  */
 int vn_episode_start(const uint8_t *terminated, const uint8_t *truncated, int32_t N, float *episode_starts,
-                     float *h, float *c, int32_t n_lstm, int32_t H, void *stream);
+                     float *h, float *c, uint16_t *h_bf16, int32_t n_lstm, int32_t H, void *stream);
 
 #ifdef __cplusplus
 }
