@@ -150,6 +150,147 @@ __global__ __launch_bounds__(256) void lstm_cell_kernel(const T *__restrict__ gx
 }
 
 // ----------------------------------------------------------------------------
+// Fused LSTM step on the matrix cores (bf16 policy path): for each LSTM b,
+//   gates[n][4H] = [x_n | h_n] @ [W_ih | W_hh]^T + (b_ih + b_hh)
+// with v_mfma_f32_32x32x16_bf16 (f32 accumulation), and the cell update as
+// the epilogue, so the 4H gate pre-activations never leave the registers.
+// Block: 4 waves, 64 agents x 64 hidden units x 4 gates; wave w owns rows
+// 32*(w&1).. and units 32*(w>>1).., one 32x32 accumulator per gate, so the
+// four gates of a (row, unit) sit in the same lane and register.  K is
+// streamed in chunks of 32 through double-buffered LDS (rows padded to 40
+// bf16).  x is read as f32 (the env's obs) and rounded to bf16 on the way
+// into LDS; W is pre-packed [B][4H][Kp] with x in columns [0, obs_dim),
+// h in [kx, kx+H) (kx = obs_dim rounded up to 8), zeros elsewhere.
+//   hin / hout  bf16 [B][N][H] (ping-pong: other blocks still read hin)
+//   c           f32 [B][N][H] in/out;  h32, h_store, c_store f32, optional
+// ----------------------------------------------------------------------------
+typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8_t;
+typedef __attribute__((ext_vector_type(16))) float f32x16_t;
+
+constexpr int LF_ROWS = 64, LF_UNITS = 64, LF_KC = 32, LF_LDK = 40;
+
+__device__ __forceinline__ uint4 pack8_bf16(const float f[8]) {
+    return make_uint4(f2bf(f[0]) | (f2bf(f[1]) << 16), f2bf(f[2]) | (f2bf(f[3]) << 16),
+                      f2bf(f[4]) | (f2bf(f[5]) << 16), f2bf(f[6]) | (f2bf(f[7]) << 16));
+}
+
+__global__ __launch_bounds__(256) void lstm_fused_bf16_kernel(
+    const float *__restrict__ x, int obs_dim, int kx, const uint16_t *__restrict__ hin,
+    const uint16_t *__restrict__ w, int Kp, const float *__restrict__ bias, float *__restrict__ c,
+    uint16_t *__restrict__ hout, float *__restrict__ h32, float *__restrict__ h_store, float *__restrict__ c_store,
+    int N, int H) {
+    __shared__ __attribute__((aligned(16))) uint16_t As[2][LF_ROWS * LF_LDK];
+    __shared__ __attribute__((aligned(16))) uint16_t Bs[2][4 * LF_UNITS * LF_LDK];
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const int ublocks = H / LF_UNITS;
+    const int b = blockIdx.y / ublocks;
+    const int u_base = (blockIdx.y - b * ublocks) * LF_UNITS;
+    const int n_base = blockIdx.x * LF_ROWS;
+    const int K = kx + H;
+    const int nchunks = Kp / LF_KC;
+    const uint16_t *wb = w + (size_t)b * 4 * H * Kp;
+    const uint16_t *hb = hin + (size_t)b * N * H;
+    const bool vec_x = (obs_dim & 3) == 0;
+
+    uint4 ra, rb0, rb1, rb2, rb3;
+#define LF_LOAD_CHUNK(ch)                                                                                   \
+    {                                                                                                       \
+        const int k0_ = (ch) * LF_KC;                                                                       \
+        const int row_ = tid >> 2, k_ = k0_ + (tid & 3) * 8;                                                \
+        const int n_ = n_base + row_;                                                                       \
+        ra = make_uint4(0u, 0u, 0u, 0u);                                                                    \
+        if (n_ < N) {                                                                                       \
+            if (k_ < kx) {                                                                                  \
+                const float *px_ = x + (size_t)n_ * obs_dim + k_;                                           \
+                float f0, f1, f2, f3, f4, f5, f6, f7;                                                       \
+                if (vec_x && k_ + 8 <= obs_dim) {                                                           \
+                    const float4 a0 = *reinterpret_cast<const float4 *>(px_);                               \
+                    const float4 a1 = *reinterpret_cast<const float4 *>(px_ + 4);                           \
+                    f0 = a0.x; f1 = a0.y; f2 = a0.z; f3 = a0.w; f4 = a1.x; f5 = a1.y; f6 = a1.z; f7 = a1.w; \
+                } else {                                                                                    \
+                    f0 = k_ + 0 < obs_dim ? px_[0] : 0.0f; f1 = k_ + 1 < obs_dim ? px_[1] : 0.0f;          \
+                    f2 = k_ + 2 < obs_dim ? px_[2] : 0.0f; f3 = k_ + 3 < obs_dim ? px_[3] : 0.0f;          \
+                    f4 = k_ + 4 < obs_dim ? px_[4] : 0.0f; f5 = k_ + 5 < obs_dim ? px_[5] : 0.0f;          \
+                    f6 = k_ + 6 < obs_dim ? px_[6] : 0.0f; f7 = k_ + 7 < obs_dim ? px_[7] : 0.0f;          \
+                }                                                                                           \
+                ra = make_uint4(f2bf(f0) | (f2bf(f1) << 16), f2bf(f2) | (f2bf(f3) << 16),                  \
+                                f2bf(f4) | (f2bf(f5) << 16), f2bf(f6) | (f2bf(f7) << 16));                 \
+            } else if (k_ < K) {                                                                            \
+                ra = *reinterpret_cast<const uint4 *>(hb + (size_t)n_ * H + (k_ - kx));                     \
+            }                                                                                               \
+        }                                                                                                   \
+        rb0 = *reinterpret_cast<const uint4 *>(wb + wrow_off(tid + 0) + k0_ + (tid & 3) * 8);               \
+        rb1 = *reinterpret_cast<const uint4 *>(wb + wrow_off(tid + 256) + k0_ + (tid & 3) * 8);             \
+        rb2 = *reinterpret_cast<const uint4 *>(wb + wrow_off(tid + 512) + k0_ + (tid & 3) * 8);             \
+        rb3 = *reinterpret_cast<const uint4 *>(wb + wrow_off(tid + 768) + k0_ + (tid & 3) * 8);             \
+    }
+#define LF_STORE_CHUNK(buf)                                                                                  \
+    {                                                                                                       \
+        *reinterpret_cast<uint4 *>(&As[buf][(tid >> 2) * LF_LDK + (tid & 3) * 8]) = ra;                      \
+        *reinterpret_cast<uint4 *>(&Bs[buf][((tid + 0) >> 2) * LF_LDK + (tid & 3) * 8]) = rb0;               \
+        *reinterpret_cast<uint4 *>(&Bs[buf][((tid + 256) >> 2) * LF_LDK + (tid & 3) * 8]) = rb1;             \
+        *reinterpret_cast<uint4 *>(&Bs[buf][((tid + 512) >> 2) * LF_LDK + (tid & 3) * 8]) = rb2;             \
+        *reinterpret_cast<uint4 *>(&Bs[buf][((tid + 768) >> 2) * LF_LDK + (tid & 3) * 8]) = rb3;             \
+    }
+    // W row (element offset) of the local B row (gi >> 2): gate = row / 64, unit = row % 64
+    auto wrow_off = [&](int gi) -> size_t {
+        const int lrow = gi >> 2, gate = lrow / LF_UNITS, uu = lrow - gate * LF_UNITS;
+        return (size_t)(gate * H + u_base + uu) * Kp;
+    };
+
+    f32x16_t acc[4];
+#pragma unroll
+    for (int g = 0; g < 4; ++g)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[g][r] = 0.0f;
+    const int wr = (wv & 1) * 32, wu = (wv >> 1) * 32;
+    LF_LOAD_CHUNK(0)
+    LF_STORE_CHUNK(0)
+    __syncthreads();
+    for (int ch = 0; ch < nchunks; ++ch) {
+        const int cur = ch & 1;
+        if (ch + 1 < nchunks) LF_LOAD_CHUNK(ch + 1)
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) {
+            const int kk = ks * 16 + 8 * (lane >> 5);
+            const bf16x8_t a = *reinterpret_cast<const bf16x8_t *>(&As[cur][(wr + (lane & 31)) * LF_LDK + kk]);
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+                const bf16x8_t bv =
+                    *reinterpret_cast<const bf16x8_t *>(&Bs[cur][(g * LF_UNITS + wu + (lane & 31)) * LF_LDK + kk]);
+                acc[g] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, bv, acc[g], 0, 0, 0);
+            }
+        }
+        if (ch + 1 < nchunks) LF_STORE_CHUNK(cur ^ 1)
+        __syncthreads();
+    }
+#undef LF_LOAD_CHUNK
+#undef LF_STORE_CHUNK
+
+    // epilogue: lane holds unit u for 16 rows; gate g of (row, u) in acc[g][reg]
+    const int u = u_base + wu + (lane & 31);
+    const float *bb = bias + (size_t)b * 4 * H;
+    const float bi = bb[u], bf = bb[H + u], bg = bb[2 * H + u], bo = bb[3 * H + u];
+#pragma unroll
+    for (int reg = 0; reg < 16; ++reg) {
+        const int n = n_base + wr + (reg & 3) + 8 * (reg >> 2) + 4 * (lane >> 5);
+        if (n < N) {
+            const size_t so = ((size_t)b * N + n) * H + u;
+            const float ig = sigm(acc[0][reg] + bi), fg = sigm(acc[1][reg] + bf);
+            const float gg = tanhf(acc[2][reg] + bg), og = sigm(acc[3][reg] + bo);
+            const float fc = fg * c[so], ig2 = ig * gg;
+            const float cn = fc + ig2;
+            const float hn = og * tanhf(cn);
+            c[so] = cn;
+            hout[so] = (uint16_t)f2bf(hn);
+            if (h32) h32[so] = hn;
+            if (h_store) h_store[so] = hn;
+            if (c_store) c_store[so] = cn;
+        }
+    }
+}
+
+// ----------------------------------------------------------------------------
 // Action + value heads and the Categorical draw.  16 lanes per agent (16
 // agents per 256-thread block): lane l reads float4s l, l+16, ... of the
 // agent's latent rows (coalesced 256-B segments), dot products against the
@@ -442,6 +583,23 @@ int vn_lstm_cell_bf16(const uint16_t *gx, int64_t gx_row_stride, const uint16_t 
     return lstm_cell_launch<uint16_t>(gx, gx_row_stride, gh, b_ih, b_hh, h, c, h_bf16, h_store, c_store, n_lstm, N,
                                       H, stream);
 }
+
+int vn_lstm_fused_bf16(const float *x, int32_t obs_dim, const uint16_t *h_in, const uint16_t *w_cat, int32_t Kp,
+                       const float *bias, float *c, uint16_t *h_out, float *h32, float *h_store, float *c_store,
+                       int32_t n_lstm, int32_t N, int32_t H, void *stream) {
+    if (!x || !h_in || !w_cat || !bias || !c || !h_out) return fail(VN_ERR_INVALID, "NULL argument");
+    if (h_in == h_out) return fail(VN_ERR_INVALID, "h_in and h_out must differ (other blocks read h_in)");
+    const int kx = (obs_dim + 7) & ~7;
+    if (n_lstm < 1 || N < 1 || obs_dim < 1 || H < 64 || (H % LF_UNITS) || (Kp % LF_KC) || Kp < kx + H)
+        return fail(VN_ERR_INVALID, "bad sizes n_lstm=%d N=%d obs_dim=%d H=%d Kp=%d (H %% 64, Kp %% 32, Kp >= %d)",
+                    n_lstm, N, obs_dim, H, Kp, kx + H);
+    const dim3 grid((unsigned)((N + LF_ROWS - 1) / LF_ROWS), (unsigned)(n_lstm * (H / LF_UNITS)));
+    hipLaunchKernelGGL(lstm_fused_bf16_kernel, grid, dim3(256), 0, (hipStream_t)stream, x, (int)obs_dim, kx, h_in,
+                       w_cat, (int)Kp, bias, c, h_out, h32, h_store, c_store, (int)N, (int)H);
+    VN_HIP(hipGetLastError());
+    return VN_OK;
+}
+
 
 int vn_policy_head(const float *latent_pi, const float *latent_vf, int32_t N, int32_t P, const float *w_action,
                    const float *b_action, int32_t n_actions, const float *w_value, const float *b_value,

@@ -72,6 +72,8 @@ _SIGS = {
     "vn_lstm_cell_bf16": (C.c_int, [P, C.c_int64, P, P, P, P, P, P, P, P, C.c_int32, C.c_int32, C.c_int32, P]),
     "vn_policy_head_bf16": (C.c_int, [P, P, C.c_int32, C.c_int32, P, P, C.c_int32, P, P, C.c_uint64, C.c_uint64,
                                       C.c_int64, C.c_int32, P, P, P, P]),
+    "vn_lstm_fused_bf16": (C.c_int, [P, C.c_int32, P, P, C.c_int32, P, P, P, P, P, P, C.c_int32, C.c_int32,
+                                     C.c_int32, P]),
     "vn_collect_compact": (C.c_int, [P, P, C.c_int32, P, P, P]),
     "vn_collect_bootstrap": (C.c_int, [P, P, C.c_int32, C.c_double, P, P]),
     "vn_episode_start": (C.c_int, [P, P, C.c_int32, P, P, P, P, C.c_int32, C.c_int32, P]),

@@ -96,6 +96,19 @@ class _Weights:
             self.w_ih_vf = g(lc.weight_ih_l0)
             self.b_ih = torch.stack([f(la.bias_ih_l0), f(lc.bias_ih_l0)])               # [2, 4H]
             self.b_hh = torch.stack([f(la.bias_hh_l0), f(lc.bias_hh_l0)])
+            # fused MFMA LSTM step (bf16 path, H % 64 == 0): [W_ih | W_hh] packed
+            # K-contiguous, x part padded to a multiple of 8, K to a multiple of 32
+            self.fused = dtype == torch.bfloat16 and self.H % 64 == 0
+            if self.fused:
+                od = la.weight_ih_l0.shape[1]
+                self.kx = (od + 7) // 8 * 8
+                self.Kp = (self.kx + self.H + 31) // 32 * 32
+                wc = torch.zeros((2, 4 * self.H, self.Kp), dtype=torch.float32, device=device)
+                for b, m in enumerate((la, lc)):
+                    wc[b, :, :od] = f(m.weight_ih_l0)
+                    wc[b, :, self.kx:self.kx + self.H] = f(m.weight_hh_l0)
+                self.w_cat = wc.to(torch.bfloat16).contiguous()
+                self.bias = (self.b_ih + self.b_hh).contiguous()
         ext = policy.mlp_extractor
         self.pi = [(g(m.weight), g(m.bias)) for m in ext.linears("pi")]
         self.vf = [(g(m.weight), g(m.bias)) for m in ext.linears("vf")]
@@ -168,6 +181,8 @@ class RolloutCollector:
             self._gx = z(N, 2 * 4 * H, dt=self.cdt)
             self._gh = z(2, N, 4 * H, dt=self.cdt)
             self.h_bf = z(2, N, H, dt=torch.bfloat16) if self.bf16 else None   # GEMM copy of h
+            self.fused = self.bf16 and self.w.fused
+            self.h_bf2 = z(2, N, H, dt=torch.bfloat16) if self.fused else None  # fused step's output (ping-pong)
             self.store = bool(store_lstm_states)
             self._hs = z(T + 1, 2, N, H) if self.store else None
             self._cs = z(T + 1, 2, N, H) if self.store else None
@@ -201,9 +216,30 @@ class RolloutCollector:
                          self.env.agent_id_base if pi else 0, int(self.deterministic) if pi else 0, _p(actions),
                          _p(values), _p(log_probs), self._stream()), "vn_policy_head")
 
+    def _fused(self, obs, h_in, c, h_out, hs, cs, nl, M, b0):
+        w = self.w
+        _native.check(self.lib.vn_lstm_fused_bf16(_p(obs), obs.shape[1], _p(h_in), _p(w.w_cat[b0:b0 + nl]), w.Kp,
+                                                  _p(w.bias[b0:b0 + nl]), _p(c), _p(h_out), None, _p(hs), _p(cs), nl,
+                                                  M, w.H, self._stream()), "vn_lstm_fused_bf16")
+
+    def hidden_state(self):
+        """(h, c) f32 [2, N, H] of the (actor, critic) LSTMs after the last step
+        (h from its bf16 copy on the fused bf16 path)."""
+        h = self.h_bf.float() if self.fused else self.h
+        return h, self.c
+
     def _forward(self, obs: torch.Tensor, t: int):
         """Policy step on obs [N, 80] into actions/values/log_probs[t]."""
         w, N = self.w, self.N
+        if self.recurrent and self.fused:
+            hs = self._hs[t + 1] if self.store else None
+            cs = self._cs[t + 1] if self.store else None
+            self._fused(obs, self.h_bf, self.c, self.h_bf2, hs, cs, 2, N, 0)
+            self.h_bf, self.h_bf2 = self.h_bf2, self.h_bf
+            lat_pi = _mlp(w.pi, self.h_bf[0])
+            lat_vf = _mlp(w.vf, self.h_bf[1])
+            self._head(lat_pi, lat_vf, N, self.t_global, self.actions[t], self.values[t], self.log_probs[t])
+            return
         x = obs if not self.bf16 else obs.to(self.cdt)
         if self.recurrent:
             H = w.H
@@ -222,8 +258,14 @@ class RolloutCollector:
         self._head(lat_pi, lat_vf, N, self.t_global, self.actions[t], self.values[t], self.log_probs[t])
 
     def _critic(self, obs: torch.Tensor, h: Optional[torch.Tensor], c: Optional[torch.Tensor], out: torch.Tensor):
-        """predict_values: one critic step from state (h, c) [M, H] (consumed), value -> out [M]."""
+        """predict_values: one critic step from state (h, c) [M, H] (consumed), value -> out [M].
+        On the fused bf16 path h is the bf16 copy."""
         w, M = self.w, obs.shape[0]
+        if self.recurrent and self.fused:
+            h_out = torch.empty((M, w.H), dtype=torch.bfloat16, device=self.device)
+            self._fused(obs.contiguous(), h.contiguous(), c, h_out, None, None, 1, M, 1)
+            self._head(None, _mlp(w.vf, h_out), M, 0, None, out, None)
+            return
         x = obs if not self.bf16 else obs.to(self.cdt)
         if self.recurrent:
             H = w.H
@@ -257,7 +299,8 @@ class RolloutCollector:
                 idx = self._boot_idx[:M].long()
                 tv = torch.empty(M, dtype=torch.float32, device=self.device)
                 if self.recurrent:
-                    self._critic(self._tobs.index_select(0, idx), self.h[1].index_select(0, idx),
+                    hsrc = self.h_bf if self.fused else self.h
+                    self._critic(self._tobs.index_select(0, idx), hsrc[1].index_select(0, idx),
                                  self.c[1].index_select(0, idx), tv)
                 else:
                     self._critic(self._tobs.index_select(0, idx), None, None, tv)
@@ -272,7 +315,8 @@ class RolloutCollector:
             self.t_global += 1
         # V(last obs) under the current (masked) critic state
         if self.recurrent:
-            self._critic(self._obs[T], self.h[1].clone(), self.c[1].clone(), self._last_values)
+            hsrc = self.h_bf if self.fused else self.h
+            self._critic(self._obs[T], hsrc[1].clone(), self.c[1].clone(), self._last_values)
         else:
             self._critic(self._obs[T], None, None, self._last_values)
         adv = torch.empty((T, N), dtype=torch.float32, device=self.device)

@@ -192,6 +192,23 @@ int vn_lstm_cell_bf16(const uint16_t *gx, int64_t gx_row_stride, const uint16_t 
                       int32_t n_lstm, int32_t N, int32_t H, void *stream);
 
 /*
+ * The whole LSTM step of the bf16 policy path on the matrix cores: gate
+ * GEMM [x | h] @ [W_ih | W_hh]^T (v_mfma_f32_32x32x16_bf16, f32 accumulate)
+ * with the cell update as its epilogue.
+ *   x        f32 [N][obs_dim] (the env's obs; rounded to bf16 in-kernel)
+ *   h_in     bf16 [n_lstm][N][H] previous h (masked); h_out bf16, != h_in
+ *   w_cat    bf16 [n_lstm][4H][Kp]: W_ih in columns [0, obs_dim), W_hh in
+ *            [kx, kx+H), kx = obs_dim rounded up to 8, zeros elsewhere;
+ *            Kp a multiple of 32 >= kx + H
+ *   bias     f32 [n_lstm][4H] = b_ih + b_hh
+ *   c        f32 [n_lstm][N][H] in/out; h32 / h_store / c_store f32 or NULL
+ * H must be a multiple of 64.
+ */
+int vn_lstm_fused_bf16(const float *x, int32_t obs_dim, const uint16_t *h_in, const uint16_t *w_cat, int32_t Kp,
+                       const float *bias, float *c, uint16_t *h_out, float *h32, float *h_store, float *c_store,
+                       int32_t n_lstm, int32_t N, int32_t H, void *stream);
+
+/*
  * Action and value heads + Categorical draw (ActorCriticPolicy action_net /
  * value_net and distribution.get_actions / log_prob).
  *   latent_pi [N][P] (NULL: value only), latent_vf [N][P] (NULL: no value)

@@ -127,8 +127,9 @@ def test_collector_matches_oracle(voxnav, kind, T, rollouts, dtype):
         _close(buf.advantages.cpu(), a64, *tol["adv"], "advantages")
         _close(buf.returns.cpu(), r64, *tol["adv"], "returns")
         if kind == "lstm":
-            _close(col.h.cpu(), h, *tol["v"], "h")
-            _close(col.c.cpu(), c, *tol["v"], "c")
+            gh, gc = col.hidden_state()
+            _close(gh.cpu(), h, *tol["v"], "h")
+            _close(gc.cpu(), c, *tol["v"], "c")
             # stored states entering step t: zero at learn() start
             if r == 0:
                 assert float(buf.lstm_h[0].abs().max()) == 0.0
@@ -198,3 +199,51 @@ def test_compaction_and_episode_start(voxnav):
         want_r[want] = (want_r[want] + gv).astype(np.float32)
         assert lib.vn_collect_bootstrap(p(idx), p(tv), M, C.c_double(0.99), p(rew), None) == 0
         assert rew.cpu().numpy().tobytes() == want_r.tobytes()
+
+
+def test_fused_mfma_lstm_exact_mapping(voxnav):
+    """vn_lstm_fused_bf16 against a float64 restatement on data that bf16
+    holds exactly (multiples of 1/8), so the gate sums are exact in f32 and
+    any row/column/gate mix-up in the MFMA operand or accumulator maps shows."""
+    import ctypes as C
+    lib = voxnav.load_library()
+    rng = np.random.default_rng(21)
+    B, N, H, od = 2, 200, 128, 80          # N not a multiple of 64: tail rows
+    kx = (od + 7) // 8 * 8
+    Kp = (kx + H + 31) // 32 * 32
+    x = (rng.integers(-4, 5, size=(N, od)) / 8.0).astype(np.float32)
+    h_in = (rng.integers(-4, 5, size=(B, N, H)) / 8.0).astype(np.float32)
+    W = (rng.integers(-3, 4, size=(B, 4 * H, od + H)) / 8.0).astype(np.float32)
+    bias = (rng.integers(-8, 9, size=(B, 4 * H)) / 8.0).astype(np.float32)
+    c0 = rng.standard_normal((B, N, H)).astype(np.float32)
+    wc = np.zeros((B, 4 * H, Kp), np.float32)
+    wc[:, :, :od] = W[:, :, :od]
+    wc[:, :, kx:kx + H] = W[:, :, od:]
+    dev = "cuda:0"
+    t = lambda a, dt=torch.float32: torch.as_tensor(a, dtype=dt, device=dev).contiguous()  # noqa: E731
+    tx, th, tw, tb, tc = t(x), t(h_in, torch.bfloat16), t(wc, torch.bfloat16), t(bias), t(c0)
+    hout = torch.zeros((B, N, H), dtype=torch.bfloat16, device=dev)
+    hst = torch.zeros((B, N, H), device=dev)
+    cst = torch.zeros((B, N, H), device=dev)
+    p = lambda a: C.c_void_p(a.data_ptr())  # noqa: E731
+    assert lib.vn_lstm_fused_bf16(p(tx), od, p(th), p(tw), Kp, p(tb), p(tc), p(hout), None, p(hst), p(cst), B, N, H,
+                                  None) == 0
+    torch.cuda.synchronize()
+    xh = np.concatenate([np.broadcast_to(x, (B, N, od)), h_in], -1).astype(np.float64)
+    pre = np.einsum("bnk,bgk->bng", xh, W.astype(np.float64)) + bias[:, None, :]
+    sg = lambda v: 1.0 / (1.0 + np.exp(-v))  # noqa: E731
+    i, f, g, o = (pre[..., k * H:(k + 1) * H] for k in range(4))
+    c1 = sg(f) * c0 + sg(i) * np.tanh(g)
+    h1 = sg(o) * np.tanh(c1)
+    np.testing.assert_allclose(tc.cpu().numpy(), c1, atol=2e-6, rtol=2e-6)
+    np.testing.assert_allclose(hst.cpu().numpy(), h1, atol=2e-6, rtol=2e-6)
+    np.testing.assert_array_equal(cst.cpu().numpy(), tc.cpu().numpy())
+    np.testing.assert_allclose(hout.float().cpu().numpy(), h1, atol=4e-3, rtol=4e-3)   # bf16 rounding of h
+    # the same sizes through the unfused bf16 path (library GEMMs + vn_lstm_cell_bf16) agree
+    gx = (t(x, torch.bfloat16) @ t(W[:, :, :od].reshape(B * 4 * H, od), torch.bfloat16).t())
+    gh = torch.stack([th[b] @ t(W[b, :, od:], torch.bfloat16).t() for b in range(B)])
+    h2 = torch.zeros((B, N, H), device=dev)
+    c2 = t(c0)
+    assert lib.vn_lstm_cell_bf16(p(gx), 8 * H, p(gh), p(tb), p(torch.zeros_like(tb)), p(h2), p(c2), None, None, None,
+                                 B, N, H, None) == 0
+    np.testing.assert_allclose(c2.cpu().numpy(), c1, atol=3e-2, rtol=3e-2)
