@@ -157,8 +157,8 @@ __global__ __launch_bounds__(256) void lstm_cell_kernel(const T *__restrict__ gx
 // Block: 4 waves, 64 agents x 64 hidden units x 4 gates; wave w owns rows
 // 32*(w&1).. and units 32*(w>>1).., one 32x32 accumulator per gate, so the
 // four gates of a (row, unit) sit in the same lane and register.  K is
-// streamed in chunks of 32 through double-buffered LDS (rows padded to 40
-// bf16).  x is read as f32 (the env's obs) and rounded to bf16 on the way
+// streamed in chunks of 64 through LDS (rows padded to 72 bf16), the next
+// chunk prefetched into registers during the current chunk's MFMAs.  x is read as f32 (the env's obs) and rounded to bf16 on the way
 // into LDS; W is pre-packed [B][4H][Kp] with x in columns [0, obs_dim),
 // h in [kx, kx+H) (kx = obs_dim rounded up to 8), zeros elsewhere.
 //   hin / hout  bf16 [B][N][H] (ping-pong: other blocks still read hin)
@@ -167,76 +167,132 @@ __global__ __launch_bounds__(256) void lstm_cell_kernel(const T *__restrict__ gx
 typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8_t;
 typedef __attribute__((ext_vector_type(16))) float f32x16_t;
 
-constexpr int LF_ROWS = 64, LF_UNITS = 64, LF_KC = 32, LF_LDK = 40;
+constexpr int LF_ROWS = 64, LF_UNITS = 64;
+#ifndef VN_LF_KC
+#define VN_LF_KC 64
+#endif
+constexpr int LF_KC = VN_LF_KC;           // K per chunk (bf16 elements)
+constexpr int LF_LDK = LF_KC + 8;         // LDS row pitch (+16 B against bank conflicts)
+constexpr int LF_GPR = LF_KC / 8;         // 16-byte groups per row and chunk
+constexpr int LF_NA = LF_ROWS * LF_GPR / 256, LF_NB = 4 * LF_UNITS * LF_GPR / 256;   // groups per thread
 
-__device__ __forceinline__ uint4 pack8_bf16(const float f[8]) {
-    return make_uint4(f2bf(f[0]) | (f2bf(f[1]) << 16), f2bf(f[2]) | (f2bf(f[3]) << 16),
-                      f2bf(f[4]) | (f2bf(f[5]) << 16), f2bf(f[6]) | (f2bf(f[7]) << 16));
-}
+// gate nonlinearities of the bf16 path on the hardware exp / rcp (~1e-6
+// relative; the operands are bf16 already): 5 per (row, unit), 80 per lane
+__device__ __forceinline__ float fast_sigm(float x) { return __frcp_rn(1.0f + __expf(-x)); }
+__device__ __forceinline__ float fast_tanh(float x) { return 2.0f * fast_sigm(2.0f * x) - 1.0f; }
 
-__global__ __launch_bounds__(256) void lstm_fused_bf16_kernel(
+#ifndef VN_LF_MIN_WAVES
+#define VN_LF_MIN_WAVES 3   // 3 blocks of 4 waves per CU
+#endif
+template <bool VEC_X>   // obs_dim % 8 == 0: branch-free staging loads
+__global__ __launch_bounds__(256, VN_LF_MIN_WAVES) void lstm_fused_bf16_kernel(
     const float *__restrict__ x, int obs_dim, int kx, const uint16_t *__restrict__ hin,
     const uint16_t *__restrict__ w, int Kp, const float *__restrict__ bias, float *__restrict__ c,
     uint16_t *__restrict__ hout, float *__restrict__ h32, float *__restrict__ h_store, float *__restrict__ c_store,
-    int N, int H) {
-    __shared__ __attribute__((aligned(16))) uint16_t As[2][LF_ROWS * LF_LDK];
-    __shared__ __attribute__((aligned(16))) uint16_t Bs[2][4 * LF_UNITS * LF_LDK];
+    int N, int H, int ncombo) {
+    // one LDS buffer; the next chunk is prefetched into registers during
+    // the current chunk's MFMAs
+    __shared__ __attribute__((aligned(16))) uint16_t lds[(LF_ROWS + 4 * LF_UNITS) * LF_LDK];
+    uint16_t *As = lds, *Bs = lds + LF_ROWS * LF_LDK;
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    // 1-D grid over (row tile, combo = LSTM x unit block).  Blocks are dealt
+    // to the 8 XCDs round-robin by id; when the tile count allows, the combos
+    // of one row tile get ids of the same residue mod 8 (same XCD, close in
+    // time), so the tile's x / h rows are fetched into that XCD's L2 once.
     const int ublocks = H / LF_UNITS;
-    const int b = blockIdx.y / ublocks;
-    const int u_base = (blockIdx.y - b * ublocks) * LF_UNITS;
-    const int n_base = blockIdx.x * LF_ROWS;
+    const int ntiles = (N + LF_ROWS - 1) / LF_ROWS;
+    const int id = (int)blockIdx.x;
+    int tile, combo;
+    if ((ntiles & 7) == 0) {
+        const int xcd = id & 7, local = id >> 3;
+        tile = xcd + 8 * (local / ncombo);
+        combo = local - (local / ncombo) * ncombo;
+    } else {
+        tile = id / ncombo;
+        combo = id - tile * ncombo;
+    }
+    const int b = combo / ublocks;
+    const int u_base = (combo - b * ublocks) * LF_UNITS;
+    const int n_base = tile * LF_ROWS;
     const int K = kx + H;
     const int nchunks = Kp / LF_KC;
     const uint16_t *wb = w + (size_t)b * 4 * H * Kp;
     const uint16_t *hb = hin + (size_t)b * N * H;
-    const bool vec_x = (obs_dim & 3) == 0;
 
-    uint4 ra, rb0, rb1, rb2, rb3;
-#define LF_LOAD_CHUNK(ch)                                                                                   \
-    {                                                                                                       \
-        const int k0_ = (ch) * LF_KC;                                                                       \
-        const int row_ = tid >> 2, k_ = k0_ + (tid & 3) * 8;                                                \
-        const int n_ = n_base + row_;                                                                       \
-        ra = make_uint4(0u, 0u, 0u, 0u);                                                                    \
+    static_assert(LF_NA == 2 && LF_NB == 8, "staging registers are spelled out for LF_KC = 64");
+    // raw staging registers: an A group is 8 obs floats (x columns) or 8 bf16
+    // of h (in lo); it is converted when written to LDS, so no wait sits
+    // between issuing the next chunk's loads and this chunk's MFMAs
+    float4 ra0lo, ra0hi, ra1lo, ra1hi;
+    uint4 rb0, rb1, rb2, rb3, rb4, rb5, rb6, rb7;
+#define LF_A_LOAD(lo, hi, i)                                                                                \
+    if (VEC_X) {                                                                                            \
+        /* unconditional loads from a clamped address, zeroed when written to LDS: */                       \
+        /* a loaded value merged across branches would force a wait right here     */                       \
+        const int gi_ = tid + 256 * (i), k_ = k0_ + (gi_ % LF_GPR) * 8;                                    \
+        const int n_ = min(n_base + gi_ / LF_GPR, N - 1);                                                   \
+        const bool isx_ = k_ < kx;                                                                          \
+        const float *p_ = isx_ ? x + (size_t)n_ * obs_dim + k_                                              \
+                               : reinterpret_cast<const float *>(hb + (size_t)n_ * H + min(k_ - kx, H - 8)); \
+        lo = *reinterpret_cast<const float4 *>(p_);                                                         \
+        hi = *reinterpret_cast<const float4 *>(p_ + (isx_ ? 4 : 0));                                        \
+    } else {                                                                                                \
+        const int gi_ = tid + 256 * (i), k_ = k0_ + (gi_ % LF_GPR) * 8;                                    \
+        const int n_ = n_base + gi_ / LF_GPR;                                                               \
+        lo = make_float4(0.f, 0.f, 0.f, 0.f);                                                               \
+        hi = lo;                                                                                            \
         if (n_ < N) {                                                                                       \
             if (k_ < kx) {                                                                                  \
                 const float *px_ = x + (size_t)n_ * obs_dim + k_;                                           \
-                float f0, f1, f2, f3, f4, f5, f6, f7;                                                       \
-                if (vec_x && k_ + 8 <= obs_dim) {                                                           \
-                    const float4 a0 = *reinterpret_cast<const float4 *>(px_);                               \
-                    const float4 a1 = *reinterpret_cast<const float4 *>(px_ + 4);                           \
-                    f0 = a0.x; f1 = a0.y; f2 = a0.z; f3 = a0.w; f4 = a1.x; f5 = a1.y; f6 = a1.z; f7 = a1.w; \
-                } else {                                                                                    \
-                    f0 = k_ + 0 < obs_dim ? px_[0] : 0.0f; f1 = k_ + 1 < obs_dim ? px_[1] : 0.0f;          \
-                    f2 = k_ + 2 < obs_dim ? px_[2] : 0.0f; f3 = k_ + 3 < obs_dim ? px_[3] : 0.0f;          \
-                    f4 = k_ + 4 < obs_dim ? px_[4] : 0.0f; f5 = k_ + 5 < obs_dim ? px_[5] : 0.0f;          \
-                    f6 = k_ + 6 < obs_dim ? px_[6] : 0.0f; f7 = k_ + 7 < obs_dim ? px_[7] : 0.0f;          \
-                }                                                                                           \
-                ra = make_uint4(f2bf(f0) | (f2bf(f1) << 16), f2bf(f2) | (f2bf(f3) << 16),                  \
-                                f2bf(f4) | (f2bf(f5) << 16), f2bf(f6) | (f2bf(f7) << 16));                 \
+                lo.x = k_ + 0 < obs_dim ? px_[0] : 0.0f; lo.y = k_ + 1 < obs_dim ? px_[1] : 0.0f;          \
+                lo.z = k_ + 2 < obs_dim ? px_[2] : 0.0f; lo.w = k_ + 3 < obs_dim ? px_[3] : 0.0f;          \
+                hi.x = k_ + 4 < obs_dim ? px_[4] : 0.0f; hi.y = k_ + 5 < obs_dim ? px_[5] : 0.0f;          \
+                hi.z = k_ + 6 < obs_dim ? px_[6] : 0.0f; hi.w = k_ + 7 < obs_dim ? px_[7] : 0.0f;          \
             } else if (k_ < K) {                                                                            \
-                ra = *reinterpret_cast<const uint4 *>(hb + (size_t)n_ * H + (k_ - kx));                     \
+                lo = *reinterpret_cast<const float4 *>(hb + (size_t)n_ * H + (k_ - kx));                    \
             }                                                                                               \
         }                                                                                                   \
-        rb0 = *reinterpret_cast<const uint4 *>(wb + wrow_off(tid + 0) + k0_ + (tid & 3) * 8);               \
-        rb1 = *reinterpret_cast<const uint4 *>(wb + wrow_off(tid + 256) + k0_ + (tid & 3) * 8);             \
-        rb2 = *reinterpret_cast<const uint4 *>(wb + wrow_off(tid + 512) + k0_ + (tid & 3) * 8);             \
-        rb3 = *reinterpret_cast<const uint4 *>(wb + wrow_off(tid + 768) + k0_ + (tid & 3) * 8);             \
     }
-#define LF_STORE_CHUNK(buf)                                                                                  \
+#define LF_B(dst, i)                                                                                        \
     {                                                                                                       \
-        *reinterpret_cast<uint4 *>(&As[buf][(tid >> 2) * LF_LDK + (tid & 3) * 8]) = ra;                      \
-        *reinterpret_cast<uint4 *>(&Bs[buf][((tid + 0) >> 2) * LF_LDK + (tid & 3) * 8]) = rb0;               \
-        *reinterpret_cast<uint4 *>(&Bs[buf][((tid + 256) >> 2) * LF_LDK + (tid & 3) * 8]) = rb1;             \
-        *reinterpret_cast<uint4 *>(&Bs[buf][((tid + 512) >> 2) * LF_LDK + (tid & 3) * 8]) = rb2;             \
-        *reinterpret_cast<uint4 *>(&Bs[buf][((tid + 768) >> 2) * LF_LDK + (tid & 3) * 8]) = rb3;             \
+        const int gi_ = tid + 256 * (i), lrow_ = gi_ / LF_GPR, gate_ = lrow_ / LF_UNITS;                   \
+        const int uu_ = lrow_ - gate_ * LF_UNITS;                                                           \
+        dst = *reinterpret_cast<const uint4 *>(wb + (size_t)(gate_ * H + u_base + uu_) * Kp + k0_ +         \
+                                               (gi_ % LF_GPR) * 8);                                         \
     }
-    // W row (element offset) of the local B row (gi >> 2): gate = row / 64, unit = row % 64
-    auto wrow_off = [&](int gi) -> size_t {
-        const int lrow = gi >> 2, gate = lrow / LF_UNITS, uu = lrow - gate * LF_UNITS;
-        return (size_t)(gate * H + u_base + uu) * Kp;
-    };
+#define LF_LOAD_CHUNK(ch)                                                                                   \
+    {                                                                                                       \
+        const int k0_ = (ch) * LF_KC;                                                                       \
+        LF_B(rb0, 0) LF_B(rb1, 1) LF_B(rb2, 2) LF_B(rb3, 3) LF_B(rb4, 4) LF_B(rb5, 5) LF_B(rb6, 6) LF_B(rb7, 7) \
+        LF_A_LOAD(ra0lo, ra0hi, 0) LF_A_LOAD(ra1lo, ra1hi, 1)                                               \
+    }
+#define LF_A_PUT(lo, hi, i)                                                                                 \
+    {                                                                                                       \
+        const int gi_ = tid + 256 * (i), k_ = k0_ + (gi_ % LF_GPR) * 8;                                    \
+        uint4 v_;                                                                                           \
+        if (VEC_X && (n_base + gi_ / LF_GPR >= N || k_ >= K)) {                                             \
+            v_ = make_uint4(0u, 0u, 0u, 0u);                                                                \
+        } else if (k_ < kx) {                                                                               \
+            v_ = make_uint4(f2bf(lo.x) | (f2bf(lo.y) << 16), f2bf(lo.z) | (f2bf(lo.w) << 16),              \
+                            f2bf(hi.x) | (f2bf(hi.y) << 16), f2bf(hi.z) | (f2bf(hi.w) << 16));             \
+        } else {                                                                                            \
+            v_ = make_uint4(__float_as_uint(lo.x), __float_as_uint(lo.y), __float_as_uint(lo.z),            \
+                            __float_as_uint(lo.w));                                                         \
+        }                                                                                                   \
+        *reinterpret_cast<uint4 *>(&As[(gi_ / LF_GPR) * LF_LDK + (gi_ % LF_GPR) * 8]) = v_;                 \
+    }
+#define LF_PUT(base, src, i)                                                                                \
+    {                                                                                                       \
+        const int gi_ = tid + 256 * (i);                                                                    \
+        *reinterpret_cast<uint4 *>(&base[(gi_ / LF_GPR) * LF_LDK + (gi_ % LF_GPR) * 8]) = src;              \
+    }
+#define LF_STORE_CHUNK(ch)                                                                                   \
+    {                                                                                                       \
+        const int k0_ = (ch) * LF_KC;                                                                       \
+        LF_A_PUT(ra0lo, ra0hi, 0) LF_A_PUT(ra1lo, ra1hi, 1)                                                 \
+        LF_PUT(Bs, rb0, 0) LF_PUT(Bs, rb1, 1) LF_PUT(Bs, rb2, 2) LF_PUT(Bs, rb3, 3)                         \
+        LF_PUT(Bs, rb4, 4) LF_PUT(Bs, rb5, 5) LF_PUT(Bs, rb6, 6) LF_PUT(Bs, rb7, 7)                         \
+    }
 
     f32x16_t acc[4];
 #pragma unroll
@@ -244,28 +300,37 @@ __global__ __launch_bounds__(256) void lstm_fused_bf16_kernel(
 #pragma unroll
         for (int r = 0; r < 16; ++r) acc[g][r] = 0.0f;
     const int wr = (wv & 1) * 32, wu = (wv >> 1) * 32;
+#ifndef VN_LF_DIAG
+#define VN_LF_DIAG 0   // timing diagnostics: 1 skips the K loop, 2 a cheap epilogue (results invalid)
+#endif
     LF_LOAD_CHUNK(0)
-    LF_STORE_CHUNK(0)
-    __syncthreads();
-    for (int ch = 0; ch < nchunks; ++ch) {
-        const int cur = ch & 1;
-        if (ch + 1 < nchunks) LF_LOAD_CHUNK(ch + 1)
+    for (int ch = 0; ch < (VN_LF_DIAG == 1 ? 0 : nchunks); ++ch) {
+        LF_STORE_CHUNK(ch)
+        __syncthreads();
+        // next chunk, in flight during this chunk's MFMAs (the last iteration
+        // reloads its own chunk: unconditional, so the staging stays in
+        // registers); the scheduling barrier keeps the loads ahead of the MFMAs
+        LF_LOAD_CHUNK(ch + 1 < nchunks ? ch + 1 : ch)
+        __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-        for (int ks = 0; ks < 2; ++ks) {
+        for (int ks = 0; ks < LF_KC / 16; ++ks) {
             const int kk = ks * 16 + 8 * (lane >> 5);
-            const bf16x8_t a = *reinterpret_cast<const bf16x8_t *>(&As[cur][(wr + (lane & 31)) * LF_LDK + kk]);
+            const bf16x8_t a = *reinterpret_cast<const bf16x8_t *>(&As[(wr + (lane & 31)) * LF_LDK + kk]);
 #pragma unroll
             for (int g = 0; g < 4; ++g) {
                 const bf16x8_t bv =
-                    *reinterpret_cast<const bf16x8_t *>(&Bs[cur][(g * LF_UNITS + wu + (lane & 31)) * LF_LDK + kk]);
+                    *reinterpret_cast<const bf16x8_t *>(&Bs[(g * LF_UNITS + wu + (lane & 31)) * LF_LDK + kk]);
                 acc[g] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, bv, acc[g], 0, 0, 0);
             }
         }
-        if (ch + 1 < nchunks) LF_STORE_CHUNK(cur ^ 1)
         __syncthreads();
     }
 #undef LF_LOAD_CHUNK
 #undef LF_STORE_CHUNK
+#undef LF_A_LOAD
+#undef LF_A_PUT
+#undef LF_B
+#undef LF_PUT
 
     // epilogue: lane holds unit u for 16 rows; gate g of (row, u) in acc[g][reg]
     const int u = u_base + wu + (lane & 31);
@@ -276,11 +341,19 @@ __global__ __launch_bounds__(256) void lstm_fused_bf16_kernel(
         const int n = n_base + wr + (reg & 3) + 8 * (reg >> 2) + 4 * (lane >> 5);
         if (n < N) {
             const size_t so = ((size_t)b * N + n) * H + u;
-            const float ig = sigm(acc[0][reg] + bi), fg = sigm(acc[1][reg] + bf);
-            const float gg = tanhf(acc[2][reg] + bg), og = sigm(acc[3][reg] + bo);
+#if VN_LF_DIAG == 2
+            const float ig = acc[0][reg] + bi, fg = acc[1][reg] + bf, gg = acc[2][reg] + bg, og = acc[3][reg] + bo;
+#else
+            const float ig = fast_sigm(acc[0][reg] + bi), fg = fast_sigm(acc[1][reg] + bf);
+            const float gg = fast_tanh(acc[2][reg] + bg), og = fast_sigm(acc[3][reg] + bo);
+#endif
             const float fc = fg * c[so], ig2 = ig * gg;
             const float cn = fc + ig2;
-            const float hn = og * tanhf(cn);
+#if VN_LF_DIAG == 2
+            const float hn = og * cn;
+#else
+            const float hn = og * fast_tanh(cn);
+#endif
             c[so] = cn;
             hout[so] = (uint16_t)f2bf(hn);
             if (h32) h32[so] = hn;
@@ -591,11 +664,17 @@ int vn_lstm_fused_bf16(const float *x, int32_t obs_dim, const uint16_t *h_in, co
     if (h_in == h_out) return fail(VN_ERR_INVALID, "h_in and h_out must differ (other blocks read h_in)");
     const int kx = (obs_dim + 7) & ~7;
     if (n_lstm < 1 || N < 1 || obs_dim < 1 || H < 64 || (H % LF_UNITS) || (Kp % LF_KC) || Kp < kx + H)
-        return fail(VN_ERR_INVALID, "bad sizes n_lstm=%d N=%d obs_dim=%d H=%d Kp=%d (H %% 64, Kp %% 32, Kp >= %d)",
-                    n_lstm, N, obs_dim, H, Kp, kx + H);
-    const dim3 grid((unsigned)((N + LF_ROWS - 1) / LF_ROWS), (unsigned)(n_lstm * (H / LF_UNITS)));
-    hipLaunchKernelGGL(lstm_fused_bf16_kernel, grid, dim3(256), 0, (hipStream_t)stream, x, (int)obs_dim, kx, h_in,
-                       w_cat, (int)Kp, bias, c, h_out, h32, h_store, c_store, (int)N, (int)H);
+        return fail(VN_ERR_INVALID, "bad sizes n_lstm=%d N=%d obs_dim=%d H=%d Kp=%d (H %% 64, Kp %% %d, Kp >= %d)",
+                    n_lstm, N, obs_dim, H, Kp, LF_KC, kx + H);
+    // one block per (row tile, combo = LSTM x 64-unit block)
+    const int ncombo = n_lstm * (H / LF_UNITS);
+    const dim3 grid((unsigned)((N + LF_ROWS - 1) / LF_ROWS) * (unsigned)ncombo);
+    if ((obs_dim & 7) == 0)
+        hipLaunchKernelGGL(lstm_fused_bf16_kernel<true>, grid, dim3(256), 0, (hipStream_t)stream, x, (int)obs_dim,
+                           kx, h_in, w_cat, (int)Kp, bias, c, h_out, h32, h_store, c_store, (int)N, (int)H, ncombo);
+    else
+        hipLaunchKernelGGL(lstm_fused_bf16_kernel<false>, grid, dim3(256), 0, (hipStream_t)stream, x, (int)obs_dim,
+                           kx, h_in, w_cat, (int)Kp, bias, c, h_out, h32, h_store, c_store, (int)N, (int)H, ncombo);
     VN_HIP(hipGetLastError());
     return VN_OK;
 }

@@ -97,12 +97,12 @@ class _Weights:
             self.b_ih = torch.stack([f(la.bias_ih_l0), f(lc.bias_ih_l0)])               # [2, 4H]
             self.b_hh = torch.stack([f(la.bias_hh_l0), f(lc.bias_hh_l0)])
             # fused MFMA LSTM step (bf16 path, H % 64 == 0): [W_ih | W_hh] packed
-            # K-contiguous, x part padded to a multiple of 8, K to a multiple of 32
+            # K-contiguous, x part padded to a multiple of 8, K to a multiple of 64
             self.fused = dtype == torch.bfloat16 and self.H % 64 == 0
             if self.fused:
                 od = la.weight_ih_l0.shape[1]
                 self.kx = (od + 7) // 8 * 8
-                self.Kp = (self.kx + self.H + 31) // 32 * 32
+                self.Kp = (self.kx + self.H + 63) // 64 * 64
                 wc = torch.zeros((2, 4 * self.H, self.Kp), dtype=torch.float32, device=device)
                 for b, m in enumerate((la, lc)):
                     wc[b, :, :od] = f(m.weight_ih_l0)

@@ -199,7 +199,7 @@ int vn_lstm_cell_bf16(const uint16_t *gx, int64_t gx_row_stride, const uint16_t 
  *   h_in     bf16 [n_lstm][N][H] previous h (masked); h_out bf16, != h_in
  *   w_cat    bf16 [n_lstm][4H][Kp]: W_ih in columns [0, obs_dim), W_hh in
  *            [kx, kx+H), kx = obs_dim rounded up to 8, zeros elsewhere;
- *            Kp a multiple of 32 >= kx + H
+ *            Kp a multiple of 64 >= kx + H
  *   bias     f32 [n_lstm][4H] = b_ih + b_hh
  *   c        f32 [n_lstm][N][H] in/out; h32 / h_store / c_store f32 or NULL
  * H must be a multiple of 64.

@@ -210,7 +210,7 @@ def test_fused_mfma_lstm_exact_mapping(voxnav):
     rng = np.random.default_rng(21)
     B, N, H, od = 2, 200, 128, 80          # N not a multiple of 64: tail rows
     kx = (od + 7) // 8 * 8
-    Kp = (kx + H + 31) // 32 * 32
+    Kp = (kx + H + 63) // 64 * 64
     x = (rng.integers(-4, 5, size=(N, od)) / 8.0).astype(np.float32)
     h_in = (rng.integers(-4, 5, size=(B, N, H)) / 8.0).astype(np.float32)
     W = (rng.integers(-3, 4, size=(B, 4 * H, od + H)) / 8.0).astype(np.float32)
