@@ -182,9 +182,16 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # rehearsal knob for the multi-rank path on a one-GPU box: every rank on
+    # cuda:0 over gloo (RCCL refuses two ranks on one device); not for numbers
+    if os.environ.get("VOXNAV_BENCH_SHARED_DEVICE") == "1":
+        local = 0
     if world > 1:
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if os.environ.get("VOXNAV_BENCH_SHARED_DEVICE") == "1":
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
 
