@@ -52,7 +52,7 @@ constexpr int MT_C = 8;  // MT words captured by the streaming seed (draws 0..7)
 
 // init_genrand(19650218): the seed-independent prefix of CPython's
 // init_by_array (Modules/_randommodule.c); filled once per device.
-__constant__ uint32_t c_mt_g[MT_N];
+alignas(16) __constant__ uint32_t c_mt_g[MT_N + 8];   // + one zero block (read-ahead)
 
 // ----------------------------------------------------------------------------
 // device data structures
@@ -127,6 +127,8 @@ struct Params {
     // simpleEnv variant
     int variant, obs_dim, pd;
     uint32_t *goal;          // per agent gx | gy<<8 | gz<<16
+    int sbits;               // simpleEnv bit-plane layout (rooms up to 64 x 64 x 31)
+    uint32_t sy_off, sz_off, qz_off;
 };
 
 __device__ __forceinline__ Agent unpack(uint4 s) {
@@ -199,69 +201,130 @@ __device__ __forceinline__ uint32_t mix2(uint32_t m, uint32_t q, uint32_t i) {
     return (m ^ ((q ^ (q >> 30)) * 1566083941u)) - i;
 }
 
-// First MT_C outputs of random.seed(seed) -> out[0..MT_C-1].
-__device__ void mt_first_outputs(uint32_t seed, uint32_t out[MT_C]) {
-    // init_by_array loop 1, i = 1..623 (key[j] + j == seed for a one-word key)
+// The two init_by_array loops are serial chains of 622 steps each (loop 2
+// recomputes the loop-1 words it reads on the fly, a second chain in
+// parallel).  The table words are read 8 at a time one block ahead (scalar
+// loads, uniform index), so a step costs the chain's ALU latency only.
+constexpr int MT_BLK = 8;
+
+// loop 1, i = 2..623: returns p = mt[623] after loop 1
+__device__ __forceinline__ uint32_t mt_loop1(uint32_t p, uint32_t seed) {
+#pragma unroll
+    for (int i = 2; i < MT_BLK; ++i) p = mix1(c_mt_g[i], p, seed);
+    const uint4 *G = reinterpret_cast<const uint4 *>(c_mt_g);
+    uint4 c0 = G[MT_BLK / 4], c1 = G[MT_BLK / 4 + 1];
+    for (int i = MT_BLK; i < MT_N; i += MT_BLK) {
+        const uint4 n0 = G[(i + MT_BLK) / 4], n1 = G[(i + MT_BLK) / 4 + 1];   // table padded by one block
+        p = mix1(c0.x, p, seed);
+        p = mix1(c0.y, p, seed);
+        p = mix1(c0.z, p, seed);
+        p = mix1(c0.w, p, seed);
+        p = mix1(c1.x, p, seed);
+        p = mix1(c1.y, p, seed);
+        p = mix1(c1.z, p, seed);
+        p = mix1(c1.w, p, seed);
+        c0 = n0;
+        c1 = n1;
+    }
+    return p;
+}
+
+// loop 2 over i in [a, b) without captures (p1: loop-1 word chain, q: new words)
+__device__ __forceinline__ void mt_loop2(uint32_t &p1, uint32_t &q, int a, int b, uint32_t seed) {
+    int i = a;
+    for (; i < b && (i & (MT_BLK - 1)); ++i) {
+        p1 = mix1(c_mt_g[i], p1, seed);
+        q = mix2(p1, q, (uint32_t)i);
+    }
+    const uint4 *G = reinterpret_cast<const uint4 *>(c_mt_g);
+    if (i + MT_BLK <= b) {
+        uint4 c0 = G[i / 4], c1 = G[i / 4 + 1];
+        for (; i + MT_BLK <= b; i += MT_BLK) {
+            const uint4 n0 = G[(i + MT_BLK) / 4], n1 = G[(i + MT_BLK) / 4 + 1];
+            const uint32_t gw[MT_BLK] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w};
+#pragma unroll
+            for (int k = 0; k < MT_BLK; ++k) {
+                p1 = mix1(gw[k], p1, seed);
+                q = mix2(p1, q, (uint32_t)(i + k));
+            }
+            c0 = n0;
+            c1 = n1;
+        }
+    }
+    for (; i < b; ++i) {
+        p1 = mix1(c_mt_g[i], p1, seed);
+        q = mix2(p1, q, (uint32_t)i);
+    }
+}
+
+// Outputs [j0, j0 + MT_C) of the first twist of random.seed(seed);
+// j0 % MT_C == 0 and j0 + MT_C <= 227 (the first twist's outputs that read
+// only final state words).  One pass over the two loops.
+struct MtBlock {            // returned by value: stays in VGPRs across the call
+    uint32_t w[MT_C];
+};
+
+__device__ MtBlock mt_outputs(uint32_t seed, int j0) {
+    MtBlock out;
     uint32_t p = mix1(c_mt_g[1], c_mt_g[0], seed);
     const uint32_t m1_1 = p;
-    for (int i = 2; i < MT_N; ++i) p = mix1(c_mt_g[i], p, seed);
+    p = mt_loop1(p, seed);
     const uint32_t m1b1 = mix1(m1_1, p, seed);  // wrap: i = 1 again, mt[0] = mt[623]
-    // loop 2, i = 2..623, recomputing loop-1 words on the fly
     uint32_t p1 = m1_1, q = m1b1;
-    uint32_t lo[MT_C + 1], hi[MT_C];
+    uint32_t lo[MT_C + 1], hi[MT_C];            // F[j0 .. j0+MT_C], F[j0+397 .. j0+397+MT_C-1]
+    if (j0 == 0) {
 #pragma unroll
-    for (int i = 2; i <= MT_C; ++i) {
-        p1 = mix1(c_mt_g[i], p1, seed);
-        q = mix2(p1, q, (uint32_t)i);
-        lo[i] = q;
-    }
-    for (int i = MT_C + 1; i < 397; ++i) {
-        p1 = mix1(c_mt_g[i], p1, seed);
-        q = mix2(p1, q, (uint32_t)i);
-    }
+        for (int i = 2; i <= MT_C; ++i) {
+            p1 = mix1(c_mt_g[i], p1, seed);
+            q = mix2(p1, q, (uint32_t)i);
+            lo[i] = q;
+        }
+    } else {
+        mt_loop2(p1, q, 2, j0, seed);
 #pragma unroll
-    for (int i = 397; i < 397 + MT_C; ++i) {
+        for (int k = 0; k <= MT_C; ++k) {
+            p1 = mix1(c_mt_g[j0 + k], p1, seed);
+            q = mix2(p1, q, (uint32_t)(j0 + k));
+            lo[k] = q;
+        }
+    }
+    mt_loop2(p1, q, j0 + MT_C + 1, 397 + j0, seed);
+#pragma unroll
+    for (int k = 0; k < MT_C; ++k) {
+        const int i = 397 + j0 + k;
         p1 = mix1(c_mt_g[i], p1, seed);
         q = mix2(p1, q, (uint32_t)i);
-        hi[i - 397] = q;
+        hi[k] = q;
     }
-    for (int i = 397 + MT_C; i < MT_N; ++i) {
-        p1 = mix1(c_mt_g[i], p1, seed);
-        q = mix2(p1, q, (uint32_t)i);
+    mt_loop2(p1, q, 397 + j0 + MT_C, MT_N, seed);
+    if (j0 == 0) {
+        lo[1] = mix2(m1b1, q, 1u);              // F[1]: loop 2's wrap step
+        lo[0] = 0x80000000u;                    // F[0]
     }
-    lo[1] = mix2(m1b1, q, 1u);
-    lo[0] = 0x80000000u;
 #pragma unroll
     for (int j = 0; j < MT_C; ++j) {
         const uint32_t y = (lo[j] & 0x80000000u) | (lo[j + 1] & 0x7fffffffu);
-        out[j] = mt_temper(hi[j] ^ (y >> 1) ^ ((y & 1u) ? 0x9908b0dfu : 0u));
+        out.w[j] = mt_temper(hi[j] ^ (y >> 1) ^ ((y & 1u) ? 0x9908b0dfu : 0u));
     }
+    return out;
 }
 
-// Final (pre-twist) state word F[idx] of random.seed(seed); slow path.
-__device__ __noinline__ uint32_t mt_state_word(uint32_t seed, int idx) {
-    if (idx == 0) return 0x80000000u;
-    uint32_t p = mix1(c_mt_g[1], c_mt_g[0], seed);
-    const uint32_t m1_1 = p;
-    for (int i = 2; i < MT_N; ++i) p = mix1(c_mt_g[i], p, seed);
-    const uint32_t m1b1 = mix1(m1_1, p, seed);
-    uint32_t p1 = m1_1, q = m1b1, cap = 0;
-    for (int i = 2; i < MT_N; ++i) {
-        p1 = mix1(c_mt_g[i], p1, seed);
-        q = mix2(p1, q, (uint32_t)i);
-        if (i == idx) cap = q;
-    }
-    return idx == 1 ? mix2(m1b1, q, 1u) : cap;
+__device__ __forceinline__ void mt_first_outputs(uint32_t seed, uint32_t out[MT_C]) {
+    const MtBlock b = mt_outputs(seed, 0);
+#pragma unroll
+    for (int j = 0; j < MT_C; ++j) out[j] = b.w[j];
 }
 
-// Output j (>= MT_C) of the first twist; valid for j < 227.
-__device__ __noinline__ uint32_t mt_output_slow(uint32_t seed, int j, int32_t *err) {
-    if (j >= MT_N - 397) {
+// the next block of outputs, one pass (rejection sampling ran past the buffer)
+__device__ __noinline__ MtBlock mt_refill(uint32_t seed, int j0, int32_t *err) {
+    if (j0 + MT_C > MT_N - 397) {
         atomicOr(err, 1);
-        return 0u;
+        MtBlock z;
+#pragma unroll
+        for (int j = 0; j < MT_C; ++j) z.w[j] = 0u;
+        return z;
     }
-    const uint32_t y = (mt_state_word(seed, j) & 0x80000000u) | (mt_state_word(seed, j + 1) & 0x7fffffffu);
-    return mt_temper(mt_state_word(seed, j + 397) ^ (y >> 1) ^ ((y & 1u) ? 0x9908b0dfu : 0u));
+    return mt_outputs(seed, j0);
 }
 
 struct MtStream {
@@ -271,14 +334,14 @@ struct MtStream {
     int32_t *err;
 
     __device__ uint32_t next() {
-        uint32_t r;
-        if (used < MT_C) {
-            r = buf[0];
+        if (used > 0 && (used % MT_C) == 0) {
+            const MtBlock b = mt_refill(seed, used, err);
 #pragma unroll
-            for (int t = 0; t < MT_C - 1; ++t) buf[t] = buf[t + 1];
-        } else {
-            r = mt_output_slow(seed, used, err);
+            for (int j = 0; j < MT_C; ++j) buf[j] = b.w[j];
         }
+        const uint32_t r = buf[0];
+#pragma unroll
+        for (int t = 0; t < MT_C - 1; ++t) buf[t] = buf[t + 1];
         ++used;
         return r;
     }
@@ -1182,13 +1245,24 @@ __global__ __launch_bounds__(BLOCK, VN_MIN_WAVES_PER_SIMD) void env_kernel(Param
 
 // absolute ray directions of the relative moves (envs/simpleEnv.py:153-158,
 // :224-231) in the ray-record byte order 0:+x 1:-x 2:+y 3:-y 4:+z 5:-z
-__constant__ int8_t c_rel_dir[4][4] = {
+constexpr int kRelDir[4][4] = {
     {2, 0, 3, 1},   // forward  (N, E, S, W)
     {0, 3, 1, 2},   // right
     {3, 1, 2, 0},   // backward
     {1, 2, 0, 3},   // left
 };
-__constant__ int8_t c_facing_of[4] = {1, 3, 0, 2};   // +x -> east(1), -x -> west(3), +y -> north(0), -y -> south(2)
+constexpr uint32_t pack_rel_dir() {
+    uint32_t v = 0;
+    for (int a = 0; a < 4; ++a)
+        for (int f = 0; f < 4; ++f) v |= (uint32_t)kRelDir[a][f] << (2 * (4 * a + f));
+    return v;
+}
+// 2-bit fields in one immediate: no memory lookups on the step's critical path
+__device__ __forceinline__ int rel_dir(int a, int facing) {
+    return (int)((pack_rel_dir() >> (2 * (4 * a + facing))) & 3u);
+}
+// +x -> east(1), -x -> west(3), +y -> north(0), -y -> south(2)
+__device__ __forceinline__ int facing_of(int d) { return (int)((0x8Du >> (2 * d)) & 3u); }
 
 // MT draws of simpleEnv's load_room (:350, :410-426): room, start (drawn if
 // absent or on a wall), goal (drawn if absent or on a wall).  Returns
@@ -1247,8 +1321,8 @@ __device__ __forceinline__ void simple_observe(int8_t *map, const Params &p, con
     const uint2 rec = p.rays[R.ray_off + (uint32_t)((g.x * R.D + g.y) * R.H + g.z)];
     const int cell = (g.x * p.pd + g.y) * p.ph + g.z;
     const int L = p.L;
-    const int dirs[6] = {c_rel_dir[0][g.facing], c_rel_dir[3][g.facing], c_rel_dir[1][g.facing],
-                         c_rel_dir[2][g.facing], 4, 5};   // forward, left, right, backward, up, down (:233)
+    const int dirs[6] = {rel_dir(0, g.facing), rel_dir(3, g.facing), rel_dir(1, g.facing),
+                         rel_dir(2, g.facing), 4, 5};   // forward, left, right, backward, up, down (:233)
 #pragma unroll
     for (int k = 0; k < 6; ++k) row[6 * L + k] = simple_ray(map, p, cell, rec, dirs[k], row + k * L);
     row[6 * L + 6] = (float)g.last_action;
@@ -1342,8 +1416,8 @@ __global__ __launch_bounds__(64) void simple_kernel(Params p) {
             // step (:109-150)
             g.step_count += 1;
             trunc = g.step_count >= R.total_free;                      // :111, max_steps = total_free (:409)
-            const int d = a < 4 ? c_rel_dir[a][g.facing] : (a == 4 ? 4 : 5);
-            if (a < 4) g.facing = c_facing_of[d];                        // :164-171
+            const int d = a < 4 ? rel_dir(a, g.facing) : (a == 4 ? 4 : 5);
+            if (a < 4) g.facing = facing_of(d);                        // :164-171
             const uint2 rec = p.rays[R.ray_off + (uint32_t)((g.x * R.D + g.y) * R.H + g.z)];
             const uint32_t e8 = ((d < 4 ? rec.x : rec.y) >> (8 * (d & 3))) & 0x7fu;
             bool bumped = false, explored = false;
@@ -1407,6 +1481,366 @@ __global__ __launch_bounds__(64) void simple_kernel(Params p) {
     (void)L;
 }
 
+// ============================================================================
+// simpleEnv, bit-plane layout (rooms up to 64 x 64 x 31; larger rooms use the
+// dense kernel above).  The belief map is not stored as bytes.  Per agent:
+//   S  the agent has stood on the cell: internal_grid == 1 (:86, :294), or a
+//      visited cell the edge quirk later turned into 2.  Kept in three axis
+//      planes so that a ray along any axis is one word:
+//      SX[y][z] (bit x, u64), SY[x][z] (bit y, u64), SZ[x][y] (bit z, u32)
+//   Q  edge-quirk mark: the last in-room cell of a ray that leaves the room
+//      becomes 2 (:311-319).  QZ[x][y] (bit z, u32); agent flag in hot.w
+// Every other internal_grid value is a function of S, Q and the walls: the
+// positions the agent has sensed from are exactly its S cells (reset and
+// every step observe where the agent stands, and every such cell is marked),
+// so a cell is known -- 0 if free, 2 if wall -- iff an S cell lies within L
+// cells of it along an axis with only free cells in between (:301-337).
+// export_belief derives the map; the step reads only S and Q.  In-run obs
+// values: Q ? 2 : S ? 1 : 0.
+// ============================================================================
+struct SPlanes {
+    uint64_t *sx, *sy;
+    uint32_t *sz, *qz;
+};
+
+__device__ __forceinline__ SPlanes splanes(const Params &p, int agent) {
+    int8_t *b = p.belief + (size_t)agent * p.agent_bytes;
+    SPlanes q;
+    q.sx = reinterpret_cast<uint64_t *>(b);
+    q.sy = reinterpret_cast<uint64_t *>(b + p.sy_off);
+    q.sz = reinterpret_cast<uint32_t *>(b + p.sz_off);
+    q.qz = reinterpret_cast<uint32_t *>(b + p.qz_off);
+    return q;
+}
+
+// cached S words through the agent's cell + the cell's ray record
+struct SRows {
+    uint64_t wx, wy;
+    uint32_t wz;
+    uint2 rec;
+};
+
+__device__ __forceinline__ uint32_t ray_e8(uint2 rec, int d) {
+    return ((d < 4 ? rec.x : rec.y) >> (8 * (d & 3))) & 0xffu;
+}
+
+// simple_ray on the bit planes: obs values of ray d (L floats) from the S
+// word along the ray axis, Q bits looked up only when the agent has any;
+// then the edge-quirk mark.  Returns count * 0.25.
+// (scalars by value: a select over struct fields folds into a dynamic load
+// from a stack copy of the struct)
+template <int LMAX>
+__device__ __forceinline__ float sb_ray(const Params &p, const SPlanes &pl, int gx, int gy, int gz, bool hasq,
+                                        uint64_t wx, uint64_t wy, uint32_t wz, uint2 rec, int d, float *out,
+                                        bool &newq) {
+    const uint32_t e8 = ray_e8(rec, d);
+    const int n = (int)(e8 & 0x7fu);
+    const int L = p.L;
+    const int m = n < L ? n : L;
+    const int ax = d >> 1;
+    const int sgn = (d & 1) ? -1 : 1;
+    const uint64_t run = ax == 0 ? wx : ax == 1 ? wy : (uint64_t)wz;
+    const int pos = ax == 0 ? gx : ax == 1 ? gy : gz;
+#pragma unroll
+    for (int s = 0; s < LMAX; ++s) {
+        if (s >= L) break;
+        float v;
+        if (s < m) {
+            const int c = pos + sgn * (s + 1);
+            uint32_t b = (uint32_t)(run >> c) & 1u;
+            if (hasq) {
+                const int qx = ax == 0 ? c : gx, qy = ax == 1 ? c : gy, qzz = ax == 2 ? c : gz;
+                if ((pl.qz[qx * p.pd + qy] >> qzz) & 1u) b = 2u;
+            }
+            v = (float)b;
+        } else {
+            v = s == n ? 2.0f : -1.0f;   // wall / edge terminator, then padding (:321-331)
+        }
+        out[s] = v;
+    }
+    if (n < L && !(e8 & 0x80u) && n >= 1) {   // edge quirk (:311-319)
+        const int c = pos + sgn * n;
+        const int qx = ax == 0 ? c : gx, qy = ax == 1 ? c : gy, qzz = ax == 2 ? c : gz;
+        uint32_t *q = pl.qz + qx * p.pd + qy;
+        // no Q bit anywhere yet -> the word is 0 (up and down share a column)
+        const uint32_t old = (hasq || newq) ? *q : 0u;
+        if (!((old >> qzz) & 1u)) *q = old | (1u << qzz);
+        newq = true;
+    }
+    return (float)m * 0.25f;                 // round(count * 0.25, 2) is exact
+}
+
+template <int LMAX>
+__device__ __forceinline__ void sb_observe(const Params &p, const SPlanes &pl, Agent &g, const SRows &w, float *row) {
+    const int L = p.L;
+    const bool hasq = g.move_mask & 1u;
+    bool newq = false;
+    const int dirs[6] = {rel_dir(0, g.facing), rel_dir(3, g.facing), rel_dir(1, g.facing),
+                         rel_dir(2, g.facing), 4, 5};   // forward, left, right, backward, up, down (:233)
+#pragma unroll
+    for (int k = 0; k < 6; ++k)
+        row[6 * L + k] = sb_ray<LMAX>(p, pl, g.x, g.y, g.z, hasq, w.wx, w.wy, w.wz, w.rec, dirs[k], row + k * L, newq);
+    row[6 * L + 6] = (float)g.last_action;
+    if (newq) g.move_mask |= 1u;
+}
+
+__device__ __forceinline__ void sb_load_rows(const Params &p, const SPlanes &pl, const Agent &g, const Room &R,
+                                             SRows &w) {
+    w.wx = pl.sx[g.y * p.ph + g.z];
+    w.wy = pl.sy[g.x * p.ph + g.z];
+    w.wz = pl.sz[g.x * p.pd + g.y];
+    w.rec = p.rays[R.ray_off + (uint32_t)((g.x * R.D + g.y) * R.H + g.z)];
+}
+
+// reset for the lanes with `need` (as simple_reset_wave): the wave zeroes
+// every resetting agent's planes, then each marks its start cell and senses.
+template <int LMAX>
+__device__ __forceinline__ void sb_reset_wave(const Params &p, const SPlanes &pl, bool need, uint32_t seed, Agent &g, uint32_t &goal,
+                              Room &R, SRows &w, float *row, int lane, int block_agent0) {
+    uint2 drawn = make_uint2(0u, 0u);
+    if (need) drawn = simple_draw(p.envc, seed);
+    uint64_t m = __ballot(need);
+    const uint32_t n16 = p.agent_bytes >> 4;
+    while (m) {
+        const int src = __ffsll((unsigned long long)m) - 1;
+        m &= m - 1;
+        uint4 *base = reinterpret_cast<uint4 *>(p.belief + (size_t)(block_agent0 + src) * p.agent_bytes);
+        for (uint32_t q = (uint32_t)lane; q < n16; q += 64u) base[q] = make_uint4(0u, 0u, 0u, 0u);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+    if (need) {
+        g.room = (int)(drawn.x >> 24);
+        R = load_room(p, g.room);
+        g.x = drawn.x & 0xff;
+        g.y = (drawn.x >> 8) & 0xff;
+        g.z = (drawn.x >> 16) & 0xff;
+        goal = drawn.y;
+        g.facing = 0;
+        g.last_action = 0;
+        g.done = g.last_bump = g.near_wall = g.was_near_wall = false;
+        g.step_count = 0;
+        g.visited = 1;
+        g.bumps = 0;
+        g.cid = 0;
+        g.move_mask = 0;
+        w.wx = 1ull << g.x;                                                     // :86
+        w.wy = 1ull << g.y;
+        w.wz = 1u << g.z;
+        pl.sx[g.y * p.ph + g.z] = w.wx;
+        pl.sy[g.x * p.ph + g.z] = w.wy;
+        pl.sz[g.x * p.pd + g.y] = w.wz;
+        w.rec = p.rays[R.ray_off + (uint32_t)((g.x * R.D + g.y) * R.H + g.z)];
+        sb_observe<LMAX>(p, pl, g, w, row);
+    }
+}
+
+#ifndef VN_SIMPLE_PROF
+#define VN_SIMPLE_PROF 0   // diagnostics build: per-section shader-clock totals (vn_debug_simple_prof)
+#endif
+#if VN_SIMPLE_PROF
+__device__ unsigned long long g_simple_prof[16];
+#define SB_T(k)                                                    \
+    do {                                                           \
+        const uint64_t t_ = __builtin_amdgcn_s_memtime();          \
+        prof[k] += t_ - tprev;                                     \
+        tprev = t_;                                                \
+    } while (0)
+#else
+#define SB_T(k) \
+    do {        \
+    } while (0)
+#endif
+
+template <bool RESET_ONLY, int LMAX>
+__global__ __launch_bounds__(64) void simple_bits_kernel(Params p) {
+    extern __shared__ float sstage[];   // [64][obs_dim]
+    const int lane = threadIdx.x;
+    const int a0 = blockIdx.x * 64;
+    const int ai = a0 + lane;
+    const bool live = ai < p.N;
+    const int OD = p.obs_dim, L = p.L;
+    const int rows = min(64, p.N - a0);
+    float *row = sstage + lane * OD;
+    const SPlanes pl = splanes(p, live ? ai : a0);
+    Agent g = unpack(live ? p.hot[ai] : make_uint4(0u, 0u, 0u, 0u));
+    uint32_t goal = live ? p.goal[ai] : 0u;
+    uint32_t next_seed = live ? p.next_seed[ai] : 0u;
+    Room R = load_room(p, g.room);
+    SRows w;
+    w.wx = w.wy = 0;
+    w.wz = 0;
+    w.rec = make_uint2(0u, 0u);
+
+    if (RESET_ONLY) {
+        const bool need = live && (!p.mask || p.mask[ai]);
+        const uint32_t seed = need ? (uint32_t)p.seeds[ai] : 0u;
+        sb_reset_wave<LMAX>(p, pl, need, seed, g, goal, R, w, row, lane, a0);
+        if (need) {
+            float *o = p.obs + (size_t)ai * OD;
+            for (int k = 0; k < OD; ++k) o[k] = row[k];
+            p.hot[ai] = pack(g);
+            p.goal[ai] = goal;
+            p.next_seed[ai] = seed + p.seed_stride;   // modulo 2^32
+        }
+        return;
+    }
+    if (live) sb_load_rows(p, pl, g, R, w);
+#if VN_SIMPLE_PROF
+    uint64_t prof[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    uint64_t tprev = __builtin_amdgcn_s_memtime();
+#endif
+
+    uint4 r4 = make_uint4(0u, 0u, 0u, 0u);   // Philox block of steps t & ~3 (one call per 4 steps)
+    for (int k = 0; k < p.K; ++k) {
+        const uint64_t t = p.t0 + (uint64_t)k;
+        int a = 0;
+        if (live) {
+            if (p.actions) {
+                a = p.actions[(size_t)k * p.N + ai];
+            } else if (p.ablate & 32u) {
+                a = (int)((ai + (int)t * 7) % 6);
+            } else {
+                if (k == 0 || (t & 3) == 0) r4 = philox4x32_10(p.policy_seed, p.gid_base + (uint64_t)ai, t >> 2);
+                const uint32_t word = (t & 3) == 0 ? r4.x : (t & 3) == 1 ? r4.y : (t & 3) == 2 ? r4.z : r4.w;
+                a = (int)(((uint64_t)word * 6u) >> 32);
+            }
+            if (p.actions_out) p.actions_out[(size_t)k * p.N + ai] = a;
+        }
+        SB_T(0);
+        bool trunc = false, term = false;
+        double r = 0.0;
+        if (live) {
+            // step (:109-150)
+            g.step_count += 1;
+            trunc = g.step_count >= R.total_free;                      // :111, max_steps = total_free (:409)
+            const int d = a < 4 ? rel_dir(a, g.facing) : (a == 4 ? 4 : 5);
+            if (a < 4) g.facing = facing_of(d);                        // :164-171
+            const bool moved = (ray_e8(w.rec, d) & 0x7fu) >= 1u;
+            bool explored = false;
+            if (moved) {                                                 // _mark_visited (:273-298)
+                const int nx = g.x + (d == 0 ? 1 : d == 1 ? -1 : 0);
+                const int ny = g.y + (d == 2 ? 1 : d == 3 ? -1 : 0);
+                const int nz = g.z + (d == 4 ? 1 : d == 5 ? -1 : 0);
+                // S bit of the target from the cached word of the move axis
+                const int ax = d >> 1;
+                const uint64_t wx0 = w.wx, wy0 = w.wy;
+                const uint32_t wz0 = w.wz;
+                bool seen = ax == 0 ? ((wx0 >> nx) & 1ull) : ax == 1 ? ((wy0 >> ny) & 1ull) : ((wz0 >> nz) & 1u);
+                g.x = nx;
+                g.y = ny;
+                g.z = nz;
+                sb_load_rows(p, pl, g, R, w);
+                // a Q cell (internal_grid 2) is entered without counting, but
+                // it is a sensing position all the same, so S is set
+                const bool q = (g.move_mask & 1u) && ((pl.qz[nx * p.pd + ny] >> nz) & 1u);
+                if (!seen) {
+                    w.wx |= 1ull << nx;
+                    w.wy |= 1ull << ny;
+                    w.wz |= 1u << nz;
+                    pl.sx[ny * p.ph + nz] = w.wx;
+                    pl.sy[nx * p.ph + nz] = w.wy;
+                    pl.sz[nx * p.pd + ny] = w.wz;
+                    if (!q) {
+                        g.visited += 1;
+                        explored = true;
+                    }
+                }
+            }
+            g.last_action = a;                                           // :137
+            SB_T(1);
+            if (!(p.ablate & 4u)) sb_observe<LMAX>(p, pl, g, w, row);    // :139
+            SB_T(2);
+            // compute_reward (:189-217), f64 in the reference's order
+            r = -0.1;
+            if (!moved) {
+                g.bumps += 1;
+                r += -10.0;
+            }
+            if (a != 2 && a < 4) r += 0.05;
+            const int gx = goal & 0xff, gy = (goal >> 8) & 0xff, gz = (goal >> 16) & 0xff;
+            if (g.x == gx && g.y == gy && g.z >= gz && g.z - gz < 5) {   // SPOT_GOAL_HEIGTH = 5 (:201-206)
+                g.done = true;
+                r += 100.0;
+            }
+            if (trunc) r += 0.0;
+            if (explored) r += 1.0;
+            term = g.done;
+            const size_t o = (size_t)k * p.N + ai;
+            if (p.reward && !(p.ablate & 8u)) p.reward[o] = (float)r;
+            if (p.reward64) p.reward64[o] = r;
+            if (p.term) p.term[o] = term;
+            if (p.trunc) p.trunc[o] = trunc;
+            if ((term || trunc) && p.autoreset && p.terminal_obs) {
+                float *to = p.terminal_obs + o * OD;
+                for (int q = 0; q < OD; ++q) to[q] = row[q];
+            }
+        }
+        SB_T(3);
+        // SB3 VecEnv auto-reset
+        const bool need = live && p.autoreset && (term || trunc);
+        if (__ballot(need)) {
+#if VN_SIMPLE_PROF
+            if (lane == 0) atomicAdd(&g_simple_prof[8], (unsigned long long)__popcll(__ballot(need)));
+            if (lane == 0) atomicAdd(&g_simple_prof[10], 1ull);
+#endif
+            sb_reset_wave<LMAX>(p, pl, need, next_seed, g, goal, R, w, row, lane, a0);
+            if (need) next_seed += p.seed_stride;
+        }
+        SB_T(4);
+        __syncthreads();
+        float *dst = p.obs + ((size_t)k * p.N + a0) * OD;
+        if (p.ablate & 16u) {
+        } else if (rows == 64 && !(reinterpret_cast<uintptr_t>(dst) & 15u)) {   // 64 rows = 16 * OD float4s
+            const float4 *s4 = reinterpret_cast<const float4 *>(sstage);
+            float4 *d4 = reinterpret_cast<float4 *>(dst);
+            for (int q = lane; q < 16 * OD; q += 64) obs_store(d4 + q, s4[q]);
+        } else {
+            for (int q = lane; q < rows * OD; q += 64) __builtin_nontemporal_store(sstage[q], dst + q);
+        }
+        __syncthreads();
+        SB_T(5);
+    }
+#if VN_SIMPLE_PROF
+    if (lane == 0) {
+        uint64_t tot = 0;
+        for (int q = 0; q < 6; ++q) {
+            atomicAdd(&g_simple_prof[q], (unsigned long long)prof[q]);
+            tot += prof[q];
+        }
+        atomicAdd(&g_simple_prof[7], 1ull);
+        atomicMax(&g_simple_prof[6], (unsigned long long)tot);
+        atomicMax(&g_simple_prof[9], (unsigned long long)prof[4]);
+    }
+#endif
+    if (live) {
+        p.hot[ai] = pack(g);
+        p.goal[ai] = goal;
+        p.next_seed[ai] = next_seed;
+    }
+}
+
+// internal_grid value of one cell from S, Q and the walls (see the layout
+// note above the bit-plane kernel)
+__device__ int8_t sb_belief_cell(const Params &p, int i, const Room &R, int x, int y, int z) {
+    const SPlanes pl = splanes(p, i);
+    auto wall = [&](int cx, int cy, int cz) {
+        return ((p.rays[R.ray_off + (uint32_t)((cx * R.D + cy) * R.H + cz)].y >> 16) & 1u) != 0u;
+    };
+    auto sbit = [&](int cx, int cy, int cz) { return ((pl.sz[cx * p.pd + cy] >> cz) & 1u) != 0u; };
+    const bool is_wall = wall(x, y, z);
+    if (!is_wall && ((pl.qz[x * p.pd + y] >> z) & 1u)) return 2;
+    if (sbit(x, y, z)) return 1;
+    static constexpr int DX[6] = {1, -1, 0, 0, 0, 0}, DY[6] = {0, 0, 1, -1, 0, 0}, DZ[6] = {0, 0, 0, 0, 1, -1};
+    for (int d = 0; d < 6; ++d) {
+        for (int s = 1; s <= p.L; ++s) {   // a sensing position p = c - s * d, free cells in between
+            const int px = x - DX[d] * s, py = y - DY[d] * s, pz = z - DZ[d] * s;
+            if (px < 0 || px >= R.W || py < 0 || py >= R.D || pz < 0 || pz >= R.H || wall(px, py, pz)) break;
+            if (sbit(px, py, pz)) return is_wall ? 2 : 0;
+        }
+    }
+    return -1;
+}
+
 // ----------------------------------------------------------------------------
 // exports (parity dumps)
 // ----------------------------------------------------------------------------
@@ -1436,7 +1870,9 @@ __global__ void export_belief_kernel(Params p, int8_t *out, int pw, int pd) {
     const Agent g = unpack(p.hot[i]);
     const Room R = load_room(p, g.room);
     int8_t v = -128;
-    if (x < R.W && y < R.D && z < R.H && p.variant == VN_VARIANT_SIMPLE) {
+    if (x < R.W && y < R.D && z < R.H && p.variant == VN_VARIANT_SIMPLE && p.sbits) {
+        v = sb_belief_cell(p, i, R, x, y, z);
+    } else if (x < R.W && y < R.D && z < R.H && p.variant == VN_VARIANT_SIMPLE) {
         v = p.belief[(size_t)i * p.agent_bytes + (size_t)(x * p.pd + y) * p.ph + z];
     } else if (x < R.W && y < R.D && z < R.H) {
         const uint32_t off = (uint32_t)((((((x >> 2) * p.nby + (y >> 2)) << 4) + ((x & 3) << 2) + (y & 3)) * p.ph) + z);
@@ -1505,6 +1941,8 @@ struct VnEnv {
     uint32_t *d_goal = nullptr;
     uint32_t ablate = 0;
     int variant = 0, obs_dim = VN_OBS_DIM;
+    int sbits = 0;
+    uint32_t sy_off = 0, sz_off = 0, qz_off = 0;
 };
 
 namespace {
@@ -1569,6 +2007,10 @@ Params base_params(VnEnv *e) {
     p.obs_dim = e->obs_dim;
     p.pd = e->pd;
     p.goal = e->d_goal;
+    p.sbits = e->sbits;
+    p.sy_off = e->sy_off;
+    p.sz_off = e->sz_off;
+    p.qz_off = e->qz_off;
     return p;
 }
 
@@ -1590,7 +2032,18 @@ template <bool RESET_ONLY>
 int launch_env(VnEnv *e, const Params &p, hipStream_t s) {
     if (e->variant == VN_VARIANT_SIMPLE) {
         const size_t lds = (size_t)64 * e->obs_dim * sizeof(float);
-        hipLaunchKernelGGL((simple_kernel<RESET_ONLY>), dim3((unsigned)((e->N + 63) / 64)), dim3(64), lds, s, p);
+        const dim3 grid((unsigned)((e->N + 63) / 64));
+        const int L = e->cfg.local_map_length;
+        if (e->sbits && L <= 4)
+            hipLaunchKernelGGL((simple_bits_kernel<RESET_ONLY, 4>), grid, dim3(64), lds, s, p);
+        else if (e->sbits && L <= 8)
+            hipLaunchKernelGGL((simple_bits_kernel<RESET_ONLY, 8>), grid, dim3(64), lds, s, p);
+        else if (e->sbits && L <= 10)
+            hipLaunchKernelGGL((simple_bits_kernel<RESET_ONLY, 10>), grid, dim3(64), lds, s, p);
+        else if (e->sbits)
+            hipLaunchKernelGGL((simple_bits_kernel<RESET_ONLY, 16>), grid, dim3(64), lds, s, p);
+        else
+            hipLaunchKernelGGL((simple_kernel<RESET_ONLY>), dim3((unsigned)((e->N + 63) / 64)), dim3(64), lds, s, p);
         VN_HIP(hipGetLastError());
         return VN_OK;
     }
@@ -1750,7 +2203,21 @@ int vn_create(const VnRoomSet *rooms, int32_t n_agents, const VnConfig *cfg, int
     e->nbx = (maxW + 3) / 4;
     e->nby = (maxD + 3) / 4;
     e->ph = maxH <= 8 ? 8 : maxH <= 16 ? 16 : 32;   // whole column = one 8/16/32-byte access
-    if (e->variant == VN_VARIANT_SIMPLE) {
+    const char *dense_env = getenv("VOXNAV_SIMPLE_DENSE");   // force the dense kernel (tests)
+    const bool dense = dense_env && dense_env[0] == '1';
+    if (e->variant == VN_VARIANT_SIMPLE && maxW <= 64 && maxD <= 64 && !dense) {
+        // bit planes: SX u64 [pd][ph], SY u64 [pw][ph], SZ u32 [pw][pd], QZ u32 [pw][pd]
+        e->sbits = 1;
+        e->pw = maxW;
+        e->pd = maxD;
+        e->map_bytes = 0;
+        e->nwx = e->nwy = 0;
+        e->sy_off = (uint32_t)(8 * e->pd * e->ph);
+        e->sz_off = e->sy_off + (uint32_t)(8 * e->pw * e->ph);
+        e->qz_off = e->sz_off + (uint32_t)(4 * e->pw * e->pd);
+        e->xp_off = e->yp_off = 0;
+        e->agent_bytes = (e->qz_off + (uint32_t)(4 * e->pw * e->pd) + 15u) & ~15u;
+    } else if (e->variant == VN_VARIANT_SIMPLE) {
         // dense [pw][pd][ph] int8 map, no planes
         e->pw = maxW;
         e->pd = maxD;
@@ -1818,8 +2285,8 @@ int vn_create(const VnRoomSet *rooms, int32_t n_agents, const VnConfig *cfg, int
     if (he == hipSuccess) he = hipMemcpy(e->d_lut, lut, sizeof(lut), hipMemcpyHostToDevice);
     if (he == hipSuccess) he = hipMemset(e->d_hot, 0, (size_t)n_agents * sizeof(uint4));
     if (he == hipSuccess) he = hipMemset(e->d_seed, 0, (size_t)n_agents * sizeof(uint32_t));
-    // unknown: 0x00 in the CubicEnv byte encoding, -1 (0xFF) in the simpleEnv map
-    if (he == hipSuccess) he = hipMemset(e->d_belief, e->variant == VN_VARIANT_SIMPLE ? 0xFF : 0x00, belief_bytes);
+    // unknown: 0x00 in the CubicEnv byte encoding, -1 (0xFF) in the dense simpleEnv map; empty bit planes
+    if (he == hipSuccess) he = hipMemset(e->d_belief, e->variant == VN_VARIANT_SIMPLE && !e->sbits ? 0xFF : 0x00, belief_bytes);
     if (he == hipSuccess) he = hipMemset(e->d_goal, 0, (size_t)n_agents * sizeof(uint32_t));
     if (he == hipSuccess) he = hipMemset(e->d_err, 0, sizeof(int32_t));
     if (he == hipSuccess) {
@@ -1935,6 +2402,17 @@ int vn_export_belief(VnEnv *env, int8_t *belief_out, void *stream) {
     VN_HIP(hipGetLastError());
     return VN_OK;
 }
+
+#if VN_SIMPLE_PROF
+int vn_debug_simple_prof(unsigned long long *out16, int clear) {
+    VN_HIP(hipMemcpyFromSymbol(out16, HIP_SYMBOL(g_simple_prof), sizeof(unsigned long long) * 16));
+    if (clear) {
+        unsigned long long z[16] = {0};
+        VN_HIP(hipMemcpyToSymbol(HIP_SYMBOL(g_simple_prof), z, sizeof(z)));
+    }
+    return VN_OK;
+}
+#endif
 
 int vn_gae(const float *rewards, const float *values, const float *episode_starts, const float *last_values,
            const float *dones, int32_t T, int32_t N, double gamma, double gae_lambda, float *advantages,

@@ -87,6 +87,27 @@ SIMPLE_CASES = [
 
 @pytest.mark.parametrize("src,L,N,K", SIMPLE_CASES, ids=[f"{c[0]}-L{c[1]}" for c in SIMPLE_CASES])
 def test_simple_random_rollout_matches_oracle(voxnav, src, L, N, K):
+    _rollout_vs_oracle(src, L, N, K)
+
+
+# the dense int8 map kernel: rooms wider or deeper than 64 cells, or forced
+# with VOXNAV_SIMPLE_DENSE=1 (the bit-plane kernel covers the cases above)
+DENSE_CASES = [
+    ("ctor:70x9x5", 4, 256, 200, False),
+    ("ctor:10x66x5", 6, 128, 150, False),
+    ("set:P3_training", 10, 512, 150, True),
+    ("box:8x8x4", 4, 256, 200, True),
+]
+
+
+@pytest.mark.parametrize("src,L,N,K,force", DENSE_CASES, ids=[f"{c[0]}-L{c[1]}" for c in DENSE_CASES])
+def test_simple_dense_layout_matches_oracle(voxnav, monkeypatch, src, L, N, K, force):
+    if force:
+        monkeypatch.setenv("VOXNAV_SIMPLE_DENSE", "1")
+    _rollout_vs_oracle(src, L, N, K)
+
+
+def _rollout_vs_oracle(src, L, N, K):
     env = make_env(src, L, n=N, autoreset=True)
     seeds = 42 + np.arange(N, dtype=np.int64)
     obs0 = env.reset(seed=42).cpu().numpy()
