@@ -11,13 +11,16 @@ include/voxnav.h.  Public API:
   SimpleGridAgent     the same for the goal-seeking simpleEnv variant
   RolloutCollector    on-device PPO rollout collection (policy in the loop)
   compute_gae         GAE advantage/return scan kernel
+  PPOLearner          (Recurrent)PPO.train on the collector's device buffers (+ DDP)
+  evaluate_policy     evaluate_grid.py's deterministic-episode metrics, batched
+  save_checkpoint / load_checkpoint   SB3 .zip layout, Grid_Train naming
   sharding            multi-GPU agent sharding helpers
 """
 from . import rooms  # noqa: F401
 from ._native import VoxnavError, load as load_library  # noqa: F401
 
 __all__ = ["rooms", "BatchedGridEnv", "GridAgent", "SimpleGridAgent", "RolloutCollector", "compute_gae",
-           "VoxnavError", "load_library"]
+           "PPOLearner", "evaluate_policy", "save_checkpoint", "load_checkpoint", "VoxnavError", "load_library"]
 
 
 def __getattr__(name):
@@ -37,4 +40,13 @@ def __getattr__(name):
     if name == "compute_gae":
         from .gae import compute_gae
         return compute_gae
+    if name == "PPOLearner":
+        from .ppo import PPOLearner
+        return PPOLearner
+    if name == "evaluate_policy":
+        from .evaluate import evaluate_policy
+        return evaluate_policy
+    if name in ("save_checkpoint", "load_checkpoint"):
+        from . import checkpoint
+        return getattr(checkpoint, name)
     raise AttributeError(name)

@@ -277,6 +277,16 @@ class RolloutCollector:
         lat = _mlp(w.vf, x)
         self._head(None, lat, M, 0, None, out, None)
 
+    @torch.no_grad()
+    def act(self, obs: torch.Tensor) -> torch.Tensor:
+        """``model.predict(obs, state)`` for all agents: one policy step on obs
+        [N, obs_dim] that advances the collector's recurrent state; returns
+        the actions [N] int32 (a view, valid until the next call).  Argmax
+        when the collector was built with ``deterministic=True``."""
+        self._forward(obs.contiguous(), 0)
+        self.t_global += 1
+        return self.actions[0]
+
     # -------------------------------------------------------------- rollout
     @torch.no_grad()
     def collect(self) -> RolloutBuffer:

@@ -1,0 +1,220 @@
+"""PPO learner on the collector's device buffers.
+
+Restates the update the reference runs through ``model.learn``
+(train/Grid_Train.py:228; RecurrentPPO with the hyperparameters of
+train/Grid_Train.py:84-86: lr 3e-4, batch_size 64, n_epochs 10, clip 0.2,
+ent_coef 0.01, vf_coef 0.5; SB3 defaults max_grad_norm 0.5,
+normalize_advantage True, Adam eps 1e-5):
+
+* sb3_contrib ``RecurrentPPO.train`` for ``RecurrentActorCriticPolicy``:
+  per epoch the env-major flattened buffer (``swap_and_flatten``) is rolled
+  by a random split index and cut into minibatches of ``batch_size``
+  samples; each minibatch is split into sequences at episode starts and env
+  changes (``create_sequencers``), padded, and both LSTMs are re-run from
+  the buffer's stored states at the sequence starts (``_process_sequence``);
+  clipped surrogate + value MSE + entropy over the unpadded positions,
+  advantages normalised per minibatch, grad-norm clip, Adam.
+* SB3 ``PPO.train`` for ``ActorCriticPolicy``: a random permutation per
+  epoch, same losses without sequences.
+
+Everything stays on the device: minibatch rows are gathered straight from
+the collector's ``[T, N]``-major buffers by index arithmetic (no flattened
+copies), sequences are packed with one scatter, and each LSTM runs as one
+``nn.LSTM`` call over the padded batch (MIOpen), which equals sb3's masked
+per-step loop because a sequence can only begin with an episode start.
+The one host round-trip per recurrent minibatch is the (n_seq, max_len)
+pair that sizes the padded tensor.
+
+With ``process_group`` set, gradients are averaged over the ranks (one
+flattened all-reduce per minibatch, RCCL over xGMI with the nccl backend)
+before the clip -- data-parallel training over agent shards.
+
+The minibatch order is drawn from ``numpy.random.default_rng(seed)``
+(sb3 uses the global numpy generator) or passed explicitly as
+``epoch_orders`` (what the parity tests do with ``oracle/ppo_oracle.py``).
+"""
+from __future__ import annotations
+
+from typing import Dict, List, Optional, Sequence
+
+import numpy as np
+import torch
+import torch.nn.functional as Fn
+
+from .policy import ActorCriticPolicy, RecurrentActorCriticPolicy
+
+
+class PPOLearner:
+    def __init__(self, policy, learning_rate: float = 3e-4, n_epochs: int = 10, batch_size: int = 64,
+                 clip_range: float = 0.2, ent_coef: float = 0.01, vf_coef: float = 0.5, max_grad_norm: float = 0.5,
+                 normalize_advantage: bool = True, seed: int = 0, process_group=None):
+        if not isinstance(policy, (ActorCriticPolicy, RecurrentActorCriticPolicy)):
+            raise TypeError("policy must be an ActorCriticPolicy or RecurrentActorCriticPolicy")
+        if batch_size < 1 or n_epochs < 1:
+            raise ValueError("batch_size and n_epochs must be >= 1")
+        self.policy = policy
+        self.recurrent = bool(getattr(policy, "recurrent", False))
+        self.lr = float(learning_rate)
+        self.n_epochs = int(n_epochs)
+        self.batch_size = int(batch_size)
+        self.clip_range = float(clip_range)
+        self.ent_coef = float(ent_coef)
+        self.vf_coef = float(vf_coef)
+        self.max_grad_norm = float(max_grad_norm)
+        self.normalize_advantage = bool(normalize_advantage)
+        self.rng = np.random.default_rng(seed)
+        self.group = process_group
+        self.params = [p for p in policy.parameters() if p.requires_grad]
+        self.optimizer = torch.optim.Adam(self.params, lr=self.lr, eps=1e-5)
+        self.n_updates = 0
+
+    # ------------------------------------------------------------ helpers
+    def _orders(self, total: int) -> List:
+        if self.recurrent:
+            return [int(self.rng.integers(total)) for _ in range(self.n_epochs)]
+        return [self.rng.permutation(total) for _ in range(self.n_epochs)]
+
+    def _allreduce_grads(self):
+        import torch.distributed as dist
+        grads = [p.grad for p in self.params if p.grad is not None]
+        flat = torch.cat([g.reshape(-1) for g in grads])
+        dist.all_reduce(flat, op=dist.ReduceOp.SUM, group=self.group)
+        flat /= dist.get_world_size(self.group)
+        o = 0
+        for g in grads:
+            n = g.numel()
+            g.copy_(flat[o:o + n].view_as(g))
+            o += n
+
+    def _heads(self, lat_pi, lat_vf, actions):
+        pol = self.policy
+        logits = pol.action_net(pol.mlp_extractor.policy_net(lat_pi))
+        values = pol.value_net(pol.mlp_extractor.value_net(lat_vf)).flatten()
+        logp_all = torch.log_softmax(logits, dim=-1)
+        log_prob = logp_all.gather(1, actions.view(-1, 1)).flatten()
+        entropy = -(logp_all.exp() * logp_all).sum(-1)
+        return values, log_prob, entropy
+
+    def _evaluate_recurrent(self, buf, idx: torch.Tensor):
+        """evaluate_actions on minibatch rows ``idx`` (env-major flat ids)."""
+        T, N = buf.actions.shape
+        dev = idx.device
+        env = idx // T
+        t = idx - env * T
+        src = t * N + env                                         # row in the [T, N]-major buffers
+        es = buf.episode_starts.reshape(-1)[src]
+        seq_start = (es > 0.5) | (t == 0)                         # episode start or env change
+        seq_start[0] = True
+        seq_id = torch.cumsum(seq_start.to(torch.int64), 0) - 1
+        first = torch.nonzero(seq_start, as_tuple=True)[0]       # position of each sequence start
+        pos = torch.arange(idx.numel(), device=dev) - first[seq_id]
+        n_seq, max_len = (int(v) for v in torch.stack([seq_id[-1] + 1, pos.max() + 1]).tolist())
+        D = buf.obs.shape[-1]
+        x = torch.zeros((max_len, n_seq, D), dtype=torch.float32, device=dev)
+        x[pos, seq_id] = buf.obs.reshape(T * N, D)[src]
+        keep = (1.0 - es[first]).view(1, n_seq, 1)               # (1 - episode_start) at the sequence start
+        tf, ef = t[first], env[first]
+        h0 = buf.lstm_h[tf, :, ef].permute(1, 0, 2) * keep        # stored states [T, 2, N, H] -> [2, n_seq, H]
+        c0 = buf.lstm_c[tf, :, ef].permute(1, 0, 2) * keep
+        pol = self.policy
+        out_pi, _ = pol.lstm_actor(x, (h0[0:1].contiguous(), c0[0:1].contiguous()))
+        out_vf, _ = pol.lstm_critic(x, (h0[1:2].contiguous(), c0[1:2].contiguous()))
+        lat_pi = out_pi[pos, seq_id]
+        lat_vf = out_vf[pos, seq_id]
+        acts = buf.actions.reshape(-1)[src].long()
+        return self._heads(lat_pi, lat_vf, acts), src
+
+    def _evaluate_ff(self, buf, idx: torch.Tensor):
+        T, N = buf.actions.shape
+        env = idx // T
+        src = (idx - env * T) * N + env
+        obs = buf.obs.reshape(T * N, -1)[src]
+        acts = buf.actions.reshape(-1)[src].long()
+        return self._heads(obs, obs, acts), src
+
+    def update(self, buf, idx: torch.Tensor) -> torch.Tensor:
+        """One minibatch (env-major flat ids ``idx``): losses, backward,
+        (all-reduce), clip, Adam.  Returns the logged values as a device
+        tensor (no host sync)."""
+        (values, log_prob, entropy), src = (self._evaluate_recurrent(buf, idx) if self.recurrent
+                                            else self._evaluate_ff(buf, idx))
+        adv = buf.advantages.reshape(-1)[src]
+        if self.normalize_advantage and (self.recurrent or adv.numel() > 1):
+            adv = (adv - adv.mean()) / (adv.std() + 1e-8)
+        old_lp = buf.log_probs.reshape(-1)[src]
+        ret = buf.returns.reshape(-1)[src]
+        ratio = torch.exp(log_prob - old_lp)
+        l1 = adv * ratio
+        l2 = adv * torch.clamp(ratio, 1 - self.clip_range, 1 + self.clip_range)
+        policy_loss = -torch.min(l1, l2).mean()
+        value_loss = Fn.mse_loss(ret, values)
+        entropy_loss = -entropy.mean()
+        loss = policy_loss + self.ent_coef * entropy_loss + self.vf_coef * value_loss
+        self.optimizer.zero_grad(set_to_none=True)
+        loss.backward()
+        if self.group is not None:
+            self._allreduce_grads()
+        gnorm = torch.nn.utils.clip_grad_norm_(self.params, self.max_grad_norm)
+        self.optimizer.step()
+        self.n_updates += 1
+        with torch.no_grad():
+            log_ratio = log_prob - old_lp
+            return torch.stack([policy_loss.detach().double(), value_loss.detach().double(),
+                                entropy_loss.detach().double(), loss.detach().double(),
+                                ((torch.exp(log_ratio) - 1) - log_ratio).mean().double(),
+                                (torch.abs(ratio - 1) > self.clip_range).double().mean(),
+                                gnorm.detach().double()])
+
+    # ------------------------------------------------------------ train
+    def train(self, buf, epoch_orders: Optional[Sequence] = None) -> Dict[str, float]:
+        """One ``train()`` over a collector ``RolloutBuffer`` (n_epochs passes).
+        Returns the means of sb3's logged quantities."""
+        T, N = buf.actions.shape
+        total = T * N
+        dev = buf.actions.device
+        if self.recurrent and (buf.lstm_h is None or buf.lstm_c is None):
+            raise ValueError("the recurrent learner needs the buffer's LSTM states (store_lstm_states=True)")
+        orders = list(epoch_orders) if epoch_orders is not None else self._orders(total)
+        acc = torch.zeros(7, dtype=torch.float64, device=dev)
+        n_mb = 0
+        self.policy.train()
+        for order in orders:
+            if self.recurrent:
+                perm = torch.roll(torch.arange(total, device=dev), -int(order))
+            else:
+                perm = torch.as_tensor(np.asarray(order), dtype=torch.int64, device=dev)
+            for s in range(0, total, self.batch_size):
+                acc += self.update(buf, perm[s:s + self.batch_size])
+                n_mb += 1
+        m = (acc / max(1, n_mb)).tolist()
+        with torch.no_grad():
+            v, r = buf.values.reshape(-1), buf.returns.reshape(-1)
+            var_r = torch.var(r)
+            ev = float("nan") if float(var_r) == 0 else float(1 - torch.var(r - v) / var_r)
+        return dict(policy_gradient_loss=m[0], value_loss=m[1], entropy_loss=m[2], loss=m[3], approx_kl=m[4],
+                    clip_fraction=m[5], grad_norm=m[6], explained_variance=ev, n_minibatches=n_mb,
+                    n_updates=self.n_updates)
+
+
+def learn(collector, learner: PPOLearner, total_timesteps: int, callback=None) -> List[Dict[str, float]]:
+    """``model.learn(total_timesteps)`` (OnPolicyAlgorithm.learn): alternate
+    ``collector.collect()`` and ``learner.train()`` until ``total_timesteps``
+    env steps (agents x steps, summed over this rank) were collected, pushing
+    the updated weights into the collector after every update.
+    ``callback(iteration, num_timesteps, stats)`` returning False stops early
+    (SB3 callback semantics).  Returns the per-iteration train stats."""
+    if collector.policy is not learner.policy:
+        raise ValueError("collector and learner must share the policy module")
+    per_rollout = collector.n_steps * collector.N
+    done, it, history = 0, 0, []
+    while done < total_timesteps:
+        buf = collector.collect()
+        done += per_rollout
+        it += 1
+        st = learner.train(buf)
+        collector.sync_weights()
+        st["num_timesteps"] = done
+        history.append(st)
+        if callback is not None and callback(it, done, st) is False:
+            break
+    return history

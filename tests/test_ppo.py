@@ -1,0 +1,157 @@
+"""PPO learner (voxnav.ppo) against the float64
+restatement of sb3_contrib RecurrentPPO.train / SB3 PPO.train in
+oracle/ppo_oracle.py (parity unpinned by the reference: SB3 is absent).
+
+Tolerances: parameters after a train() call within 2e-5 absolute + 1e-4
+relative of the f64 oracle (the learner runs in f32; a few Adam steps of
+lr 3e-4 move parameters by ~1e-3); logged losses within 1e-4 relative.
+"""
+import numpy as np
+import pytest
+
+torch = pytest.importorskip("torch")
+
+from oracle import ppo_oracle as po  # noqa: E402
+
+
+# ------------------------------------------------------------------ sequencers
+def test_create_sequencers_known_answer():
+    # 2 envs x 4 steps, env-major flat order: env0 t0..3, env1 t0..3
+    starts = np.array([0, 0, 1, 0, 0, 1, 0, 0], float)
+    env_change = np.array([1, 0, 0, 0, 1, 0, 0, 0], float)
+    st, en = po.create_sequencers(starts, env_change)
+    assert st.tolist() == [0, 2, 4, 5]
+    assert en.tolist() == [1, 3, 4, 8]
+    padded = po.pad(st, en, np.arange(8, dtype=float))
+    assert padded.tolist() == [[0, 1, 0], [2, 3, 0], [4, 0, 0], [5, 6, 7]]
+    # a minibatch cut mid-sequence starts a sequence at its first row
+    st2, _ = po.create_sequencers(starts[3:], env_change[3:])
+    assert st2.tolist() == [0, 1, 2]
+
+
+def test_swap_and_flatten_is_env_major():
+    a = np.arange(12).reshape(3, 4)          # [T=3, N=4]
+    assert po.swap_and_flatten(a).reshape(-1).tolist() == [0, 4, 8, 1, 5, 9, 2, 6, 10, 3, 7, 11]
+
+
+# ------------------------------------------------------------------ learner
+def _policy(recurrent, seed=0):
+    from voxnav.policy import ActorCriticPolicy, RecurrentActorCriticPolicy
+    torch.manual_seed(seed)
+    arch = dict(pi=[32, 16], vf=[32, 16])
+    if recurrent:
+        return RecurrentActorCriticPolicy(obs_dim=80, lstm_hidden_size=16, net_arch=arch)
+    return ActorCriticPolicy(obs_dim=80, net_arch=arch)
+
+
+def _buffer(T, N, H, recurrent, seed=1):
+    rng = np.random.default_rng(seed)
+    b = dict(
+        obs=rng.random((T, N, 80), dtype=np.float32),
+        actions=rng.integers(0, 6, (T, N)).astype(np.int32),
+        episode_starts=(rng.random((T, N)) < 0.15).astype(np.float32),
+        values=rng.normal(0, 1, (T, N)).astype(np.float32),
+        log_probs=(np.log(1 / 6) + rng.normal(0, 0.15, (T, N))).astype(np.float32),
+        advantages=rng.normal(0, 2, (T, N)).astype(np.float32),
+        returns=rng.normal(0, 2, (T, N)).astype(np.float32),
+    )
+    b["episode_starts"][0, :2] = 1.0
+    if recurrent:
+        b["lstm_h"] = rng.normal(0, 0.3, (T, 2, N, H)).astype(np.float32)
+        b["lstm_c"] = rng.normal(0, 0.3, (T, 2, N, H)).astype(np.float32)
+    return b
+
+
+def _as_rollout(b, device):
+    from voxnav.collector import RolloutBuffer
+    t = {k: torch.as_tensor(v, device=device) for k, v in b.items()}
+    return RolloutBuffer(obs=t["obs"], actions=t["actions"], rewards=torch.zeros_like(t["values"]),
+                         episode_starts=t["episode_starts"], values=t["values"], log_probs=t["log_probs"],
+                         advantages=t["advantages"], returns=t["returns"], lstm_h=t.get("lstm_h"),
+                         lstm_c=t.get("lstm_c"))
+
+
+def _run_parity(device, recurrent, T=12, N=5, batch_size=16, epochs=2):
+    from voxnav.policy import numpy_weights
+    from voxnav.ppo import PPOLearner
+    pol = _policy(recurrent).to(device)
+    w0 = numpy_weights(pol)
+    b = _buffer(T, N, 16, recurrent)
+    rng = np.random.default_rng(7)
+    orders = ([int(rng.integers(T * N)) for _ in range(epochs)] if recurrent
+              else [rng.permutation(T * N) for _ in range(epochs)])
+    ln = PPOLearner(pol, n_epochs=epochs, batch_size=batch_size)
+    st = ln.train(_as_rollout(b, device), epoch_orders=orders)
+    w1, ost, _ = po.train(w0, b, orders, batch_size=batch_size)
+    got = numpy_weights(pol)
+    moved = 0.0
+    for k in w1:
+        np.testing.assert_allclose(got[k], w1[k], atol=2e-5, rtol=1e-4, err_msg=k)
+        moved = max(moved, float(np.abs(w1[k] - w0[k]).max()))
+    assert moved > 1e-4                                 # the update did something
+    n = len(ost)
+    assert st["n_minibatches"] == n == epochs * -(-T * N // batch_size)
+    for key, okey in (("policy_gradient_loss", "policy_loss"), ("value_loss", "value_loss"),
+                      ("entropy_loss", "entropy_loss"), ("approx_kl", "approx_kl"),
+                      ("clip_fraction", "clip_fraction")):
+        ref = np.mean([s[okey] for s in ost])
+        assert abs(st[key] - ref) <= 1e-4 * max(1.0, abs(ref)), (key, st[key], ref)
+    if recurrent:
+        assert sum(s["n_seq"] for s in ost) > n        # sequences were actually split
+
+
+@pytest.mark.parametrize("recurrent", [True, False], ids=["lstm", "mlp"])
+def test_learner_matches_oracle_cpu(recurrent):
+    _run_parity("cpu", recurrent)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("recurrent", [True, False], ids=["lstm", "mlp"])
+def test_learner_matches_oracle_gpu(recurrent):
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    _run_parity("cuda:0", recurrent)
+
+
+def test_learner_batch_larger_than_buffer_and_defaults():
+    from voxnav.ppo import PPOLearner
+    pol = _policy(True)
+    b = _buffer(6, 3, 16, True)
+    ln = PPOLearner(pol, n_epochs=1, batch_size=1000, seed=3)
+    st = ln.train(_as_rollout(b, "cpu"))
+    assert st["n_minibatches"] == 1 and np.isfinite(st["loss"])
+    with pytest.raises(ValueError):
+        PPOLearner(pol, batch_size=0)
+
+
+@pytest.mark.gpu
+def test_learn_loop_end_to_end_gpu(tmp_path):
+    """collect -> train -> sync_weights -> evaluate -> checkpoint on the GPU."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from helpers import product_room_set
+    from voxnav.checkpoint import load_checkpoint, save_checkpoint
+    from voxnav.collector import RolloutCollector
+    from voxnav.env import BatchedGridEnv
+    from voxnav.evaluate import evaluate_policy
+    from voxnav.ppo import PPOLearner, learn
+    pol = _policy(True).to("cuda:0")
+    rooms = product_room_set("set:P2_training")
+    env = BatchedGridEnv(num_agents=256, rooms=rooms, local_map_length=10, device="cuda:0")
+    col = RolloutCollector(env, pol, n_steps=32)
+    ln = PPOLearner(pol, n_epochs=2, batch_size=2048, seed=1)
+    w0 = torch.cat([p.detach().reshape(-1).clone() for p in pol.parameters()])
+    hist = learn(col, ln, total_timesteps=3 * 32 * 256)
+    assert len(hist) == 3 and hist[-1]["num_timesteps"] == 3 * 32 * 256
+    assert all(np.isfinite(h["loss"]) and h["n_minibatches"] == 8 for h in hist)
+    w1 = torch.cat([p.detach().reshape(-1) for p in pol.parameters()])
+    assert float((w1 - w0).abs().max()) > 1e-4
+    # the collector acts with the updated weights
+    assert torch.equal(col.w.pi[0][0], pol.mlp_extractor.policy_net[0].weight.detach())
+    r = evaluate_policy(pol, rooms, n_episodes=8, local_map_length=10, seed=5, max_steps=300)
+    assert len(r["episodes"]) == 8
+    path = save_checkpoint(tmp_path / "m.zip", pol, ln.optimizer, num_timesteps=hist[-1]["num_timesteps"])
+    pol2, data = load_checkpoint(path, device="cuda:0")
+    assert data["num_timesteps"] == 3 * 32 * 256
+    assert torch.equal(torch.cat([p.reshape(-1) for p in pol2.parameters()]), w1)
+    env.close()
