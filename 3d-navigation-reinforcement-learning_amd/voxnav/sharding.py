@@ -77,3 +77,23 @@ def max_over_ranks(value: float, device=None, group=None) -> float:
     t = torch.tensor([value], dtype=torch.float64, device=device)
     dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
     return float(t.item())
+
+
+def reduce_episode_stats(result: Dict[str, object], device=None, group=None) -> Dict[str, object]:
+    """Global evaluation averages from per-rank ``evaluate_policy`` results
+    (episode statistics by a tiny all-reduce): sums of
+    score / bumps / finished / discovered / steps and the episode count are
+    summed over ranks (one 6-float all-reduce) and re-averaged.  The local
+    per-episode list stays as it is."""
+    eps = result["episodes"]
+    t = torch.tensor([sum(e["score"] for e in eps), sum(e["bumps"] for e in eps),
+                      sum(bool(e["finished"]) for e in eps), sum(e["discovered_cells"] for e in eps),
+                      sum(e["steps"] for e in eps), len(eps)], dtype=torch.float64, device=device)
+    if dist.is_available() and dist.is_initialized() and dist.get_world_size(group) > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.SUM, group=group)
+    s = t.tolist()
+    n = max(1.0, s[5])
+    out = dict(result)
+    out.update(avg_score=s[0] / n, avg_bumps=s[1] / n, finished_pct=100.0 * s[2] / n, avg_discovered=s[3] / n,
+               avg_steps=s[4] / n, n_episodes_global=int(s[5]))
+    return out

@@ -67,11 +67,24 @@ def parse():
     ap.add_argument("--collector-rollouts", type=int, default=2, help="timed rollouts of the collector leg")
     ap.add_argument("--collector-bf16", type=int, default=1,
                     help="also time the collector with bf16 policy GEMMs (the reference's policy is f32)")
+    ap.add_argument("--learner-batch", type=int, default=65536,
+                    help="PPO learner leg: minibatch size (0 = skip); runs on the f32 PPO-LSTM collector's buffer")
+    ap.add_argument("--learner-minibatches", type=int, default=16, help="timed learner minibatch updates")
     ap.add_argument("--json-out", default=None)
     return ap.parse_args()
 
 
-def cpu_baseline(room_whd, L, seconds):
+def cpu_model() -> str:
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def cpu_baseline(room_whd, L, seconds, threads_override=None):
     """The CPU oracle (C restatement of envs/CubicEnv.py step/reset) on the
     host cores, same room / L / policy / seed schedule, bounded sample."""
     import numpy as np
@@ -80,6 +93,8 @@ def cpu_baseline(room_whd, L, seconds):
     from voxnav.rooms import box_room, room_to_text
     cores = len(os.sched_getaffinity(0))
     threads = max(1, min(cores, int(os.environ.get("OMP_NUM_THREADS", cores))))
+    if threads_override is not None:
+        threads = int(threads_override)
     N = 512 * threads
     W, D, H = room_whd
     env = OracleEnv([parse_room_text(room_to_text(box_room(W, D, H)))], n_agents=N, local_map_length=L,
@@ -158,6 +173,9 @@ def collector_leg(args, torch, dist, dev, rank, world, N, dtype="f32"):
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el = float(t[0].item())
     assert torch.isfinite(buf.advantages).all().item()
+    learner = None
+    if dtype == "f32" and args.collector == "lstm" and args.learner_batch > 0:
+        learner = learner_leg(args, torch, dist, dev, world, pol, buf)
     steps = args.collector_T * args.collector_rollouts
     fl = lstm_flops_per_agent_step() if args.collector == "lstm" else mlp_flops_per_agent_step()
     tflops = fl * N * steps / el / 1e12
@@ -166,13 +184,52 @@ def collector_leg(args, torch, dist, dev, rank, world, N, dtype="f32"):
     peak = 157.3 if dtype == "f32" else 2500.0     # dense MFMA peak for the GEMM dtype (MI355X_MICROARCH.md)
     env.close()
     del col, env
-    return {"value": round(N * world * steps / el, 1), "unit": "env-steps/s", "policy": name, "dtype": dtype,
+    out = {"value": round(N * world * steps / el, 1), "unit": "env-steps/s", "policy": name, "dtype": dtype,
             "rooms": args.collector_rooms, "agents_per_gpu": N, "rollout_steps": args.collector_T,
             "timed_rollouts": args.collector_rollouts, "ms_per_step": round(el * 1e3 / steps, 4),
             "includes": "policy forward, Categorical draw, env step + auto-reset, truncation bootstrap, "
                         "LSTM-state buffer stores, last values, GAE",
             "policy_flops_per_agent_step": fl, "policy_tflops": round(tflops, 2),
             "policy_frac_of_mfma_peak": round(tflops / peak, 4), "mfma_peak_tflops": peak}
+    if learner is not None:
+        out["learner"] = learner
+    return out
+
+
+def learner_leg(args, torch, dist, dev, world, pol, buf):
+    """PPO learner: sb3_contrib RecurrentPPO.train
+    minibatch updates (packed-sequence LSTM re-run, clipped surrogate, value
+    MSE, entropy, grad clip, Adam; gradient all-reduce over RCCL when N>1)
+    on the collector's buffer.  Timed over a bounded number of minibatches."""
+    from voxnav.ppo import PPOLearner
+    T, N = buf.actions.shape
+    B = min(args.learner_batch, T * N)
+    n = max(1, min(args.learner_minibatches, (T * N) // B))
+    ln = PPOLearner(pol, n_epochs=1, batch_size=B, seed=0,
+                    process_group=dist.group.WORLD if world > 1 else None)
+    perm = torch.roll(torch.arange(T * N, device=dev), -12345 % (T * N))
+    for m in range(2):
+        ln.update(buf, perm[m * B:(m + 1) * B])
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for m in range(n):
+        ln.update(buf, perm[(m % ((T * N) // B)) * B:(m % ((T * N) // B) + 1) * B])
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([el], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t[0].item())
+    sps = n * B * world / el
+    fl = 3 * lstm_flops_per_agent_step()        # forward + backward ~ 3x forward
+    return {"value": round(sps, 1), "unit": "samples/s", "batch_size": B, "minibatches": n,
+            "ms_per_minibatch": round(el * 1e3 / n, 3), "tflops": round(fl * sps / 1e12, 2),
+            "includes": "sequence packing, actor+critic LSTM re-run (MIOpen), MLPs, losses, backward, "
+                        "grad clip, Adam" + (", RCCL gradient all-reduce" if world > 1 else "")}
 
 
 def main():
@@ -306,7 +363,11 @@ def main():
         if coll is not None:
             rec["collector"] = coll               # policy in the loop
         if world == 1 and args.cpu_seconds > 0:
-            rec["cpu_baseline"] = cpu_baseline((W, D, H), args.L, args.cpu_seconds)
+            cb = cpu_baseline((W, D, H), args.L, args.cpu_seconds)
+            one = cpu_baseline((W, D, H), args.L, max(2.0, args.cpu_seconds / 4), threads_override=1)
+            cb["single_core_value"] = one["value"]
+            cb["cpu_model"] = cpu_model()
+            rec["cpu_baseline"] = cb
         line = json.dumps(rec)
         print(line, flush=True)
         if args.json_out:

@@ -52,8 +52,15 @@ def _worker(rank, world, port, q):
         dist.all_gather(g, v)
         spread = float((g[0] - g[1]).abs().max())
         moved = float((v - flat(tp._policy(True, seed=0))).abs().max())
+        # episode statistics: one all-reduce, global averages on every rank
+        from voxnav.sharding import reduce_episode_stats
+        mine = dict(episodes=[dict(score=10.0 * (rank + 1) + i, bumps=rank, finished=(i == 0), discovered_cells=5,
+                                   steps=7 + rank) for i in range(2 + rank)])
+        g_stats = reduce_episode_stats(mine)
+        stats_ok = (g_stats["n_episodes_global"] == 5 and abs(g_stats["avg_score"] - (21 + 63) / 5) < 1e-12
+                    and abs(g_stats["finished_pct"] - 40.0) < 1e-12 and abs(g_stats["avg_steps"] - 38 / 5) < 1e-12)
         if rank == 0:
-            q.put(("ok", same, spread, moved))
+            q.put(("ok" if stats_ok else "stats mismatch", same, spread, moved))
         dist.barrier()
         dist.destroy_process_group()
     except Exception as e:  # noqa: BLE001
