@@ -42,6 +42,13 @@
 
 #include "vn_common.h"
 
+// Diagnostics only: VN_ABLATE bits skip parts of the step (results invalid)
+// in a separately built library (scripts/ab.py); 0 in the product.  A
+// compile-time constant, so the product kernels carry no branch for it.
+#ifndef VN_ABLATE
+#define VN_ABLATE 0u
+#endif
+
 namespace {
 
 using vn_detail::fail;
@@ -123,7 +130,7 @@ struct Params {
     uint8_t *term, *trunc;
     const int64_t *seeds;    // reset-only launches
     const uint8_t *mask;
-    uint32_t ablate;         // diagnostics only (VOXNAV_ABLATE): skip parts of the step, results invalid
+    uint32_t ablate;         // unused (ablations are the compile-time VN_ABLATE)
     // simpleEnv variant
     int variant, obs_dim, pd;
     uint32_t *goal;          // per agent gx | gy<<8 | gz<<16
@@ -685,14 +692,16 @@ __device__ __forceinline__ void tile_shift_issue(const Params &p, int8_t *map, c
         sl.entering = 0x1111u << (ey & 3);
     }
     sl.s = tslot(ex, ey);
-    if (!(p.ablate & 8u) && ((dirty >> sl.s) & 1u) && lx >= 0 && lx < R.W && ly >= 0 && ly < R.D) {
+    // the load first: vmcnt retires in issue order, so a store issued ahead
+    // of it would hold its data until the store completes
+    col_zero<PH>(sl.c);
+    if (!(VN_ABLATE & 1u) && ex >= 0 && ex < R.W && ey >= 0 && ey < R.D)
+        col_load<PH>(map + boff<PH>(ex, ey, 0, p.nby), sl.c);
+    if (!(VN_ABLATE & 8u) && ((dirty >> sl.s) & 1u) && lx >= 0 && lx < R.W && ly >= 0 && ly < R.D) {
         Col<PH> old;
         tile_read<PH>(tile, sl.s, old);
         col_store<PH>(map + boff<PH>(lx, ly, 0, p.nby), old);
     }
-    col_zero<PH>(sl.c);
-    if (!(p.ablate & 1u) && ex >= 0 && ex < R.W && ey >= 0 && ey < R.D)
-        col_load<PH>(map + boff<PH>(ex, ey, 0, p.nby), sl.c);
 }
 
 template <int PH>
@@ -711,7 +720,7 @@ __device__ __forceinline__ void plane_prefetch(const Params &p, const int8_t *ma
     if (q < 2) {
         const bool xr = q == 0;
         const int nw = xr ? p.nwx : p.nwy;
-        if (nw <= 2 && !(p.ablate & 2u)) {
+        if (nw <= 2 && !(VN_ABLATE & 2u)) {
             const int rowi = (xr ? y : x) * PH + z;
             if (pc_.row != rowi) {
                 const uint64_t *prow =
@@ -877,7 +886,7 @@ __device__ __forceinline__ int sense_observe(const Params &p, int8_t *map, uint6
                 const uint64_t nv = pn[w] | pm[w];
                 if (pofs + w == 0) pc_.w[0] = nv;
                 else if (pofs + w == 1) pc_.w[1] = nv;
-                if (!(p.ablate & 32u)) prow[pw0 + w] = nv;
+                if (!(VN_ABLATE & 32u)) prow[pw0 + w] = nv;
             }
         }
         const int sh = pa - pw0 * 64;      // 0..63
@@ -892,8 +901,8 @@ __device__ __forceinline__ int sense_observe(const Params &p, int8_t *map, uint6
         const uint32_t ryh = (uint32_t)__shfl((int)(uint32_t)(rel >> 32), 1, GROUP);
         const int pax = __shfl(pa, 0, GROUP), pay = __shfl(pa, 1, GROUP);
         const uint64_t lane_sel = 0x1111111111111111ull << q;
-        uint64_t mx = (p.ablate & 32u) ? 0ull : (((uint64_t)rxh << 32) | rxl) & lane_sel;
-        uint64_t my = (p.ablate & 32u) ? 0ull : (((uint64_t)ryh << 32) | ryl) & lane_sel;
+        uint64_t mx = (VN_ABLATE & 32u) ? 0ull : (((uint64_t)rxh << 32) | rxl) & lane_sel;
+        uint64_t my = (VN_ABLATE & 32u) ? 0ull : (((uint64_t)ryh << 32) | ryl) & lane_sel;
         while (mx) {
             const int pos = pax + __ffsll((unsigned long long)mx) - 1;
             mx &= mx - 1;
@@ -918,8 +927,8 @@ __device__ __forceinline__ int sense_observe(const Params &p, int8_t *map, uint6
     // two single-address-space destinations (an LDS/global select would
     // compile to flat stores, which occupy the vector-memory path even for LDS)
     const bool to_term = dst.select && (dst.truncated || g.done || g.visited >= R.finish_visits);
-    float4 *lds4 = (!to_term && dst.stage && !(p.ablate & 4u)) ? reinterpret_cast<float4 *>(dst.stage) : nullptr;
-    float4 *glb4 = (p.ablate & 4u) ? nullptr
+    float4 *lds4 = (!to_term && dst.stage && !(VN_ABLATE & 4u)) ? reinterpret_cast<float4 *>(dst.stage) : nullptr;
+    float4 *glb4 = (VN_ABLATE & 4u) ? nullptr
                    : to_term       ? reinterpret_cast<float4 *>(dst.term_row)
                    : dst.stage     ? nullptr
                                    : reinterpret_cast<float4 *>(dst.row);
@@ -1060,7 +1069,13 @@ __device__ __forceinline__ void group_reset(const Params &p, int8_t *map, uint64
 constexpr int BLOCK = 256;
 constexpr int AGENTS_PER_BLOCK = BLOCK / GROUP;
 
-template <int PH, int LMAX, bool RESET_ONLY>
+// EXT: actions come from p.actions (else the Philox random policy).  A
+// separate instantiation: with both sources in one loop the action register
+// may hold a pending load on entry to every step, and the compiler then waits
+// for all outstanding stores of the previous step before the move is known.
+// FAST: reward / terminated / truncated requested, reward64 / actions_out
+// not (the rollout-buffer call): no runtime pointer tests in the step loop.
+template <int PH, bool EXT, bool FAST, bool RESET_ONLY>
 #ifndef VN_MIN_WAVES_PER_SIMD
 #define VN_MIN_WAVES_PER_SIMD 4   // <= 128 VGPRs: the 16 waves of 256 agents per CU resident at once
 #endif
@@ -1114,7 +1129,7 @@ __global__ __launch_bounds__(BLOCK, VN_MIN_WAVES_PER_SIMD) void env_kernel(Param
     for (int k = 0; k < p.K;) {
     const uint64_t tb = p.t0 + (uint64_t)k;
     uint32_t acts = 0;                                    // 4 actions, 8 bits each, by (t & 3)
-    if (!p.actions) {
+    if (!EXT) {
         const uint4 o = philox4x32_10(p.policy_seed, p.gid_base + (uint64_t)ai, tb >> 2);
         acts = __umulhi(o.x, 6u) | (__umulhi(o.y, 6u) << 8) | (__umulhi(o.z, 6u) << 16) | (__umulhi(o.w, 6u) << 24);
     }
@@ -1124,8 +1139,8 @@ __global__ __launch_bounds__(BLOCK, VN_MIN_WAVES_PER_SIMD) void env_kernel(Param
         const size_t row = (size_t)k * (size_t)p.N + (size_t)i;
         const uint64_t tt = tb + (uint64_t)j;
         if (active) {
-            const int a = p.actions ? p.actions[row] : (int)((acts >> (8 * (uint32_t)(tt & 3u))) & 0xffu);
-            if (p.actions_out && q == 0) p.actions_out[row] = a;
+            const int a = EXT ? p.actions[row] : (int)((acts >> (8 * (uint32_t)(tt & 3u))) & 0xffu);
+            if (!FAST && p.actions_out && q == 0) p.actions_out[row] = a;
 
             // step() prologue (:111-116)
             if (g.near_wall) {
@@ -1195,10 +1210,10 @@ __global__ __launch_bounds__(BLOCK, VN_MIN_WAVES_PER_SIMD) void env_kernel(Param
             g.last_action = a;
 
             if (q == 0) {
-                if (p.reward) p.reward[row] = (float)r;
-                if (p.reward64) p.reward64[row] = r;
-                if (p.term) p.term[row] = g.done ? 1 : 0;
-                if (p.trunc) p.trunc[row] = truncated ? 1 : 0;
+                if (FAST || p.reward) p.reward[row] = (float)r;
+                if (!FAST && p.reward64) p.reward64[row] = r;
+                if (FAST || p.term) p.term[row] = g.done ? 1 : 0;
+                if (FAST || p.trunc) p.trunc[row] = truncated ? 1 : 0;
             }
             finished = g.done || truncated;
         }
@@ -1210,7 +1225,7 @@ __global__ __launch_bounds__(BLOCK, VN_MIN_WAVES_PER_SIMD) void env_kernel(Param
             if (need) next_seed = seed + p.seed_stride;
         }
         // flush the wave's 16 staged obs rows: contiguous in [K][N][80]
-        if (VN_STAGE_OBS && !(p.ablate & 16u)) {
+        if (VN_STAGE_OBS && !(VN_ABLATE & 16u)) {
             const int lane = threadIdx.x & 63;
             const int wave_agent0 = (int)((blockIdx.x * blockDim.x + (threadIdx.x & ~63)) / GROUP);
             const float4 *ws = stage + (size_t)((threadIdx.x & ~63) / GROUP) * (VN_OBS_DIM / 4);
@@ -1697,7 +1712,7 @@ __global__ __launch_bounds__(64) void simple_bits_kernel(Params p) {
         if (live) {
             if (p.actions) {
                 a = p.actions[(size_t)k * p.N + ai];
-            } else if (p.ablate & 32u) {
+            } else if (VN_ABLATE & 32u) {
                 a = (int)((ai + (int)t * 7) % 6);
             } else {
                 if (k == 0 || (t & 3) == 0) r4 = philox4x32_10(p.policy_seed, p.gid_base + (uint64_t)ai, t >> 2);
@@ -1748,7 +1763,7 @@ __global__ __launch_bounds__(64) void simple_bits_kernel(Params p) {
             }
             g.last_action = a;                                           // :137
             SB_T(1);
-            if (!(p.ablate & 4u)) sb_observe<LMAX>(p, pl, g, w, row);    // :139
+            if (!(VN_ABLATE & 4u)) sb_observe<LMAX>(p, pl, g, w, row);    // :139
             SB_T(2);
             // compute_reward (:189-217), f64 in the reference's order
             r = -0.1;
@@ -1766,7 +1781,7 @@ __global__ __launch_bounds__(64) void simple_bits_kernel(Params p) {
             if (explored) r += 1.0;
             term = g.done;
             const size_t o = (size_t)k * p.N + ai;
-            if (p.reward && !(p.ablate & 8u)) p.reward[o] = (float)r;
+            if (p.reward && !(VN_ABLATE & 8u)) p.reward[o] = (float)r;
             if (p.reward64) p.reward64[o] = r;
             if (p.term) p.term[o] = term;
             if (p.trunc) p.trunc[o] = trunc;
@@ -1789,7 +1804,7 @@ __global__ __launch_bounds__(64) void simple_bits_kernel(Params p) {
         SB_T(4);
         __syncthreads();
         float *dst = p.obs + ((size_t)k * p.N + a0) * OD;
-        if (p.ablate & 16u) {
+        if (VN_ABLATE & 16u) {
         } else if (rows == 64 && !(reinterpret_cast<uintptr_t>(dst) & 15u)) {   // 64 rows = 16 * OD float4s
             const float4 *s4 = reinterpret_cast<const float4 *>(sstage);
             float4 *d4 = reinterpret_cast<float4 *>(dst);
@@ -2015,15 +2030,18 @@ Params base_params(VnEnv *e) {
 }
 
 template <int PH, bool RESET_ONLY>
-int launch_ph(int L, dim3 grid, dim3 block, hipStream_t s, const Params &p) {
-    if (L <= 4)
-        hipLaunchKernelGGL((env_kernel<PH, 4, RESET_ONLY>), grid, block, 0, s, p);
-    else if (L <= 8)
-        hipLaunchKernelGGL((env_kernel<PH, 8, RESET_ONLY>), grid, block, 0, s, p);
-    else if (L <= 10)
-        hipLaunchKernelGGL((env_kernel<PH, 10, RESET_ONLY>), grid, block, 0, s, p);
+int launch_ph(int /*L*/, dim3 grid, dim3 block, hipStream_t s, const Params &p) {
+    const bool fast = p.reward && p.term && p.trunc && !p.reward64 && !p.actions_out;
+    if (RESET_ONLY)
+        hipLaunchKernelGGL((env_kernel<PH, false, false, true>), grid, block, 0, s, p);
+    else if (p.actions && fast)
+        hipLaunchKernelGGL((env_kernel<PH, true, true, false>), grid, block, 0, s, p);
+    else if (p.actions)
+        hipLaunchKernelGGL((env_kernel<PH, true, false, false>), grid, block, 0, s, p);
+    else if (fast)
+        hipLaunchKernelGGL((env_kernel<PH, false, true, false>), grid, block, 0, s, p);
     else
-        hipLaunchKernelGGL((env_kernel<PH, 16, RESET_ONLY>), grid, block, 0, s, p);
+        hipLaunchKernelGGL((env_kernel<PH, false, false, false>), grid, block, 0, s, p);
     VN_HIP(hipGetLastError());
     return VN_OK;
 }
@@ -2197,7 +2215,6 @@ int vn_create(const VnRoomSet *rooms, int32_t n_agents, const VnConfig *cfg, int
     // agent's room (bits: 1 entering-column loads, 2 plane rows and blind marks,
     // 4 obs rows, 8 column write-backs, 16 obs flush to HBM, 32 plane word writes
     // and blind marks; 2 skips the plane row loads)
-    if (const char *ab = getenv("VOXNAV_ABLATE")) e->ablate = (uint32_t)strtoul(ab, nullptr, 0) & 0x3fu;
     e->variant = cfg->variant;
     e->obs_dim = cfg->variant == VN_VARIANT_SIMPLE ? 6 * cfg->local_map_length + 7 : VN_OBS_DIM;
     e->nbx = (maxW + 3) / 4;

@@ -1,6 +1,10 @@
 #!/usr/bin/env python3
 """Interleaved A/B timing of library variants in ONE process (same device,
-same state), e.g.  python scripts/ab.py --variants base:path.so,lb4:other.so"""
+same state), e.g.  python scripts/ab.py --variants base:path.so,lb4:other.so
+
+Ablation variants (VN_ABLATE bits, diagnostics only) are separate builds:
+  python -c "import voxnav._build as b; b.build_variant('noobs', ['VN_ABLATE=16u'])"
+(run with 3d-navigation-reinforcement-learning_amd on sys.path)."""
 import argparse
 import os
 import json
@@ -24,11 +28,9 @@ def main():
     ap.add_argument("--steps", type=int, default=256)
     ap.add_argument("--rounds", type=int, default=5)
     a = ap.parse_args()
-    libs, ablate = {}, {}
+    libs = {}
     for v in a.variants.split(","):
-        parts = v.split(":")
-        name, path = parts[0], parts[1]
-        ablate[name] = parts[2] if len(parts) > 2 else "0"     # VOXNAV_ABLATE bits (diagnostics)
+        name, path = v.split(":")[:2]
         libs[name] = _native.load_variant(REPO / path if not path.startswith("/") else path)
     cfgs = [c.split(":") for c in a.configs.split(",")]
     # One env alive at a time, created and destroyed per measurement, so every
@@ -47,7 +49,6 @@ def main():
             rs = load_archive_set(room) if room.startswith("P") else single_room_set(box_room(*map(int, room.split("x"))))
             names = list(libs) if r % 2 == 0 else list(libs)[::-1]
             for name in names:
-                os.environ["VOXNAV_ABLATE"] = ablate[name]
                 e = BatchedGridEnv(num_agents=n, rooms=rs, local_map_length=L, autoreset=True, device="cuda:0",
                                    lib=libs[name])
                 e.reset(seed=42)

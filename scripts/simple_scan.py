@@ -25,7 +25,7 @@ def main():
     ap.add_argument("--steps", type=int, default=512)
     ap.add_argument("--autoreset", default="1", help="comma list of 0/1")
     ap.add_argument("--lib", default=None, help="another build of the library (e.g. -DVN_SIMPLE_PROF=1)")
-    ap.add_argument("--ablate", default="0", help="VOXNAV_ABLATE values to scan (diagnostics; results invalid)")
+    ap.add_argument("--ablate", default="0", help="ignored: ablations are compile-time VN_ABLATE builds (see scripts/ab.py)")
     a = ap.parse_args()
     lib = raw = None
     if a.lib:

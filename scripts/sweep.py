@@ -18,7 +18,7 @@ from voxnav.rooms import box_room, load_archive_set, single_room_set  # noqa: E4
 
 def make(n, room, L, ablate=0):
     import os
-    os.environ["VOXNAV_ABLATE"] = str(ablate)
+    os.environ["VOXNAV_ABLATE"] = str(ablate)   # no effect: ablations are compile-time VN_ABLATE builds
     rs = load_archive_set(room) if room.startswith("P") else single_room_set(box_room(*map(int, room.split("x"))))
     e = BatchedGridEnv(num_agents=n, rooms=rs, local_map_length=L, autoreset=True, device="cuda:0")
     e.reset(seed=42)

@@ -121,6 +121,45 @@ def test_random_rollout_matches_oracle(voxnav, src, L, N, K):
     assert bad.size == 0, f"obs mismatch at (step, agent) {bad[:5].tolist()}"
 
 
+FAST_CASES = [("ctor:32x32x8", 10, 1024, 160), ("set:P3_training", 10, 1000, 120), ("box:8x8x4", 4, 333, 200)]
+
+
+@pytest.mark.parametrize("src,L,N,K", FAST_CASES, ids=[f"{c[0]}-N{c[2]}" for c in FAST_CASES])
+def test_rollout_buffer_call_matches_oracle(voxnav, src, L, N, K):
+    """The rollout-buffer call (f32 reward, flags, no action record / f64
+    reward) runs its own kernel instantiation: bit-exact against the oracle,
+    including agent counts that leave a partly filled wave (N % 16 != 0)."""
+    env = make_env(voxnav, src, L, n=N, autoreset=True)
+    env.reset(seed=42)
+    ro = env.step_random(K, policy_seed=7, t0=0)
+    orc = oracle_env(src, L, n_agents=N).run_random(42 + np.arange(N, dtype=np.int64), policy_seed=7, K=K,
+                                                    seed_stride=N)
+    np.testing.assert_array_equal(ro.terminated.cpu().numpy(), orc["terminated"])
+    np.testing.assert_array_equal(ro.truncated.cpu().numpy(), orc["truncated"])
+    np.testing.assert_array_equal(ro.reward.cpu().numpy(), orc["reward"].astype(np.float32))
+    assert ro.obs.cpu().numpy().tobytes() == orc["obs"].tobytes()
+
+
+def test_step_with_actions_f32_matches_oracle(voxnav):
+    """vn_step with explicit actions, f32 reward, terminal_obs (the collector's call)."""
+    src, L, N, K = "box:8x8x4", 4, 400, 100
+    env = make_env(voxnav, src, L, n=N, autoreset=True)
+    env.reset(seed=1000)
+    acts = np.random.default_rng(5).integers(0, 6, size=(K, N)).astype(np.int32)
+    orc = oracle_env(src, L, n_agents=N).run_random(1000 + np.arange(N), policy_seed=0, K=K, seed_stride=N,
+                                                    actions=acts, terminal_obs=True)
+    at = torch.as_tensor(acts, device="cuda:0")
+    for k in range(K):
+        res = env.step(at[k], reward_f64=False, terminal_obs=True)
+        np.testing.assert_array_equal(res.obs.cpu().numpy(), orc["obs"][k])
+        np.testing.assert_array_equal(res.reward.cpu().numpy(), orc["reward"][k].astype(np.float32))
+        te, tr = res.terminated.cpu().numpy(), res.truncated.cpu().numpy()
+        np.testing.assert_array_equal(te, orc["terminated"][k].astype(bool))
+        np.testing.assert_array_equal(tr, orc["truncated"][k].astype(bool))
+        done = te | tr
+        np.testing.assert_array_equal(res.terminal_obs.cpu().numpy()[done], orc["terminal_obs"][k][done])
+
+
 def test_step_with_actions_autoreset_terminal_obs(voxnav):
     """vn_step with explicit actions: obs/terminal_obs/flags vs oracle (SB3 semantics)."""
     src, L, N, K = "box:8x8x4", 4, 384, 160
