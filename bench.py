@@ -173,6 +173,9 @@ def collector_leg(args, torch, dist, dev, rank, world, N, dtype="f32"):
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el = float(t[0].item())
     assert torch.isfinite(buf.advantages).all().item()
+    gather = None
+    if world > 1 and dtype == "f32" and dist.get_backend() == "nccl":   # not under the gloo rehearsal knob
+        gather = allgather_leg(torch, dist, dev, rank, world, buf)
     learner = None
     if dtype == "f32" and args.collector == "lstm" and args.learner_batch > 0:
         learner = learner_leg(args, torch, dist, dev, world, pol, buf)
@@ -193,7 +196,55 @@ def collector_leg(args, torch, dist, dev, rank, world, N, dtype="f32"):
             "policy_frac_of_mfma_peak": round(tflops / peak, 4), "mfma_peak_tflops": peak}
     if learner is not None:
         out["learner"] = learner
+    if gather is not None:
+        out["trajectory_allgather"] = gather
     return out
+
+
+def allgather_leg(torch, dist, dev, rank, world, buf, reps=3):
+    """the one exchange of the path -- the rollout's
+    trajectory buffers all-gathered over RCCL (xGMI) at the rollout boundary
+    (obs, actions, rewards, episode starts, values, log-probs, advantages,
+    returns, and the LSTM states at the rollout's first step).  Timed
+    max-over-ranks; bus bandwidth = algorithm bytes x (world-1)/world."""
+    from voxnav.sharding import allgather_rollout
+    bufs = {"obs": buf.obs, "actions": buf.actions, "rewards": buf.rewards, "episode_starts": buf.episode_starts,
+            "values": buf.values, "log_probs": buf.log_probs, "advantages": buf.advantages,
+            "returns": buf.returns}
+    if buf.lstm_h is not None:
+        bufs["lstm_h0"] = buf.lstm_h[:1]
+        bufs["lstm_c0"] = buf.lstm_c[:1]
+    dims = {k: (2 if k.startswith("lstm") else 1) for k in bufs}
+    local_bytes = sum(t.numel() * t.element_size() for t in bufs.values())
+    got = None
+    times = []
+    sync = (lambda: torch.cuda.synchronize(dev)) if dev.type == "cuda" else (lambda: None)
+    for _ in range(reps):
+        dist.barrier()
+        sync()
+        t0 = time.perf_counter()
+        got = {}
+        for k, t in bufs.items():
+            got.update(allgather_rollout({k: t}, agent_dim=dims[k]))
+        sync()
+        el = time.perf_counter() - t0
+        tt = torch.tensor([el], dtype=torch.float64, device=dev)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        times.append(float(tt.item()))
+        if _ < reps - 1:
+            del got
+    # this rank's slice of the gathered buffers is its own data
+    n = buf.rewards.shape[1]
+    assert torch.equal(got["rewards"][:, rank * n:(rank + 1) * n], buf.rewards)
+    assert torch.equal(got["obs"][:, rank * n:(rank + 1) * n], buf.obs)
+    if buf.lstm_h is not None:
+        assert torch.equal(got["lstm_h0"][:, :, rank * n:(rank + 1) * n], buf.lstm_h[:1])
+    del got
+    el = min(times)
+    total = local_bytes * world
+    return {"bytes_per_rank": local_bytes, "gathered_bytes": total, "seconds": round(el, 5),
+            "algbw_GBps": round(total / el / 1e9, 2), "busbw_GBps": round(total * (world - 1) / world / el / 1e9, 2),
+            "collective": "all_gather_into_tensor per buffer (RCCL over xGMI)", "reps": reps}
 
 
 def learner_leg(args, torch, dist, dev, world, pol, buf):

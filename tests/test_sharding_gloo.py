@@ -78,3 +78,47 @@ def test_two_rank_shards_equal_single_run():
     assert results, "no result from rank 0"
     assert all(r[0] != "error" for r in results), results
     assert results[0][0] == "ok", results
+
+
+def _bench_gather_worker(rank, world, port, q):
+    try:
+        sys.path.insert(0, str(REPO))
+        sys.path.insert(0, str(REPO / "3d-navigation-reinforcement-learning_amd"))
+        import torch
+        import torch.distributed as dist
+        import bench
+        from voxnav.collector import RolloutBuffer
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        T, n, H = 5, 7, 4
+        g = torch.Generator().manual_seed(rank)
+        f = lambda *s: torch.randn(*s, generator=g)  # noqa: E731
+        buf = RolloutBuffer(obs=f(T, n, 80), actions=torch.randint(0, 6, (T, n), generator=g, dtype=torch.int32),
+                            rewards=f(T, n), episode_starts=f(T, n), values=f(T, n), log_probs=f(T, n),
+                            advantages=f(T, n), returns=f(T, n), lstm_h=f(T, 2, n, H), lstm_c=f(T, 2, n, H))
+        out = bench.allgather_leg(torch, dist, torch.device("cpu"), rank, world, buf, reps=2)
+        per_rank = (T * n * (80 + 7) + 2 * 2 * n * H) * 4
+        ok = out["bytes_per_rank"] == per_rank and out["gathered_bytes"] == world * per_rank
+        q.put(("ok" if ok else f"bad {out}", rank))
+        dist.barrier()
+        dist.destroy_process_group()
+    except Exception as e:  # noqa: BLE001
+        q.put(("error", repr(e)))
+
+
+def test_bench_trajectory_allgather_leg_two_ranks():
+    """bench.py's N>1 trajectory all-gather leg (RCCL on the GPU node): the
+    same code over gloo on CPU tensors; each rank checks its own slice."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_bench_gather_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=180)
+    results = [q.get(timeout=5) for _ in range(2)]
+    for p in procs:
+        if p.is_alive():
+            p.kill()
+    assert all(r[0] == "ok" for r in results), results
