@@ -1,0 +1,131 @@
+"""The PPO learner's LSTM re-run on the GPU, forward and backward.
+
+sb3_contrib ``RecurrentPPO.train`` re-runs the actor and the critic LSTM of
+``RecurrentActorCriticPolicy`` over each minibatch's sequences
+(``evaluate_actions`` -> ``_process_sequence``; reached from ``model.learn``
+at train/Grid_Train.py:228) and back-propagates through them.  Here both
+LSTMs run together over the padded ``[L, B]`` batch:
+
+forward   ``gx = X @ [W_ih_actor | W_ih_critic]^T`` for all steps (one GEMM);
+          per step ``h_{t-1} @ W_hh^T`` for both LSTMs (one batched GEMM)
+          and ``vn_lstm_seq_fwd_cell`` (gates, cell, h; the activations are
+          kept for the backward pass);
+backward  per step, in reverse, ``vn_lstm_seq_bwd_cell`` (gate gradients
+          dG_t, dc_{t-1}) and ``dh_{t-1} = dG_t @ W_hh`` (batched); then the
+          weight gradients over all steps at once: ``dW_hh = dG^T H_prev``
+          (batched), ``dW_ih = dG^T X``, ``db = sum dG``.
+
+The GEMMs are library GEMMs (hipBLASLt through torch), f32 -- the
+reference's dtype; the per-step cell kernels are csrc/voxnav_learn.hip.
+Padded steps sit after each sequence's real steps and get zero output
+gradient from the masked losses, so they never influence the real ones --
+the same result as sb3's per-step masked loop (a sequence only begins with
+an episode start or the minibatch's first step of an env).
+
+There is no fallback for CUDA tensors: the HIP library must be loaded.
+CPU tensors (the CPU parity tests) run torch's own ``nn.LSTM``.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from typing import Tuple
+
+import torch
+
+from . import _native
+
+
+def _p(t: torch.Tensor):
+    return C.c_void_p(t.data_ptr())
+
+
+def _stream(dev):
+    return C.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
+
+
+class _DualLSTM(torch.autograd.Function):
+    """Actor and critic LSTM (one layer each, same input) over [L, B, D]."""
+
+    @staticmethod
+    def forward(ctx, x, h0, c0, w_ih_a, w_hh_a, b_ih_a, b_hh_a, w_ih_c, w_hh_c, b_ih_c, b_hh_c):
+        lib = _native.load()
+        L, B, D = x.shape
+        H = w_hh_a.shape[1]
+        G = 4 * H
+        dev = x.device
+        st = _stream(dev)
+        xf = x.reshape(L * B, D).contiguous()
+        w_ih = torch.cat([w_ih_a, w_ih_c], 0)                       # [2*4H, D]
+        w_hh = torch.stack([w_hh_a, w_hh_c]).contiguous()          # [2, 4H, H]
+        bias = torch.stack([b_ih_a + b_hh_a, b_ih_c + b_hh_c]).contiguous()
+        gx = xf @ w_ih.t()                                          # [L*B, 2*4H]
+        hs = torch.empty((2, L + 1, B, H), dtype=torch.float32, device=dev)
+        cs = torch.empty_like(hs)
+        hs[:, 0] = h0
+        cs[:, 0] = c0
+        act = torch.empty((L, 2, B, G), dtype=torch.float32, device=dev)   # step-major: act[t] contiguous
+        w_hh_t = w_hh.transpose(1, 2)
+        s_state = (L + 1) * B * H
+        row_bytes = B * 2 * G * 4
+        gx_base = gx.data_ptr()
+        hs_base, cs_base = hs.data_ptr(), cs.data_ptr()
+        for t in range(L):
+            torch.bmm(hs[:, t], w_hh_t, out=act[t])
+            _native.check(lib.vn_lstm_seq_fwd_cell(
+                C.c_void_p(gx_base + t * row_bytes), 2 * G, G, _p(act[t]), B * G, _p(bias),
+                C.c_void_p(cs_base + t * B * H * 4), C.c_void_p(cs_base + (t + 1) * B * H * 4),
+                C.c_void_p(hs_base + (t + 1) * B * H * 4), s_state, 2, B, H, st), "vn_lstm_seq_fwd_cell")
+        ctx.save_for_backward(xf, w_ih_a, w_ih_c, w_hh, hs, cs, act)
+        ctx.dims = (L, B, D, H)
+        return hs[:, 1:]
+
+    @staticmethod
+    def backward(ctx, d_out):
+        lib = _native.load()
+        xf, w_ih_a, w_ih_c, w_hh, hs, cs, act = ctx.saved_tensors
+        L, B, D, H = ctx.dims
+        G = 4 * H
+        dev = xf.device
+        st = _stream(dev)
+        dh_out = d_out.contiguous()                                 # [2, L, B, H]
+        dG = torch.empty((2, L, B, G), dtype=torch.float32, device=dev)
+        dc = torch.zeros((2, B, H), dtype=torch.float32, device=dev)
+        dh = torch.empty((2, B, H), dtype=torch.float32, device=dev)
+        s_state = (L + 1) * B * H
+        cs_base, dG_base, do_base = cs.data_ptr(), dG.data_ptr(), dh_out.data_ptr()
+        need_h0 = ctx.needs_input_grad[1]
+        for t in range(L - 1, -1, -1):
+            _native.check(lib.vn_lstm_seq_bwd_cell(
+                C.c_void_p(do_base + t * B * H * 4), L * B * H, _p(dh) if t < L - 1 else None, _p(dc),
+                _p(act[t]), B * G, C.c_void_p(cs_base + t * B * H * 4), C.c_void_p(cs_base + (t + 1) * B * H * 4),
+                s_state, C.c_void_p(dG_base + t * B * G * 4), L * B * G, 2, B, H, st), "vn_lstm_seq_bwd_cell")
+            if t > 0 or need_h0:
+                torch.bmm(dG[:, t], w_hh, out=dh)                   # dh_{t-1} = dG_t @ W_hh
+        dGf = dG.view(2, L * B, G)
+        d_w_hh = torch.bmm(dGf.transpose(1, 2), hs[:, :L].reshape(2, L * B, H))
+        d_w_ih_a = dGf[0].t() @ xf
+        d_w_ih_c = dGf[1].t() @ xf
+        db = dGf.sum(1)
+        dx = None
+        if ctx.needs_input_grad[0]:
+            dx = (dGf[0] @ w_ih_a + dGf[1] @ w_ih_c).view(L, B, D)
+        dh0 = dh.clone() if need_h0 else None
+        dc0 = dc.clone() if ctx.needs_input_grad[2] else None
+        return dx, dh0, dc0, d_w_ih_a, d_w_hh[0], db[0], db[0], d_w_ih_c, d_w_hh[1], db[1], db[1]
+
+
+def dual_lstm(policy, x: torch.Tensor, h0: torch.Tensor, c0: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
+    """(out_actor, out_critic), each [L, B, H], of ``policy.lstm_actor`` and
+    ``policy.lstm_critic`` over x [L, B, D] from states h0, c0 [2, B, H]
+    (actor, critic) -- ``nn.LSTM`` semantics, differentiable w.r.t. the
+    LSTM parameters."""
+    la, lc = policy.lstm_actor, policy.lstm_critic
+    if x.device.type != "cuda":
+        out_pi, _ = la(x, (h0[0:1].contiguous(), c0[0:1].contiguous()))
+        out_vf, _ = lc(x, (h0[1:2].contiguous(), c0[1:2].contiguous()))
+        return out_pi, out_vf
+    if la.num_layers != 1 or lc.num_layers != 1 or la.bidirectional or lc.bidirectional or not la.bias:
+        raise ValueError("dual_lstm supports one-layer unidirectional LSTMs with biases")
+    out = _DualLSTM.apply(x, h0, c0, la.weight_ih_l0, la.weight_hh_l0, la.bias_ih_l0, la.bias_hh_l0,
+                          lc.weight_ih_l0, lc.weight_hh_l0, lc.bias_ih_l0, lc.bias_hh_l0)
+    return out[0], out[1]

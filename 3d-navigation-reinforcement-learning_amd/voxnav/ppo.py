@@ -19,9 +19,11 @@ normalize_advantage True, Adam eps 1e-5):
 
 Everything stays on the device: minibatch rows are gathered straight from
 the collector's ``[T, N]``-major buffers by index arithmetic (no flattened
-copies), sequences are packed with one scatter, and each LSTM runs as one
-``nn.LSTM`` call over the padded batch (MIOpen), which equals sb3's masked
-per-step loop because a sequence can only begin with an episode start.
+copies), sequences are packed with one scatter, and both LSTMs run together
+over the padded batch (``voxnav.lstm_seq.dual_lstm``: library GEMMs and the
+per-step cell kernels of csrc/voxnav_learn.hip, forward and backward),
+which equals sb3's masked per-step loop because a sequence can only begin
+with an episode start.
 The one host round-trip per recurrent minibatch is the (n_seq, max_len)
 pair that sizes the padded tensor.
 
@@ -41,6 +43,7 @@ import numpy as np
 import torch
 import torch.nn.functional as Fn
 
+from .lstm_seq import dual_lstm
 from .policy import ActorCriticPolicy, RecurrentActorCriticPolicy
 
 
@@ -116,9 +119,7 @@ class PPOLearner:
         tf, ef = t[first], env[first]
         h0 = buf.lstm_h[tf, :, ef].permute(1, 0, 2) * keep        # stored states [T, 2, N, H] -> [2, n_seq, H]
         c0 = buf.lstm_c[tf, :, ef].permute(1, 0, 2) * keep
-        pol = self.policy
-        out_pi, _ = pol.lstm_actor(x, (h0[0:1].contiguous(), c0[0:1].contiguous()))
-        out_vf, _ = pol.lstm_critic(x, (h0[1:2].contiguous(), c0[1:2].contiguous()))
+        out_pi, out_vf = dual_lstm(self.policy, x, h0, c0)
         lat_pi = out_pi[pos, seq_id]
         lat_vf = out_vf[pos, seq_id]
         acts = buf.actions.reshape(-1)[src].long()

@@ -253,6 +253,43 @@ int vn_collect_bootstrap(const int32_t *boot_idx, const float *terminal_values, 
 int vn_episode_start(const uint8_t *terminated, const uint8_t *truncated, int32_t N, float *episode_starts,
                      float *h, float *c, uint16_t *h_bf16, int32_t n_lstm, int32_t H, void *stream);
 
+/* ------------------------------------------------------------------------
+ * PPO learner: the LSTM re-run of sb3_contrib RecurrentPPO.train
+ * (RecurrentActorCriticPolicy.evaluate_actions -> _process_sequence, from
+ * model.learn at train/Grid_Train.py:228) and its backward pass.  The
+ * GEMMs are library GEMMs issued by the caller; these are the per-step
+ * cell kernels in between, for n_lstm LSTMs (actor, critic) at once.
+ * Gate order i, f, g, o (torch nn.LSTM).  All device f32, stream-ordered.
+ * ---------------------------------------------------------------------- */
+
+/*
+ * Forward step: pre = gx + gates + bias; i,f,g,o = sig, sig, tanh, sig;
+ * c_new = f*c_prev + i*g; h_new = o*tanh(c_new); gates := (i, f, g, o).
+ *   gx     element (l, b, j) at gx[b*gx_row_stride + l*gx_lstm_stride + j]
+ *          (X @ [W_ih_0 | W_ih_1 ...]^T, one GEMM for all steps)
+ *   gates  [n_lstm][B][4H] at lstm stride gate_lstm_stride; in: h_prev @
+ *          W_hh^T, out: the activations (kept for the backward step)
+ *   bias   [n_lstm][4H] (b_ih + b_hh)
+ *   c_prev, c_new, h_new  [n_lstm][B][H] at lstm stride state_lstm_stride
+ * H and every stride a multiple of 4.
+ */
+int vn_lstm_seq_fwd_cell(const float *gx, int64_t gx_row_stride, int64_t gx_lstm_stride, float *gates,
+                         int64_t gate_lstm_stride, const float *bias, const float *c_prev, float *c_new, float *h_new,
+                         int64_t state_lstm_stride, int32_t n_lstm, int32_t B, int32_t H, void *stream);
+
+/*
+ * Backward step: dh = dh_out + dh_rec (dh_rec = dG_{t+1} @ W_hh, or NULL at
+ * the last step); dc [n_lstm][B][H] contiguous (in: dL/dc_t, out:
+ * dL/dc_{t-1}); dG [n_lstm][B][4H] at lstm stride dG_lstm_stride, the gate
+ * pre-activation gradient, from the forward's activations act (lstm stride
+ * act_lstm_stride) and c_prev, c_new (lstm stride state_lstm_stride).
+ *   dh_out [n_lstm][B][H] at lstm stride dh_out_lstm_stride
+ */
+int vn_lstm_seq_bwd_cell(const float *dh_out, int64_t dh_out_lstm_stride, const float *dh_rec, float *dc,
+                         const float *act, int64_t act_lstm_stride, const float *c_prev, const float *c_new,
+                         int64_t state_lstm_stride, float *dG, int64_t dG_lstm_stride, int32_t n_lstm, int32_t B,
+                         int32_t H, void *stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -155,3 +155,35 @@ def test_learn_loop_end_to_end_gpu(tmp_path):
     assert data["num_timesteps"] == 3 * 32 * 256
     assert torch.equal(torch.cat([p.reshape(-1) for p in pol2.parameters()]), w1)
     env.close()
+
+
+# ------------------------------------------------------------------ learner LSTM kernels
+@pytest.mark.gpu
+@pytest.mark.parametrize("L,B", [(1, 8), (7, 33), (128, 256)])
+def test_dual_lstm_matches_nn_lstm_gpu(L, B):
+    """voxnav.lstm_seq.dual_lstm (library GEMMs + csrc/voxnav_learn.hip cell
+    kernels) against plain PyTorch fp32 nn.LSTM on the same device: outputs
+    within 2e-5 absolute, parameter gradients within 1e-4 relative of their
+    scale (f32 accumulation orders differ over L*B terms)."""
+    from voxnav.lstm_seq import dual_lstm
+    from voxnav.policy import RecurrentActorCriticPolicy
+    dev = torch.device("cuda:0")
+    torch.manual_seed(L * 1000 + B)
+    pol = RecurrentActorCriticPolicy().to(dev)
+    x = torch.randn(L, B, 80, device=dev)
+    h0 = 0.5 * torch.randn(2, B, 256, device=dev)
+    c0 = 0.5 * torch.randn(2, B, 256, device=dev)
+    wpi = torch.randn(L, B, 256, device=dev)
+    wvf = torch.randn(L, B, 256, device=dev)
+    params = list(pol.lstm_actor.parameters()) + list(pol.lstm_critic.parameters())
+
+    a, c = dual_lstm(pol, x, h0, c0)
+    ga = torch.autograd.grad((a * wpi).sum() + (c * wvf).sum(), params)
+    ra, _ = pol.lstm_actor(x, (h0[0:1].contiguous(), c0[0:1].contiguous()))
+    rc, _ = pol.lstm_critic(x, (h0[1:2].contiguous(), c0[1:2].contiguous()))
+    gr = torch.autograd.grad((ra * wpi).sum() + (rc * wvf).sum(), params)
+    assert (a - ra).abs().max().item() < 2e-5
+    assert (c - rc).abs().max().item() < 2e-5
+    for g, r in zip(ga, gr):
+        scale = r.abs().max().item() + 1e-6
+        assert (g - r).abs().max().item() <= 1e-4 * scale, (g - r).abs().max().item() / scale
