@@ -279,7 +279,8 @@ def learner_leg(args, torch, dist, dev, world, pol, buf):
     fl = 3 * lstm_flops_per_agent_step()        # forward + backward ~ 3x forward
     return {"value": round(sps, 1), "unit": "samples/s", "batch_size": B, "minibatches": n,
             "ms_per_minibatch": round(el * 1e3 / n, 3), "tflops": round(fl * sps / 1e12, 2),
-            "includes": "sequence packing, actor+critic LSTM re-run (MIOpen), MLPs, losses, backward, "
+            "includes": "sequence packing, actor+critic LSTM re-run (dual-LSTM: library GEMMs + HIP cell kernels), MLPs, "
+                        "losses, backward, "
                         "grad clip, Adam" + (", RCCL gradient all-reduce" if world > 1 else "")}
 
 
