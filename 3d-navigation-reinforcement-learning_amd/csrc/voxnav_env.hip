@@ -1837,6 +1837,161 @@ __global__ __launch_bounds__(64) void simple_bits_kernel(Params p) {
     }
 }
 
+// ----------------------------------------------------------------------------
+// The bit-plane step with a store wave: block = 2 waves, wave 0 steps 64
+// agents and stages each step's obs rows, rewards and flags in LDS (double
+// buffered), wave 1 writes step k's staging to HBM while wave 0 computes step
+// k+1.  vmcnt retires in issue order per wave, so in the one-wave kernel every
+// step's loads waited for the previous step's ~8 obs stores per lane to
+// complete; here the stepping wave issues no output stores at all (only its
+// own S-word / Q updates).  One barrier per step hands a buffer over: the
+// store wave has drained its LDS reads of buffer k&1 before it reaches the
+// barrier after which wave 0 overwrites that buffer (step k+2).
+// LDS: stage[2][64][OD] f32, reward[2][64] f32, flags[2][64] u32.
+// ----------------------------------------------------------------------------
+template <int LMAX>
+__global__ __launch_bounds__(128) void simple_split_kernel(Params p) {
+    extern __shared__ float sm[];
+    const int OD = p.obs_dim, L = p.L;
+    float *stage = sm;
+    float *srew = sm + 2 * 64 * OD;
+    uint32_t *sflg = reinterpret_cast<uint32_t *>(srew + 2 * 64);
+    const int lane = threadIdx.x & 63;
+    const int a0 = blockIdx.x * 64;
+    const int rows = min(64, p.N - a0);
+
+    if (threadIdx.x >= 64) {                     // ---- store wave ----
+        for (int k = 0; k < p.K; ++k) {
+            __syncthreads();                     // step k staged in buffer k & 1
+            const int b = k & 1;
+            const float *st = stage + b * 64 * OD;
+            float *dst = p.obs + ((size_t)k * p.N + a0) * OD;
+            if (!((rows * OD) & 3) && !(reinterpret_cast<uintptr_t>(dst) & 15u)) {
+                const float4 *s4 = reinterpret_cast<const float4 *>(st);
+                float4 *d4 = reinterpret_cast<float4 *>(dst);
+                for (int q = lane; q < (rows * OD) >> 2; q += 64) obs_store(d4 + q, s4[q]);
+            } else {
+                for (int q = lane; q < rows * OD; q += 64) __builtin_nontemporal_store(st[q], dst + q);
+            }
+            if (lane < rows) {
+                const size_t o = (size_t)k * p.N + a0 + lane;
+                const uint32_t f = sflg[b * 64 + lane];
+                if (p.reward) p.reward[o] = srew[b * 64 + lane];
+                if (p.term) p.term[o] = (uint8_t)(f & 1u);
+                if (p.trunc) p.trunc[o] = (uint8_t)(f >> 1);
+            }
+        }
+        return;
+    }
+
+    // ---- stepping wave (simple_bits_kernel's step, outputs to LDS) ----
+    const int ai = a0 + lane;
+    const bool live = ai < p.N;
+    const SPlanes pl = splanes(p, live ? ai : a0);
+    Agent g = unpack(live ? p.hot[ai] : make_uint4(0u, 0u, 0u, 0u));
+    uint32_t goal = live ? p.goal[ai] : 0u;
+    uint32_t next_seed = live ? p.next_seed[ai] : 0u;
+    Room R = load_room(p, g.room);
+    SRows w;
+    w.wx = w.wy = 0;
+    w.wz = 0;
+    w.rec = make_uint2(0u, 0u);
+    if (live) sb_load_rows(p, pl, g, R, w);
+
+    uint4 r4 = make_uint4(0u, 0u, 0u, 0u);   // Philox block of steps t & ~3 (one call per 4 steps)
+    for (int k = 0; k < p.K; ++k) {
+        const int b = k & 1;
+        float *row = stage + b * 64 * OD + lane * OD;
+        const uint64_t t = p.t0 + (uint64_t)k;
+        int a = 0;
+        if (live) {
+            if (p.actions) {
+                a = p.actions[(size_t)k * p.N + ai];
+            } else {
+                if (k == 0 || (t & 3) == 0) r4 = philox4x32_10(p.policy_seed, p.gid_base + (uint64_t)ai, t >> 2);
+                const uint32_t word = (t & 3) == 0 ? r4.x : (t & 3) == 1 ? r4.y : (t & 3) == 2 ? r4.z : r4.w;
+                a = (int)(((uint64_t)word * 6u) >> 32);
+            }
+            if (p.actions_out) p.actions_out[(size_t)k * p.N + ai] = a;
+        }
+        bool trunc = false, term = false;
+        if (live) {
+            // step (:109-150)
+            g.step_count += 1;
+            trunc = g.step_count >= R.total_free;                      // :111, max_steps = total_free (:409)
+            const int d = a < 4 ? rel_dir(a, g.facing) : (a == 4 ? 4 : 5);
+            if (a < 4) g.facing = facing_of(d);                        // :164-171
+            const bool moved = (ray_e8(w.rec, d) & 0x7fu) >= 1u;
+            bool explored = false;
+            if (moved) {                                                 // _mark_visited (:273-298)
+                const int nx = g.x + (d == 0 ? 1 : d == 1 ? -1 : 0);
+                const int ny = g.y + (d == 2 ? 1 : d == 3 ? -1 : 0);
+                const int nz = g.z + (d == 4 ? 1 : d == 5 ? -1 : 0);
+                const int ax = d >> 1;
+                const uint64_t wx0 = w.wx, wy0 = w.wy;
+                const uint32_t wz0 = w.wz;
+                bool seen = ax == 0 ? ((wx0 >> nx) & 1ull) : ax == 1 ? ((wy0 >> ny) & 1ull) : ((wz0 >> nz) & 1u);
+                g.x = nx;
+                g.y = ny;
+                g.z = nz;
+                sb_load_rows(p, pl, g, R, w);
+                // a Q cell (internal_grid 2) is entered without counting, but
+                // it is a sensing position all the same, so S is set
+                const bool q = (g.move_mask & 1u) && ((pl.qz[nx * p.pd + ny] >> nz) & 1u);
+                if (!seen) {
+                    w.wx |= 1ull << nx;
+                    w.wy |= 1ull << ny;
+                    w.wz |= 1u << nz;
+                    pl.sx[ny * p.ph + nz] = w.wx;
+                    pl.sy[nx * p.ph + nz] = w.wy;
+                    pl.sz[nx * p.pd + ny] = w.wz;
+                    if (!q) {
+                        g.visited += 1;
+                        explored = true;
+                    }
+                }
+            }
+            g.last_action = a;                                           // :137
+            sb_observe<LMAX>(p, pl, g, w, row);                          // :139
+            // compute_reward (:189-217), f64 in the reference's order
+            double r = -0.1;
+            if (!moved) {
+                g.bumps += 1;
+                r += -10.0;
+            }
+            if (a != 2 && a < 4) r += 0.05;
+            const int gx = goal & 0xff, gy = (goal >> 8) & 0xff, gz = (goal >> 16) & 0xff;
+            if (g.x == gx && g.y == gy && g.z >= gz && g.z - gz < 5) {   // SPOT_GOAL_HEIGTH = 5 (:201-206)
+                g.done = true;
+                r += 100.0;
+            }
+            if (trunc) r += 0.0;
+            if (explored) r += 1.0;
+            term = g.done;
+            const size_t o = (size_t)k * p.N + ai;
+            srew[b * 64 + lane] = (float)r;
+            sflg[b * 64 + lane] = (term ? 1u : 0u) | (trunc ? 2u : 0u);
+            if (p.reward64) p.reward64[o] = r;
+            if ((term || trunc) && p.autoreset && p.terminal_obs) {
+                float *to = p.terminal_obs + o * OD;
+                for (int q = 0; q < OD; ++q) to[q] = row[q];
+            }
+        }
+        // SB3 VecEnv auto-reset
+        const bool need = live && p.autoreset && (term || trunc);
+        if (__ballot(need)) {
+            sb_reset_wave<LMAX>(p, pl, need, next_seed, g, goal, R, w, row, lane, a0);
+            if (need) next_seed += p.seed_stride;
+        }
+        __syncthreads();                         // hand buffer b to the store wave
+    }
+    if (live) {
+        p.hot[ai] = pack(g);
+        p.goal[ai] = goal;
+        p.next_seed[ai] = next_seed;
+    }
+}
+
 // internal_grid value of one cell from S, Q and the walls (see the layout
 // note above the bit-plane kernel)
 __device__ int8_t sb_belief_cell(const Params &p, int i, const Room &R, int x, int y, int z) {
@@ -1960,6 +2115,7 @@ struct VnEnv {
     uint32_t ablate = 0;
     int variant = 0, obs_dim = VN_OBS_DIM;
     int sbits = 0;
+    int sb_split = 1;  // simpleEnv step with a store wave (simple_split_kernel)
     int sb_aw = 32;   // measured: 32 agents per wave 5.62 vs 64 5.43 G env-steps/s (16: 4.97)
     uint32_t sy_off = 0, sz_off = 0, qz_off = 0;
 };
@@ -2054,10 +2210,25 @@ int launch_ph(int /*L*/, dim3 grid, dim3 block, hipStream_t s, const Params &p) 
 template <bool RESET_ONLY>
 int launch_env(VnEnv *e, const Params &p, hipStream_t s) {
     if (e->variant == VN_VARIANT_SIMPLE) {
+        const int L = e->cfg.local_map_length;
+        if (!RESET_ONLY && e->sbits && e->sb_split) {
+            // stepping wave + store wave per 64 agents (simple_split_kernel)
+            const size_t lds = (size_t)2 * 64 * e->obs_dim * sizeof(float) + 2 * 64 * 8;
+            const dim3 grid((unsigned)((e->N + 63) / 64));
+            if (L <= 4)
+                hipLaunchKernelGGL((simple_split_kernel<4>), grid, dim3(128), lds, s, p);
+            else if (L <= 8)
+                hipLaunchKernelGGL((simple_split_kernel<8>), grid, dim3(128), lds, s, p);
+            else if (L <= 10)
+                hipLaunchKernelGGL((simple_split_kernel<10>), grid, dim3(128), lds, s, p);
+            else
+                hipLaunchKernelGGL((simple_split_kernel<16>), grid, dim3(128), lds, s, p);
+            VN_HIP(hipGetLastError());
+            return VN_OK;
+        }
         const int aw = e->sbits ? e->sb_aw : 64;
         const size_t lds = (size_t)aw * e->obs_dim * sizeof(float);
         const dim3 grid((unsigned)((e->N + aw - 1) / aw));
-        const int L = e->cfg.local_map_length;
         if (e->sbits && L <= 4)
             hipLaunchKernelGGL((simple_bits_kernel<RESET_ONLY, 4>), grid, dim3(64), lds, s, p);
         else if (e->sbits && L <= 8)
@@ -2231,6 +2402,7 @@ int vn_create(const VnRoomSet *rooms, int32_t n_agents, const VnConfig *cfg, int
     if (e->variant == VN_VARIANT_SIMPLE && maxW <= 64 && maxD <= 64 && !dense) {
         // bit planes: SX u64 [pd][ph], SY u64 [pw][ph], SZ u32 [pw][pd], QZ u32 [pw][pd]
         e->sbits = 1;
+        if (const char *sp = getenv("VOXNAV_SIMPLE_SPLIT")) e->sb_split = sp[0] == '1';   // A/B knob
         if (const char *aw = getenv("VOXNAV_SIMPLE_AW")) {   // agents per wave (A/B knob)
             const int v = atoi(aw);
             if (v == 16 || v == 32 || v == 64) e->sb_aw = v;
