@@ -90,6 +90,19 @@ def test_simple_random_rollout_matches_oracle(voxnav, src, L, N, K):
     _rollout_vs_oracle(src, L, N, K)
 
 
+# the one-wave bit-plane kernel (the default is the stepping + store wave
+# kernel); VOXNAV_SIMPLE_AW sets its agents per wave
+ONE_WAVE_CASES = [("box:8x8x4", 4, 300, 200, "32"), ("set:P2_training", 10, 1000, 150, "64"),
+                  ("file:P3_training/kitchen2.txt", 16, 200, 150, "16")]
+
+
+@pytest.mark.parametrize("src,L,N,K,aw", ONE_WAVE_CASES, ids=[f"{c[0]}-aw{c[4]}" for c in ONE_WAVE_CASES])
+def test_simple_one_wave_kernel_matches_oracle(voxnav, monkeypatch, src, L, N, K, aw):
+    monkeypatch.setenv("VOXNAV_SIMPLE_SPLIT", "0")
+    monkeypatch.setenv("VOXNAV_SIMPLE_AW", aw)
+    _rollout_vs_oracle(src, L, N, K)
+
+
 # the dense int8 map kernel: rooms wider or deeper than 64 cells, or forced
 # with VOXNAV_SIMPLE_DENSE=1 (the bit-plane kernel covers the cases above)
 DENSE_CASES = [
