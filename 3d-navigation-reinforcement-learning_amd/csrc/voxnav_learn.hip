@@ -152,171 +152,6 @@ __global__ __launch_bounds__(256) void seq_cell_bwd_kernel(const float *__restri
 
 #undef VN_F4
 
-// ----------------------------------------------------------------------------
-// Fused steps: the recurrent GEMM on the matrix cores (v_mfma_f32_16x16x4_f32,
-// exact f32) with the cell update as the epilogue.  A block of 4 waves owns a
-// tile of 16 rows x 16 hidden units of one LSTM and splits K four ways (one
-// wave per quarter: short dependent-load chains and 4 waves per SIMD); the
-// partial tiles meet in LDS and wave w finishes accumulator register w, i.e.
-// rows b0 + 4q + w.  Operands come straight from L2 as float4s: lane l
-// (r = l & 15, q = l >> 4) loads k = k0 + 4q .. +3 of its A row and B column,
-// and MFMA s of the k-block uses element s, so k-index q of MFMA s is
-// k0 + 4q + s -- the same permutation on both operands: the four MFMAs of a
-// block sum k0 .. k0+15 exactly once.  C/D: col = l & 15 (unit), row = 4q + reg.
-// ----------------------------------------------------------------------------
-typedef __attribute__((ext_vector_type(4))) float f32x4_t;
-
-__device__ __forceinline__ void tile_of(int tile, int B, int H, int &l, int &b0, int &u0) {
-    const int rb = (B + 15) >> 4, ub = H >> 4;
-    l = tile / (rb * ub);
-    const int r = tile - l * rb * ub;
-    u0 = (r / rb) << 4;                      // consecutive tiles: same units, next rows
-    b0 = (r - (r / rb) * rb) << 4;
-}
-
-// forward step t: pre = gx + h_prev @ W_hh^T + bias; cell; act, c_new, h_new
-//   w_hh [n_lstm][4H][H] (nn.LSTM layout), h_prev / c_prev / c_new / h_new
-//   [n_lstm][B][H] at lstm stride s1, act [n_lstm][B][4H] at lstm stride s4
-__global__ __launch_bounds__(256) void seq_step_fwd_kernel(const float *__restrict__ gx, int64_t gx_row,
-                                                           int64_t gx_lstm, const float *__restrict__ w_hh,
-                                                           const float *__restrict__ bias,
-                                                           const float *__restrict__ h_prev,
-                                                           const float *__restrict__ c_prev, float *__restrict__ c_new,
-                                                           float *__restrict__ h_new, float *__restrict__ act,
-                                                           int64_t s4, int64_t s1, int n_lstm, int B, int H) {
-    __shared__ float part[4][4][4][64];      // [wave][gate][reg][lane]
-    int l, b0, u0;
-    tile_of((int)blockIdx.x, B, H, l, b0, u0);
-    const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63, r = lane & 15, q = lane >> 4;
-    const int G = 4 * H, KW = H >> 2;        // K per wave
-    const float *pa = h_prev + (int64_t)l * s1 + (int64_t)min(b0 + r, B - 1) * H + wv * KW + 4 * q;
-    const float *pw = w_hh + (int64_t)l * G * H + (int64_t)(u0 + r) * H + wv * KW + 4 * q;
-    f32x4_t acc[4];
-#pragma unroll
-    for (int g = 0; g < 4; ++g) acc[g] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-    // the wave's whole quarter of K (4 blocks of 16) is loaded up front: 20
-    // float4 in flight, one round trip, then 64 MFMAs
-    float4 a[4], bw[4][4];
-#pragma unroll
-    for (int kb = 0; kb < 4; ++kb) {
-        a[kb] = ld4(pa + 16 * kb);
-#pragma unroll
-        for (int g = 0; g < 4; ++g) bw[kb][g] = ld4(pw + (int64_t)g * H * H + 16 * kb);
-    }
-#pragma unroll
-    for (int kb = 0; kb < 4; ++kb)
-#pragma unroll
-        for (int g = 0; g < 4; ++g) {
-            acc[g] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[kb].x, bw[kb][g].x, acc[g], 0, 0, 0);
-            acc[g] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[kb].y, bw[kb][g].y, acc[g], 0, 0, 0);
-            acc[g] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[kb].z, bw[kb][g].z, acc[g], 0, 0, 0);
-            acc[g] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[kb].w, bw[kb][g].w, acc[g], 0, 0, 0);
-        }
-#pragma unroll
-    for (int g = 0; g < 4; ++g)
-#pragma unroll
-        for (int reg = 0; reg < 4; ++reg) part[wv][g][reg][lane] = acc[g][reg];
-    __syncthreads();
-    const int u = u0 + r, b = b0 + 4 * q + wv;   // this wave finishes register wv
-    if (b < B) {
-        float pre[4];
-#pragma unroll
-        for (int g = 0; g < 4; ++g) {
-            float v = part[0][g][wv][lane];
-            v += part[1][g][wv][lane];
-            v += part[2][g][wv][lane];
-            v += part[3][g][wv][lane];
-            pre[g] = v;
-        }
-        const float *px = gx + (int64_t)b * gx_row + (int64_t)l * gx_lstm + u;
-        const float *pb = bias + (int64_t)l * G + u;
-#pragma unroll
-        for (int g = 0; g < 4; ++g) {
-            pre[g] += px[g * H];
-            pre[g] += pb[g * H];
-        }
-        const float ig = sigm(pre[0]), fg = sigm(pre[1]), gg = tanhf(pre[2]), og = sigm(pre[3]);
-        const int64_t so = (int64_t)l * s1 + (int64_t)b * H + u;
-        const float fc = fg * c_prev[so], ig2 = ig * gg;
-        const float cn = fc + ig2;
-        c_new[so] = cn;
-        h_new[so] = og * tanhf(cn);
-        float *pact = act + (int64_t)l * s4 + (int64_t)b * G + u;
-        pact[0] = ig;
-        pact[H] = fg;
-        pact[2 * H] = gg;
-        pact[3 * H] = og;
-    }
-}
-
-// backward step t: dh = dh_out(t) + dG(t+1) @ W_hh (dG_next NULL at the last
-// step), then the cell backward -> dG(t), dc.  w_hh_t [n_lstm][H][4H] is
-// W_hh transposed (so the B operand is a float4 along k); dG_next, dG at lstm
-// strides sgn, sg; act at sa; dc [n_lstm][B][H] contiguous in/out.
-__global__ __launch_bounds__(256) void seq_step_bwd_kernel(const float *__restrict__ dG_next, int64_t sgn,
-                                                           const float *__restrict__ w_hh_t,
-                                                           const float *__restrict__ dh_out, int64_t so1,
-                                                           float *__restrict__ dc, const float *__restrict__ act,
-                                                           int64_t sa, const float *__restrict__ c_prev,
-                                                           const float *__restrict__ c_new, int64_t s1,
-                                                           float *__restrict__ dG, int64_t sg, int n_lstm, int B,
-                                                           int H) {
-    __shared__ float part[4][4][64];         // [wave][reg][lane]
-    int l, b0, u0;
-    tile_of((int)blockIdx.x, B, H, l, b0, u0);
-    const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63, r = lane & 15, q = lane >> 4;
-    const int G = 4 * H, KW = G >> 2;        // K = 4H, a quarter per wave
-    if (dG_next) {
-        // two accumulators (alternate k-blocks): one chain would run at the
-        // 40-cycle dependent latency instead of the 32-cycle issue interval
-        f32x4_t acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
-        const float *pa = dG_next + (int64_t)l * sgn + (int64_t)min(b0 + r, B - 1) * G + wv * KW + 4 * q;
-        const float *pw = w_hh_t + (int64_t)l * H * G + (int64_t)(u0 + r) * G + wv * KW + 4 * q;
-        // next iteration's operands in flight during this one's MFMAs
-        float4 a0 = ld4(pa), w0 = ld4(pw), a1 = ld4(pa + 16), w1 = ld4(pw + 16);
-        for (int k0 = 0; k0 < KW; k0 += 32) {
-            const int kn = k0 + 32 < KW ? k0 + 32 : k0;
-            const float4 a0n = ld4(pa + kn), w0n = ld4(pw + kn), a1n = ld4(pa + kn + 16), w1n = ld4(pw + kn + 16);
-            acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a0.x, w0.x, acc0, 0, 0, 0);
-            acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a1.x, w1.x, acc1, 0, 0, 0);
-            acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a0.y, w0.y, acc0, 0, 0, 0);
-            acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a1.y, w1.y, acc1, 0, 0, 0);
-            acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a0.z, w0.z, acc0, 0, 0, 0);
-            acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a1.z, w1.z, acc1, 0, 0, 0);
-            acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a0.w, w0.w, acc0, 0, 0, 0);
-            acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a1.w, w1.w, acc1, 0, 0, 0);
-            a0 = a0n; w0 = w0n; a1 = a1n; w1 = w1n;
-        }
-#pragma unroll
-        for (int reg = 0; reg < 4; ++reg) part[wv][reg][lane] = acc0[reg] + acc1[reg];
-    } else {
-#pragma unroll
-        for (int reg = 0; reg < 4; ++reg) part[wv][reg][lane] = 0.0f;
-    }
-    __syncthreads();
-    const int u = u0 + r, b = b0 + 4 * q + wv;   // this wave finishes register wv
-    if (b < B) {
-        float rec = part[0][wv][lane];
-        rec += part[1][wv][lane];
-        rec += part[2][wv][lane];
-        rec += part[3][wv][lane];
-        const float dh = dh_out[(int64_t)l * so1 + (int64_t)b * H + u] + rec;
-        const int64_t sd = ((int64_t)l * B + b) * H + u;
-        const int64_t so = (int64_t)l * s1 + (int64_t)b * H + u;
-        const float *pa = act + (int64_t)l * sa + (int64_t)b * G + u;
-        const float ig = pa[0], fg = pa[H], gg = pa[2 * H], og = pa[3 * H];
-        const float tc = tanhf(c_new[so]);
-        const float dtc = dh * og;
-        const float dcc = dc[sd] + dtc * (1.0f - tc * tc);
-        float *pg = dG + (int64_t)l * sg + (int64_t)b * G + u;
-        pg[0] = dcc * gg * (ig * (1.0f - ig));
-        pg[H] = dcc * c_prev[so] * (fg * (1.0f - fg));
-        pg[2 * H] = dcc * ig * (1.0f - gg * gg);
-        pg[3 * H] = dh * tc * (og * (1.0f - og));
-        dc[sd] = dcc * fg;
-    }
-}
-
 int grid_for(int n_lstm, int B, int H, dim3 &grid) {
     const int64_t threads = (int64_t)n_lstm * B * (H / 4);
     grid = dim3((unsigned)((threads + 255) / 256));
@@ -356,39 +191,6 @@ int vn_lstm_seq_bwd_cell(const float *dh_out, int64_t dh_out_lstm_stride, const 
     hipLaunchKernelGGL(seq_cell_bwd_kernel, grid, dim3(256), 0, (hipStream_t)stream, dh_out, dh_out_lstm_stride,
                        dh_rec, dc, act, act_lstm_stride, c_prev, c_new, state_lstm_stride, dG, dG_lstm_stride, n_lstm,
                        B, H);
-    VN_HIP(hipGetLastError());
-    return VN_OK;
-}
-
-int vn_lstm_seq_fwd_step(const float *gx, int64_t gx_row_stride, int64_t gx_lstm_stride, const float *w_hh,
-                         const float *bias, const float *h_prev, const float *c_prev, float *c_new, float *h_new,
-                         float *act, int64_t act_lstm_stride, int64_t state_lstm_stride, int32_t n_lstm, int32_t B,
-                         int32_t H, void *stream) {
-    if (!gx || !w_hh || !bias || !h_prev || !c_prev || !c_new || !h_new || !act)
-        return fail(VN_ERR_INVALID, "NULL argument");
-    if (n_lstm < 1 || B < 1 || H < 64 || (H % 64)) return fail(VN_ERR_INVALID, "bad sizes n_lstm=%d B=%d H=%d (H %% 64)", n_lstm, B, H);
-    if ((state_lstm_stride | act_lstm_stride) & 3) return fail(VN_ERR_INVALID, "strides must be multiples of 4 floats");
-    const int64_t tiles = (int64_t)n_lstm * ((B + 15) / 16) * (H / 16);
-    hipLaunchKernelGGL(seq_step_fwd_kernel, dim3((unsigned)tiles), dim3(256), 0, (hipStream_t)stream, gx,
-                       gx_row_stride, gx_lstm_stride, w_hh, bias, h_prev, c_prev, c_new, h_new, act, act_lstm_stride,
-                       state_lstm_stride, n_lstm, B, H);
-    VN_HIP(hipGetLastError());
-    return VN_OK;
-}
-
-int vn_lstm_seq_bwd_step(const float *dG_next, int64_t dG_next_lstm_stride, const float *w_hh_t, const float *dh_out,
-                         int64_t dh_out_lstm_stride, float *dc, const float *act, int64_t act_lstm_stride,
-                         const float *c_prev, const float *c_new, int64_t state_lstm_stride, float *dG,
-                         int64_t dG_lstm_stride, int32_t n_lstm, int32_t B, int32_t H, void *stream) {
-    if (!w_hh_t || !dh_out || !dc || !act || !c_prev || !c_new || !dG) return fail(VN_ERR_INVALID, "NULL argument");
-    if (n_lstm < 1 || B < 1 || H < 64 || (H % 64)) return fail(VN_ERR_INVALID, "bad sizes n_lstm=%d B=%d H=%d (H %% 64)", n_lstm, B, H);
-    if ((dG_next_lstm_stride | dh_out_lstm_stride | act_lstm_stride | state_lstm_stride | dG_lstm_stride) & 3)
-        return fail(VN_ERR_INVALID, "strides must be multiples of 4 floats");
-    if (dG_next && dG_next == dG) return fail(VN_ERR_INVALID, "dG_next and dG must differ");
-    const int64_t tiles = (int64_t)n_lstm * ((B + 15) / 16) * (H / 16);
-    hipLaunchKernelGGL(seq_step_bwd_kernel, dim3((unsigned)tiles), dim3(256), 0, (hipStream_t)stream,
-                       dG_next, dG_next_lstm_stride, w_hh_t, dh_out, dh_out_lstm_stride, dc, act, act_lstm_stride,
-                       c_prev, c_new, state_lstm_stride, dG, dG_lstm_stride, n_lstm, B, H);
     VN_HIP(hipGetLastError());
     return VN_OK;
 }

@@ -7,15 +7,13 @@ at train/Grid_Train.py:228) and back-propagates through them.  Here both
 LSTMs run together over the padded ``[L, B]`` batch:
 
 forward   ``gx = X @ [W_ih_actor | W_ih_critic]^T`` for all steps (one GEMM);
-          per step ``vn_lstm_seq_fwd_step``: ``h_{t-1} @ W_hh^T`` for both
-          LSTMs on the f32 matrix cores with gx, bias and the cell update as
-          the epilogue (the activations are kept for the backward pass);
-backward  per step, in reverse, ``vn_lstm_seq_bwd_step``: ``dh = dh_out +
-          dG_{t+1} @ W_hh`` on the matrix cores, then the cell backward
-          (gate gradients dG_t, dc_{t-1}); then the weight gradients over all
-          steps at once: ``dW_hh = dG^T H_prev`` (batched), ``dW_ih = dG^T X``,
-          ``db = sum dG``.  (``FUSED_STEPS = False``: library batched GEMMs
-          per step + the cell-only kernels ``vn_lstm_seq_{fwd,bwd}_cell``.)
+          per step ``h_{t-1} @ W_hh^T`` for both LSTMs (one batched GEMM)
+          and ``vn_lstm_seq_fwd_cell`` (gates, cell, h; the activations are
+          kept for the backward pass);
+backward  per step, in reverse, ``vn_lstm_seq_bwd_cell`` (gate gradients
+          dG_t, dc_{t-1}) and ``dh_{t-1} = dG_t @ W_hh`` (batched); then the
+          weight gradients over all steps at once: ``dW_hh = dG^T H_prev``
+          (batched), ``dW_ih = dG^T X``, ``db = sum dG``.
 
 The GEMMs are library GEMMs (hipBLASLt through torch), f32 -- the
 reference's dtype; the per-step cell kernels are csrc/voxnav_learn.hip.
@@ -35,11 +33,6 @@ from typing import Tuple
 import torch
 
 from . import _native
-
-
-# per-step kernels with the recurrent GEMM fused in (csrc/voxnav_learn.hip
-# seq_step_*); False: library batched GEMM + separate cell kernels (A/B)
-FUSED_STEPS = True
 
 
 def _p(t: torch.Tensor):
@@ -76,15 +69,7 @@ class _DualLSTM(torch.autograd.Function):
         row_bytes = B * 2 * G * 4
         gx_base = gx.data_ptr()
         hs_base, cs_base = hs.data_ptr(), cs.data_ptr()
-        fused = FUSED_STEPS and H % 64 == 0
         for t in range(L):
-            if fused:       # recurrent GEMM + cell in one kernel (f32 MFMA)
-                _native.check(lib.vn_lstm_seq_fwd_step(
-                    C.c_void_p(gx_base + t * row_bytes), 2 * G, G, _p(w_hh), _p(bias),
-                    C.c_void_p(hs_base + t * B * H * 4), C.c_void_p(cs_base + t * B * H * 4),
-                    C.c_void_p(cs_base + (t + 1) * B * H * 4), C.c_void_p(hs_base + (t + 1) * B * H * 4),
-                    _p(act[t]), B * G, s_state, 2, B, H, st), "vn_lstm_seq_fwd_step")
-                continue
             torch.bmm(hs[:, t], w_hh_t, out=act[t])
             _native.check(lib.vn_lstm_seq_fwd_cell(
                 C.c_void_p(gx_base + t * row_bytes), 2 * G, G, _p(act[t]), B * G, _p(bias),
@@ -109,17 +94,7 @@ class _DualLSTM(torch.autograd.Function):
         s_state = (L + 1) * B * H
         cs_base, dG_base, do_base = cs.data_ptr(), dG.data_ptr(), dh_out.data_ptr()
         need_h0 = ctx.needs_input_grad[1]
-        if FUSED_STEPS and H % 64 == 0:   # dG_{t+1} @ W_hh fused into the step (f32 MFMA)
-            w_hh_tr = w_hh.transpose(1, 2).contiguous()            # [2, H, 4H]
-            for t in range(L - 1, -1, -1):
-                _native.check(lib.vn_lstm_seq_bwd_step(
-                    C.c_void_p(dG_base + (t + 1) * B * G * 4) if t < L - 1 else None, L * B * G, _p(w_hh_tr),
-                    C.c_void_p(do_base + t * B * H * 4), L * B * H, _p(dc), _p(act[t]), B * G,
-                    C.c_void_p(cs_base + t * B * H * 4), C.c_void_p(cs_base + (t + 1) * B * H * 4), s_state,
-                    C.c_void_p(dG_base + t * B * G * 4), L * B * G, 2, B, H, st), "vn_lstm_seq_bwd_step")
-            if need_h0:
-                torch.bmm(dG[:, 0], w_hh, out=dh)
-        for t in (range(L - 1, -1, -1) if not (FUSED_STEPS and H % 64 == 0) else ()):
+        for t in range(L - 1, -1, -1):
             _native.check(lib.vn_lstm_seq_bwd_cell(
                 C.c_void_p(do_base + t * B * H * 4), L * B * H, _p(dh) if t < L - 1 else None, _p(dc),
                 _p(act[t]), B * G, C.c_void_p(cs_base + t * B * H * 4), C.c_void_p(cs_base + (t + 1) * B * H * 4),

@@ -290,27 +290,6 @@ int vn_lstm_seq_bwd_cell(const float *dh_out, int64_t dh_out_lstm_stride, const 
                          int64_t state_lstm_stride, float *dG, int64_t dG_lstm_stride, int32_t n_lstm, int32_t B,
                          int32_t H, void *stream);
 
-/*
- * The same two steps with the recurrent GEMM fused in (f32 matrix cores,
- * v_mfma_f32_16x16x4_f32; the cell update is the GEMM's epilogue):
- * forward   pre = gx + h_prev @ W_hh^T + bias, then as vn_lstm_seq_fwd_cell
- *           with the activations written to act (lstm stride act_lstm_stride);
- *           w_hh [n_lstm][4H][H] (nn.LSTM weight_hh_l0 layout); h_prev, c_prev,
- *           c_new, h_new [n_lstm][B][H] at lstm stride state_lstm_stride
- * backward  dh = dh_out + dG_next @ W_hh (dG_next = the later step's dG,
- *           NULL at the last step; w_hh_t [n_lstm][H][4H] = W_hh transposed),
- *           then as vn_lstm_seq_bwd_cell
- * H a multiple of 64.
- */
-int vn_lstm_seq_fwd_step(const float *gx, int64_t gx_row_stride, int64_t gx_lstm_stride, const float *w_hh,
-                         const float *bias, const float *h_prev, const float *c_prev, float *c_new, float *h_new,
-                         float *act, int64_t act_lstm_stride, int64_t state_lstm_stride, int32_t n_lstm, int32_t B,
-                         int32_t H, void *stream);
-int vn_lstm_seq_bwd_step(const float *dG_next, int64_t dG_next_lstm_stride, const float *w_hh_t, const float *dh_out,
-                         int64_t dh_out_lstm_stride, float *dc, const float *act, int64_t act_lstm_stride,
-                         const float *c_prev, const float *c_new, int64_t state_lstm_stride, float *dG,
-                         int64_t dG_lstm_stride, int32_t n_lstm, int32_t B, int32_t H, void *stream);
-
 #ifdef __cplusplus
 }
 #endif

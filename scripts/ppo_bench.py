@@ -25,7 +25,6 @@ def main():
     ap.add_argument("--batch", default="4096,16384")
     ap.add_argument("--minibatches", type=int, default=24)
     ap.add_argument("--policy", default="lstm")
-    ap.add_argument("--fused", default="1", help="comma list of voxnav.lstm_seq.FUSED_STEPS values to time")
     a = ap.parse_args()
     dev = torch.device("cuda:0")
     torch.manual_seed(0)
@@ -37,9 +36,7 @@ def main():
     torch.cuda.synchronize()
     from bench import lstm_flops_per_agent_step, mlp_flops_per_agent_step
     fwd = lstm_flops_per_agent_step() if a.policy == "lstm" else mlp_flops_per_agent_step()
-    import voxnav.lstm_seq as ls
-    for B, fz in [(int(b), f) for b in a.batch.split(",") for f in a.fused.split(",")]:
-        ls.FUSED_STEPS = fz == "1"
+    for B in map(int, a.batch.split(",")):
         ln = PPOLearner(pol, n_epochs=1, batch_size=B, seed=0)
         total = a.T * a.agents
         nmb = min(a.minibatches, total // B)
@@ -56,7 +53,7 @@ def main():
         torch.cuda.synchronize()
         el = time.perf_counter() - t0
         sps = nmb * B / el
-        print(f"policy={a.policy} batch={B} fused_steps={fz}: {el / nmb * 1e3:.2f} ms/minibatch, {sps / 1e6:.3f} M samples/s, "
+        print(f"policy={a.policy} batch={B}: {el / nmb * 1e3:.2f} ms/minibatch, {sps / 1e6:.3f} M samples/s, "
               f"~{3 * fwd * sps / 1e12:.2f} TFLOP/s (fwd+bwd = 3x fwd)", flush=True)
 
 

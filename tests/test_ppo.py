@@ -159,16 +159,12 @@ def test_learn_loop_end_to_end_gpu(tmp_path):
 
 # ------------------------------------------------------------------ learner LSTM kernels
 @pytest.mark.gpu
-@pytest.mark.parametrize("fused", [True, False], ids=["fused-steps", "gemm+cell"])
 @pytest.mark.parametrize("L,B", [(1, 8), (7, 33), (128, 256)])
-def test_dual_lstm_matches_nn_lstm_gpu(L, B, fused, monkeypatch):
-    """voxnav.lstm_seq.dual_lstm (per-step MFMA GEMM + cell kernels, or
-    library GEMMs + cell-only kernels) against plain PyTorch fp32 nn.LSTM on
-    the same device: outputs within 2e-5 absolute, parameter gradients within
-    1e-4 relative of their scale (f32 accumulation orders differ over L*B
-    terms)."""
-    import voxnav.lstm_seq as ls
-    monkeypatch.setattr(ls, "FUSED_STEPS", fused)
+def test_dual_lstm_matches_nn_lstm_gpu(L, B):
+    """voxnav.lstm_seq.dual_lstm (library GEMMs + csrc/voxnav_learn.hip cell
+    kernels) against plain PyTorch fp32 nn.LSTM on the same device: outputs
+    within 2e-5 absolute, parameter gradients within 1e-4 relative of their
+    scale (f32 accumulation orders differ over L*B terms)."""
     from voxnav.lstm_seq import dual_lstm
     from voxnav.policy import RecurrentActorCriticPolicy
     dev = torch.device("cuda:0")
