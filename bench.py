@@ -419,6 +419,12 @@ def main():
             one = cpu_baseline((W, D, H), args.L, max(2.0, args.cpu_seconds / 4), threads_override=1)
             cb["single_core_value"] = one["value"]
             cb["cpu_model"] = cpu_model()
+            # the reference itself (Python, envs/CubicEnv.py) cannot travel to this
+            # box; its step rate as measured in the build container
+            cb["reference_python_build_container"] = {
+                "single_core": 7.0e3, "eight_processes": 4.95e4, "unit": "env-steps/s",
+                "workload": "32x32x8 box, L=10, random actions, 1 env per process",
+                "source": "SURVEY.md §6 (Intel Xeon, 8 vCPU; not this box)"}
             rec["cpu_baseline"] = cb
         line = json.dumps(rec)
         print(line, flush=True)
