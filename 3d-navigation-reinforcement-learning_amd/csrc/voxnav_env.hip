@@ -1608,6 +1608,16 @@ __device__ __forceinline__ void sb_load_rows(const Params &p, const SPlanes &pl,
     w.rec = p.rays[R.ray_off + (uint32_t)((g.x * R.D + g.y) * R.H + g.z)];
 }
 
+// after a move along axis ax the S word along that axis is the same row (only
+// this agent writes it, so the cached copy is current): reload the other two
+__device__ __forceinline__ void sb_move_rows(const Params &p, const SPlanes &pl, const Agent &g, const Room &R,
+                                             SRows &w, int ax) {
+    if (ax != 0) w.wx = pl.sx[g.y * p.ph + g.z];
+    if (ax != 1) w.wy = pl.sy[g.x * p.ph + g.z];
+    if (ax != 2) w.wz = pl.sz[g.x * p.pd + g.y];
+    w.rec = p.rays[R.ray_off + (uint32_t)((g.x * R.D + g.y) * R.H + g.z)];
+}
+
 // reset for the lanes with `need` (as simple_reset_wave): the wave zeroes
 // every resetting agent's planes, then each marks its start cell and senses.
 template <int LMAX>
@@ -1747,7 +1757,7 @@ __global__ __launch_bounds__(64) void simple_bits_kernel(Params p) {
                 g.x = nx;
                 g.y = ny;
                 g.z = nz;
-                sb_load_rows(p, pl, g, R, w);
+                sb_move_rows(p, pl, g, R, w, ax);
                 // a Q cell (internal_grid 2) is entered without counting, but
                 // it is a sensing position all the same, so S is set
                 const bool q = (g.move_mask & 1u) && ((pl.qz[nx * p.pd + ny] >> nz) & 1u);
@@ -1934,7 +1944,7 @@ __global__ __launch_bounds__(128) void simple_split_kernel(Params p) {
                 g.x = nx;
                 g.y = ny;
                 g.z = nz;
-                sb_load_rows(p, pl, g, R, w);
+                sb_move_rows(p, pl, g, R, w, ax);
                 // a Q cell (internal_grid 2) is entered without counting, but
                 // it is a sensing position all the same, so S is set
                 const bool q = (g.move_mask & 1u) && ((pl.qz[nx * p.pd + ny] >> nz) & 1u);
