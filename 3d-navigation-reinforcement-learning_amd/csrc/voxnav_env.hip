@@ -557,7 +557,10 @@ typedef float F4v __attribute__((ext_vector_type(4)));
 
 // Streaming store of one obs float4 to HBM.  VN_OBS_STORE: 0 plain, 1
 // non-temporal, 2 sc1 (write-through; the line is dropped from L2, so the
-// obs stream does not evict the belief / plane / ray-table lines).
+// obs stream does not evict the belief / plane / ray-table lines), 3 sc1 nt,
+// 4 sc0 sc1 nt.  Measured (scripts/ab.py, 65536 agents, 32x32x8, 5408
+// steps, 7 rounds): 1 = 6.83, 3 = 6.86, 4 = 6.65 G env-steps/s -- equal
+// within noise; 0 and 2 are ~15% slower.  1 stays the default.
 #ifndef VN_OBS_STORE
 #define VN_OBS_STORE 1
 #endif
@@ -567,6 +570,12 @@ __device__ __forceinline__ void obs_store(float4 *dst, const float4 &v) {
 #elif VN_OBS_STORE == 2
     const F4v w{v.x, v.y, v.z, v.w};
     asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(dst), "v"(w) : "memory");
+#elif VN_OBS_STORE == 3
+    const F4v w{v.x, v.y, v.z, v.w};
+    asm volatile("global_store_dwordx4 %0, %1, off sc1 nt" ::"v"(dst), "v"(w) : "memory");
+#elif VN_OBS_STORE == 4
+    const F4v w{v.x, v.y, v.z, v.w};
+    asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1 nt" ::"v"(dst), "v"(w) : "memory");
 #else
     *dst = v;
 #endif
