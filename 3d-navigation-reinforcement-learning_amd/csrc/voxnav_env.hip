@@ -38,6 +38,7 @@
 #include <cstring>
 #include <new>
 #include <string>
+#include <type_traits>
 #include <vector>
 
 #include "vn_common.h"
@@ -97,8 +98,9 @@ struct EnvConst {
     const uint2 *rays;
     const uint32_t *starts;
     int32_t *err;
-    int n_rooms, use_room_draw, nby, pad0;
-    uint32_t agent_bytes, xp_off, pad1, pad2;
+    int n_rooms, use_room_draw, nby, pcache;
+    uint32_t agent_bytes, xp_off, map_bytes, pad2;
+    const uint4 *wimg;       // plane-set mode: per room, the bricked map with latent wall bits
 };
 
 struct Params {
@@ -137,6 +139,9 @@ struct Params {
     int sbits;               // simpleEnv bit-plane layout (rooms up to 64 x 64 x 31)
     int sb_aw;               // bit-plane kernel: agents per 64-lane wave (16, 32 or 64)
     uint32_t sy_off, sz_off, qz_off;
+    const int8_t *wimg;      // plane-set mode (CubicEnv, PH 8, rooms <= 64 x 64): latent-wall room images
+    int pcache;
+    float *scratch;          // 4 KiB: targets of inactive lanes' output stores
 };
 
 __device__ __forceinline__ Agent unpack(uint4 s) {
@@ -548,10 +553,29 @@ __device__ __forceinline__ uint32_t boff(int x, int y, int z, int nby) {
 struct ObsDst {
     float *row;          // direct HBM row (NULL: none)
     float *term_row;     // terminal-obs HBM row under auto-reset (NULL: dropped)
-    float *stage;        // LDS staging row: used instead of `row` when set
+    uint32_t *stage;     // the wave's LDS staging block (STAGE_WORDS): used instead of `row` when set
     bool select;
     bool truncated;
+    int aslot;           // the agent's slot (0..15) in the staging block
 };
+
+// Staging block of one wave (16 agents) in plane-set mode: the window bytes
+// of each obs row in obs order (byte 16i + 4q + k of agent a at byte a * 64),
+// then each agent's 16 tail floats.  The flush expands the bytes through the
+// LUT, so the block is 2 KiB per wave instead of the 5 KiB of float rows (the
+// byte-mark kernels' format, STAGE_WORDS_F).
+constexpr int STAGE_WORDS = 16 * 16 + 16 * 16;
+constexpr int STAGE_WORDS_F = 16 * VN_OBS_DIM;
+
+// float4 f (of the wave's 16 rows x 20) of the staged obs rows
+__device__ __forceinline__ float4 stage_float4(const uint32_t *ws, const float *tab, int f) {
+    const int a = f / 20, r = f - 20 * a;
+    if (r < 16) {
+        const uint32_t wb = ws[a * 16 + r];
+        return make_float4(tab[wb & 0xffu], tab[(wb >> 8) & 0xffu], tab[(wb >> 16) & 0xffu], tab[wb >> 24]);
+    }
+    return reinterpret_cast<const float4 *>(ws + 256)[a * 4 + (r - 16)];
+}
 
 typedef float F4v __attribute__((ext_vector_type(4)));
 
@@ -582,6 +606,7 @@ __device__ __forceinline__ void obs_store(float4 *dst, const float4 &v) {
 }
 typedef __attribute__((address_space(3))) F4v LdsF4;     // LDS
 typedef __attribute__((address_space(1))) F4v GlbF4;     // global
+typedef __attribute__((address_space(3))) uint32_t LdsU32;  // LDS
 __device__ __forceinline__ F4v f4v(const float4 &v) { return F4v{v.x, v.y, v.z, v.w}; }
 
 struct Rays {
@@ -596,6 +621,123 @@ __device__ __forceinline__ bool mark(Col<PH> &c, int z, const Rays &ry, int r, i
     if (s <= ry.nf[r]) return col_or_chk<PH>(c, z, KNOWN);
     if (ry.wh[r] && s == ry.nf[r] + 1) return col_or_chk<PH>(c, z, WALLB);
     return false;
+}
+
+// ----------------------------------------------------------------------------
+// Plane-set mode (PH == 8, rooms <= 64 x 64; VnEnv::pcache).  A sensing mark
+// outside the window is recorded only in the marked-bit planes, never as a
+// byte: the belief is byte map UNION planes, and a column takes the plane
+// bits into its known bits (bit7) when it enters the window.  Wall cells
+// carry a latent wall bit (0x40 without 0x80 = still unknown) from the reset
+// onwards (copied from a per-room image), so a plane bit alone tells a known
+// wall from a known free cell.  The plane rows the window needs stay in LDS
+// for the whole launch: the x-plane rows (y', z = 0..7) of the 4 window rows
+// y' (slot y' & 3) and the y-plane rows (x', z) of the 4 window columns x'
+// (slot 4 + (x' & 3)); in HBM such a set is one 64-byte line.  A move swaps
+// one set (written back if dirty, like a tile column), so a ray mark costs an
+// LDS word instead of an HBM row write plus one blind byte store per new cell.
+// ----------------------------------------------------------------------------
+// RT, the LDS row word: uint32_t when every room of the set is at most
+// 32 x 32 (half the LDS, so 16 waves fit a CU), else uint64_t.  The HBM
+// rows stay u64 either way.
+template <typename RT>
+struct PsetGeom {
+    static constexpr int STRIDE = sizeof(RT) == 4 ? 8 * 8 + 4 : 8 * 8 + 2;   // RT words per agent, 16-B aligned
+};
+
+__device__ __forceinline__ uint4 *pset_hbm(const Params &p, int8_t *map, bool xs, int c) {
+    return reinterpret_cast<uint4 *>(map + (xs ? p.xp_off : p.yp_off) + (uint32_t)c * 64u);
+}
+
+// lane q's share of a set: rows z = 2q, 2q + 1 (16 B of the HBM line)
+template <typename RT>
+__device__ __forceinline__ void pset_put(RT *ps, int slot, int q, uint4 v) {
+    if constexpr (sizeof(RT) == 8)
+        *reinterpret_cast<uint4 *>(ps + slot * 8 + 2 * q) = v;
+    else
+        *reinterpret_cast<uint2 *>(ps + slot * 8 + 2 * q) = make_uint2(v.x, v.z);
+}
+
+template <typename RT>
+__device__ __forceinline__ uint4 pset_get(const RT *ps, int slot, int q) {
+    if constexpr (sizeof(RT) == 8) {
+        return *reinterpret_cast<const uint4 *>(ps + slot * 8 + 2 * q);
+    } else {
+        const uint2 w = *reinterpret_cast<const uint2 *>(ps + slot * 8 + 2 * q);
+        return make_uint4(w.x, 0u, w.y, 0u);
+    }
+}
+
+// the known bits (byte z: 0x80) the planes hold for column (cx, cy), both in the window
+template <typename RT>
+__device__ __forceinline__ uint64_t pset_known(const RT *ps, int cx, int cy) {
+    const RT *xs = ps + (cy & 3) * 8, *ys = ps + (4 + (cx & 3)) * 8;
+    uint64_t k = 0;
+#pragma unroll
+    for (int z = 0; z < 8; ++z) k |= (uint64_t)(((xs[z] >> cx) | (ys[z] >> cy)) & 1u) << (8 * z + 7);
+    return k;
+}
+
+// launch start: lane q loads 16 B of each of the 8 sets (one 64-B request per set)
+template <typename RT>
+__device__ __forceinline__ void pset_fill(const Params &p, int8_t *map, RT *ps, const Agent &g, const Room &R, int q) {
+    uint4 v[8];
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+        const int yy = g.y - 2 + s, xx = g.x - 2 + s;
+        v[s] = make_uint4(0u, 0u, 0u, 0u);
+        v[4 + s] = make_uint4(0u, 0u, 0u, 0u);
+        if (yy >= 0 && yy < R.D) v[s] = pset_hbm(p, map, true, yy)[q];
+        if (xx >= 0 && xx < R.W) v[4 + s] = pset_hbm(p, map, false, xx)[q];
+    }
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+        pset_put(ps, (g.y - 2 + s) & 3, q, v[s]);
+        pset_put(ps, 4 + ((g.x - 2 + s) & 3), q, v[4 + s]);
+    }
+    __builtin_amdgcn_wave_barrier();
+}
+
+// launch end: the dirty sets back to HBM
+template <typename RT>
+__device__ __forceinline__ void pset_flush(const Params &p, int8_t *map, const RT *ps, const Agent &g, const Room &R,
+                                           uint32_t pdirty, int q) {
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+        const int yy = g.y - 2 + s, xx = g.x - 2 + s;
+        if (((pdirty >> (yy & 3)) & 1u) && yy >= 0 && yy < R.D) pset_hbm(p, map, true, yy)[q] = pset_get(ps, yy & 3, q);
+        if (((pdirty >> (4 + (xx & 3))) & 1u) && xx >= 0 && xx < R.W)
+            pset_hbm(p, map, false, xx)[q] = pset_get(ps, 4 + (xx & 3), q);
+    }
+}
+
+struct SetLoad {
+    uint4 v;
+    int slot;
+};
+
+// after a horizontal move in axis dir to (x, y): the set of the entering
+// coordinate (y-plane set of the entering x for an x move, x-plane set of the
+// entering y for a y move) replaces the leaving one.  Load first, then the
+// write-back (vmcnt retires in issue order).
+template <typename RT>
+__device__ __forceinline__ void pset_shift_issue(const Params &p, int8_t *map, const RT *ps, int dir, int x, int y,
+                                                 const Room &R, uint32_t pdirty, int q, SetLoad &sl) {
+    const bool xm = dir < 2;
+    const int e = xm ? (dir == 0 ? x + 1 : x - 2) : (dir == 2 ? y + 1 : y - 2);
+    const int l = (dir == 0 || dir == 2) ? e - 4 : e + 4;
+    const int lim = xm ? R.W : R.D;
+    sl.slot = xm ? 4 + (e & 3) : (e & 3);
+    sl.v = make_uint4(0u, 0u, 0u, 0u);
+    if (!(VN_ABLATE & 1u) && e >= 0 && e < lim) sl.v = pset_hbm(p, map, !xm, e)[q];
+    if (((pdirty >> sl.slot) & 1u) && l >= 0 && l < lim) pset_hbm(p, map, !xm, l)[q] = pset_get(ps, sl.slot, q);
+}
+
+template <typename RT>
+__device__ __forceinline__ uint32_t pset_shift_commit(RT *ps, const SetLoad &sl, uint32_t pdirty, int q) {
+    pset_put(ps, sl.slot, q, sl.v);
+    __builtin_amdgcn_wave_barrier();
+    return pdirty & ~(1u << sl.slot);
 }
 
 // ----------------------------------------------------------------------------
@@ -641,16 +783,20 @@ struct PlaneCache {      // lane 0: x-plane row, lane 1: y-plane row
 };
 
 // Fill the tile from HBM (launch start): lane q loads its 4 window columns.
-template <int PH>
-__device__ __forceinline__ void tile_fill(const Params &p, const int8_t *map, uint64_t *tile, const Agent &g,
-                                          const Room &R, int q) {
+// PC: the plane sets (ps, already filled) add their known bits.
+template <int PH, bool PC, typename RT>
+__device__ __forceinline__ void tile_fill(const Params &p, const int8_t *map, uint64_t *tile, const RT *ps,
+                                          const Agent &g, const Room &R, int q) {
     const int cy = g.y + q - 2;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
         const int cx = g.x + i - 2;
         Col<PH> c;
         col_zero<PH>(c);
-        if (cx >= 0 && cx < R.W && cy >= 0 && cy < R.D) col_load<PH>(map + boff<PH>(cx, cy, 0, p.nby), c);
+        if (cx >= 0 && cx < R.W && cy >= 0 && cy < R.D) {
+            col_load<PH>(map + boff<PH>(cx, cy, 0, p.nby), c);
+            if constexpr (PC) c.w[0] |= pset_known(ps, cx, cy);
+        }
         tile_write<PH>(tile, tslot(cx, cy), c);
     }
 }
@@ -682,6 +828,8 @@ struct ShiftLoad {
     Col<PH> c;
     int s;
     uint32_t entering;
+    int ex, ey;          // the entering column
+    bool in;             // ... inside the room
 };
 
 template <int PH>
@@ -702,11 +850,13 @@ __device__ __forceinline__ void tile_shift_issue(const Params &p, int8_t *map, c
         sl.entering = 0x1111u << (ey & 3);
     }
     sl.s = tslot(ex, ey);
+    sl.ex = ex;
+    sl.ey = ey;
+    sl.in = ex >= 0 && ex < R.W && ey >= 0 && ey < R.D;
     // the load first: vmcnt retires in issue order, so a store issued ahead
     // of it would hold its data until the store completes
     col_zero<PH>(sl.c);
-    if (!(VN_ABLATE & 1u) && ex >= 0 && ex < R.W && ey >= 0 && ey < R.D)
-        col_load<PH>(map + boff<PH>(ex, ey, 0, p.nby), sl.c);
+    if (!(VN_ABLATE & 1u) && sl.in) col_load<PH>(map + boff<PH>(ex, ey, 0, p.nby), sl.c);
     if (!(VN_ABLATE & 8u) && ((dirty >> sl.s) & 1u) && lx >= 0 && lx < R.W && ly >= 0 && ly < R.D) {
         Col<PH> old;
         tile_read<PH>(tile, sl.s, old);
@@ -719,6 +869,7 @@ __device__ __forceinline__ uint32_t tile_shift_commit(uint64_t *tile, const Shif
     tile_write<PH>(tile, sl.s, sl.c);
     return dirty & ~sl.entering;
 }
+
 
 // Plane rows of the agent's new cell (lane 0: x-plane row (y, z), lane 1:
 // y-plane row (x, z)).  Rooms up to 128 wide keep a whole row (<= 2 words)
@@ -747,10 +898,12 @@ __device__ __forceinline__ void plane_prefetch(const Params &p, const int8_t *ma
 // One sensing pass (get_obs :254-312 with _sense_direction :345-397 and the
 // visit update of _mark_visited/do_action :156-166) on the agent's tile.
 // Returns the center cell's visit count after the update.
-template <int PH, bool FRESH>
+// PC: plane-set mode (ps = the agent's LDS plane sets, pdirty their dirty bits).
+template <int PH, bool FRESH, bool PC, typename RT>
 __device__ __forceinline__ int sense_observe(const Params &p, int8_t *map, uint64_t *tile, uint32_t &dirty,
-                                             PlaneCache &pc_, Agent &g, const Room &R, bool moved, bool &explored,
-                                             const float *tab, ObsDst dst, uint2 rec, int q) {
+                                             PlaneCache &pc_, RT *ps, uint32_t &pdirty, Agent &g,
+                                             const Room &R, bool moved, bool &explored, const float *tab, ObsDst dst,
+                                             uint2 rec, int q) {
     const int x = g.x, y = g.y, z = g.z, nby = p.nby, L = p.L;
 
     // ---- x / y marked-bit plane rows (lane 0: x row (y,z), lane 1: y row (x,z)) ----
@@ -767,6 +920,8 @@ __device__ __forceinline__ int sense_observe(const Params &p, int8_t *map, uint6
         // the row words needed depend on the span; fetch lazily below
         (void)nw;
     }
+    // PC: lane 0 owns the x-plane row (y, z), lane 1 the y-plane row (x, z), both in LDS
+    RT *prow_lds = (PC && q < 2) ? ps + (q == 0 ? (y & 3) : 4 + (x & 3)) * 8 + z : nullptr;
 
     // ---- this lane's 4 window columns from the tile ----
     const int cy = y + q - 2;
@@ -776,6 +931,10 @@ __device__ __forceinline__ int sense_observe(const Params &p, int8_t *map, uint6
     for (int i = 0; i < 4; ++i) {
         if (FRESH) {
             col_zero<PH>(col[i]);
+            // PC: the reset copied the room image (latent walls) to HBM; the
+            // tile takes the same columns
+            if (PC && yin && x + i - 2 >= 0 && x + i - 2 < R.W)
+                col_load<PH>(p.wimg + (size_t)g.room * p.map_bytes + boff<PH>(x + i - 2, cy, 0, nby), col[i]);
         } else {
             tile_read<PH>(tile, tslot(x + i - 2, cy), col[i]);
         }
@@ -817,7 +976,11 @@ __device__ __forceinline__ int sense_observe(const Params &p, int8_t *map, uint6
             const int lo = pa - base < 0 ? 0 : pa - base, hi = pb - base > 63 ? 63 : pb - base;
             pm[w] = (w == 0 || pw0 + 1 <= pwend) && hi >= lo ? ((~0ull) >> (63 - (hi - lo))) << lo : 0ull;
         }
-        if (FRESH) {                       // planes were cleared by the reset
+        if (PC) {                          // nw == 1: the row word is in LDS
+            pc_.w[0] = *prow_lds;
+            pc_.w[1] = 0ull;
+            pc_.w0 = 0;
+        } else if (FRESH) {                // planes were cleared by the reset
             pc_.row = rowi;
             pc_.w0 = nw <= 2 ? 0 : pw0;
             pc_.w[0] = pc_.w[1] = 0ull;
@@ -877,10 +1040,24 @@ __device__ __forceinline__ int sense_observe(const Params &p, int8_t *map, uint6
         if (FRESH || (inroom && ((chg >> i) & 1u))) {
             const int s = tslot(x + i - 2, cy);
             tile_write<PH>(tile, s, col[i]);
-            if (inroom) dm |= 1u << s;
+            // PC: an x/y ray mark is also in the planes, so only the agent's own
+            // column (visit count, z rays) has to reach HBM
+            if (inroom && (!PC || (q == 2 && i == 2))) dm |= 1u << s;
         }
     }
     dirty |= group_or(dm);
+
+    if constexpr (PC) {
+        uint32_t pd = 0;
+        if (q < 2) {
+            const uint64_t nv = pn[0] | pm[0];
+            if (nv != pn[0]) {
+                *prow_lds = (RT)nv;
+                pd = 1u << (q == 0 ? (y & 3) : 4 + (x & 3));
+            }
+        }
+        pdirty |= group_or(pd);
+    } else {
 
     // new marks: row bits set now for the first time.  Those inside the window
     // (d = -2..+1 from the agent) live in the tile; the others get their
@@ -911,8 +1088,8 @@ __device__ __forceinline__ int sense_observe(const Params &p, int8_t *map, uint6
         const uint32_t ryh = (uint32_t)__shfl((int)(uint32_t)(rel >> 32), 1, GROUP);
         const int pax = __shfl(pa, 0, GROUP), pay = __shfl(pa, 1, GROUP);
         const uint64_t lane_sel = 0x1111111111111111ull << q;
-        uint64_t mx = (VN_ABLATE & 32u) ? 0ull : (((uint64_t)rxh << 32) | rxl) & lane_sel;
-        uint64_t my = (VN_ABLATE & 32u) ? 0ull : (((uint64_t)ryh << 32) | ryl) & lane_sel;
+        uint64_t mx = (VN_ABLATE & 96u) ? 0ull : (((uint64_t)rxh << 32) | rxl) & lane_sel;
+        uint64_t my = (VN_ABLATE & 96u) ? 0ull : (((uint64_t)ryh << 32) | ryl) & lane_sel;
         while (mx) {
             const int pos = pax + __ffsll((unsigned long long)mx) - 1;
             mx &= mx - 1;
@@ -928,6 +1105,7 @@ __device__ __forceinline__ int sense_observe(const Params &p, int8_t *map, uint6
             map[boff<PH>(x, pos, z, nby)] = (int8_t)v;
         }
     }
+    }   // !PC
 
     g.near_wall = g.near_wall || near;
     g.cid = ry.nf[5];
@@ -937,45 +1115,48 @@ __device__ __forceinline__ int sense_observe(const Params &p, int8_t *map, uint6
     // two single-address-space destinations (an LDS/global select would
     // compile to flat stores, which occupy the vector-memory path even for LDS)
     const bool to_term = dst.select && (dst.truncated || g.done || g.visited >= R.finish_visits);
-    float4 *lds4 = (!to_term && dst.stage && !(VN_ABLATE & 4u)) ? reinterpret_cast<float4 *>(dst.stage) : nullptr;
+    const bool to_stage = !to_term && dst.stage && !(VN_ABLATE & 4u);
     float4 *glb4 = (VN_ABLATE & 4u) ? nullptr
                    : to_term       ? reinterpret_cast<float4 *>(dst.term_row)
                    : dst.stage     ? nullptr
                                    : reinterpret_cast<float4 *>(dst.row);
-    if (lds4 || glb4) {
-        float4 ov[5];
+    float4 tail;                                                  // obs[64 + 4q .. +3]
+    if (q == 0) {
+        tail = make_float4(g.facing == 0 ? 1.0f : 0.0f, g.facing == 1 ? 1.0f : 0.0f, g.facing == 2 ? 1.0f : 0.0f,
+                           g.facing == 3 ? 1.0f : 0.0f);                                            // (:279-280)
+    } else if (q == 1) {
+        tail = make_float4(tab[TAB_ACTION + g.last_action], g.was_near_wall ? 1.0f : 0.0f, g.last_bump ? 1.0f : 0.0f,
+                           tab[TAB_CID + g.cid]);                                                   // (:284-287)
+    } else if (q == 2) {
+        tail = make_float4((float)((double)g.visited / (double)R.total_free), 0.f, 0.f, 0.f);      // (:291)
+    } else {
+        tail = make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+    if (to_stage && PC) {
+        // window bytes in obs order + the tail; the flush expands the bytes (stage_float4)
+        LdsU32 *l = (LdsU32 *)dst.stage;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) l[dst.aslot * 16 + 4 * i + q] = col_window<PH>(col[i], z);
+        ((LdsF4 *)(dst.stage + 256))[dst.aslot * 4 + q] = f4v(tail);
+    } else if (to_stage) {
+        // float rows (20 float4 per agent): the LDS this costs is free in the
+        // byte-mark kernels, whose occupancy the VGPRs set
+        LdsF4 *l = (LdsF4 *)dst.stage + dst.aslot * 20;
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
             const uint32_t wb = col_window<PH>(col[i], z);
-            ov[i].x = tab[wb & 0xffu];
-            ov[i].y = tab[(wb >> 8) & 0xffu];
-            ov[i].z = tab[(wb >> 16) & 0xffu];
-            ov[i].w = tab[wb >> 24];
+            l[4 * i + q] = F4v{tab[wb & 0xffu], tab[(wb >> 8) & 0xffu], tab[(wb >> 16) & 0xffu], tab[wb >> 24]};
         }
-        if (q == 0) {
-            ov[4] = make_float4(g.facing == 0 ? 1.0f : 0.0f, g.facing == 1 ? 1.0f : 0.0f,
-                                g.facing == 2 ? 1.0f : 0.0f, g.facing == 3 ? 1.0f : 0.0f);       // (:279-280)
-        } else if (q == 1) {
-            ov[4] = make_float4(tab[TAB_ACTION + g.last_action], g.was_near_wall ? 1.0f : 0.0f,
-                                g.last_bump ? 1.0f : 0.0f, tab[TAB_CID + g.cid]);                // (:284-287)
-        } else if (q == 2) {
-            ov[4] = make_float4((float)((double)g.visited / (double)R.total_free), 0.f, 0.f, 0.f);  // (:291)
-        } else {
-            ov[4] = make_float4(0.f, 0.f, 0.f, 0.f);
-        }
-        // explicit address spaces keep the compiler from merging the two
-        // store sequences behind one flat pointer
-        if (lds4) {
-            LdsF4 *l = (LdsF4 *)lds4;
+        l[16 + q] = f4v(tail);
+    } else if (glb4) {
+        // explicit address space: no flat stores
+        GlbF4 *gp = (GlbF4 *)glb4;
 #pragma unroll
-            for (int i = 0; i < 4; ++i) l[4 * i + q] = f4v(ov[i]);
-            l[16 + q] = f4v(ov[4]);
-        } else {
-            GlbF4 *gp = (GlbF4 *)glb4;
-#pragma unroll
-            for (int i = 0; i < 4; ++i) gp[4 * i + q] = f4v(ov[i]);
-            gp[16 + q] = f4v(ov[4]);
+        for (int i = 0; i < 4; ++i) {
+            const uint32_t wb = col_window<PH>(col[i], z);
+            gp[4 * i + q] = F4v{tab[wb & 0xffu], tab[(wb >> 8) & 0xffu], tab[(wb >> 16) & 0xffu], tab[wb >> 24]};
         }
+        gp[16 + q] = f4v(tail);
     }
     return t;
 }
@@ -1003,7 +1184,7 @@ __device__ __forceinline__ Room load_room_c(const EnvConst *ec, int r) {
 // room's bricks and both marked-bit planes.  Returns x | y<<8 | z<<16 |
 // room<<24.  Reads only through `ec` (device memory), so the step loop
 // keeps none of this in registers.
-template <int PH>
+template <int PH, bool PC>
 __device__ __noinline__ uint32_t reset_prepare(const EnvConst *ec, uint32_t seed, int8_t *map, int q) {
     MtStream mt;
     mt.seed = seed;
@@ -1020,14 +1201,17 @@ __device__ __noinline__ uint32_t reset_prepare(const EnvConst *ec, uint32_t seed
         const uint2 rec = ec->rays[R.ray_off + (uint32_t)((sx * R.D + sy) * R.H + sz)];
         if ((rec.y >> 16) & 1u) s = ec->starts[R.start_off + mt.below(R.total_free)];   // start in a wall
     }
-    // clear the room's bricks to "unknown" (0x00), 16 B per lane per store
+    // clear the room's bricks to "unknown" (0x00; PC: the room image, 0x40
+    // at the walls), 16 B per lane per store
     uint4 *base = reinterpret_cast<uint4 *>(map);
+    const uint4 *img = PC ? ec->wimg + (size_t)room * (ec->map_bytes / 16u) : nullptr;
     const uint32_t per_brick = (uint32_t)PH;          // 16-byte chunks per brick
     const uint32_t total = (uint32_t)(R.nbx * R.nby) * per_brick;
     for (uint32_t c = (uint32_t)q; c < total; c += 4u) {
         const uint32_t brick = c / per_brick, w = c - brick * per_brick;
         const uint32_t bx = brick / (uint32_t)R.nby, by = brick - bx * (uint32_t)R.nby;
-        base[(bx * (uint32_t)ec->nby + by) * per_brick + w] = make_uint4(0u, 0u, 0u, 0u);
+        const uint32_t o = (bx * (uint32_t)ec->nby + by) * per_brick + w;
+        base[o] = PC ? img[o] : make_uint4(0u, 0u, 0u, 0u);
     }
     // and both marked-bit planes
     uint4 *pl = reinterpret_cast<uint4 *>(map + ec->xp_off);
@@ -1041,12 +1225,13 @@ __device__ __noinline__ uint32_t reset_prepare(const EnvConst *ec, uint32_t seed
 // the new room's bricks and planes in HBM by the 4 lanes, a zero tile, then
 // sensing from the start cell.  The old episode's dirty tile is dropped.
 // ----------------------------------------------------------------------------
-template <int PH>
+template <int PH, bool PC, typename RT>
 __device__ __forceinline__ void group_reset(const Params &p, int8_t *map, uint64_t *tile, uint32_t &dirty,
-                                            PlaneCache &pc_, bool need, uint32_t seed, Agent &g, Room &R,
-                                            const float *tab, float *obs_row, float *stage_row, int q) {
+                                            PlaneCache &pc_, RT *ps, uint32_t &pdirty, bool need,
+                                            uint32_t seed, Agent &g, Room &R, const float *tab, float *obs_row,
+                                            uint32_t *stage, int aslot, int q) {
     if (need) {
-        const uint32_t drawn = reset_prepare<PH>(p.envc, seed, map, q);
+        const uint32_t drawn = reset_prepare<PH, PC>(p.envc, seed, map, q);
         const int room = (int)(drawn >> 24);
         R = load_room(p, room);
         g.room = room;
@@ -1063,13 +1248,18 @@ __device__ __forceinline__ void group_reset(const Params &p, int8_t *map, uint64
         g.move_mask = 0;
         dirty = 0;
         pc_.row = -1;
+        if (PC) {                         // the planes were cleared: empty sets
+#pragma unroll
+            for (int k = 0; k < 8; ++k) pset_put(ps, 2 * q + (k >> 2), k & 3, make_uint4(0u, 0u, 0u, 0u));
+            pdirty = 0;
+        }
     }
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
     if (need) {
         bool explored = false;
         const uint2 rec = p.rays[R.ray_off + (uint32_t)((g.x * R.D + g.y) * R.H + g.z)];
-        sense_observe<PH, true>(p, map, tile, dirty, pc_, g, R, false, explored, tab,
-                                ObsDst{obs_row, nullptr, stage_row, false, false}, rec, q);
+        sense_observe<PH, true, PC, RT>(p, map, tile, dirty, pc_, ps, pdirty, g, R, false, explored, tab,
+                                        ObsDst{obs_row, nullptr, stage, false, false, aslot}, rec, q);
     }
 }
 
@@ -1085,17 +1275,38 @@ constexpr int AGENTS_PER_BLOCK = BLOCK / GROUP;
 // for all outstanding stores of the previous step before the move is known.
 // FAST: reward / terminated / truncated requested, reward64 / actions_out
 // not (the rollout-buffer call): no runtime pointer tests in the step loop.
-template <int PH, bool EXT, bool FAST, bool RESET_ONLY>
+// PC: plane-set mode (see pset_fill); 128-thread blocks, so the larger LDS
+// footprint still leaves 10 waves per CU.
+#ifndef VN_PC_BLOCK
+#define VN_PC_BLOCK 128
+#endif
+#ifndef VN_PC_MIN_WAVES
+#define VN_PC_MIN_WAVES 4   // waves per SIMD the VGPR budget is set for
+#endif
+template <int PH, bool EXT, bool FAST, bool RESET_ONLY, int PCM>
 #ifndef VN_MIN_WAVES_PER_SIMD
 #define VN_MIN_WAVES_PER_SIMD 4   // <= 128 VGPRs: the 16 waves of 256 agents per CU resident at once
 #endif
-__global__ __launch_bounds__(BLOCK, VN_MIN_WAVES_PER_SIMD) void env_kernel(Params p) {
+__global__ __launch_bounds__(PCM ? VN_PC_BLOCK : BLOCK, PCM ? VN_PC_MIN_WAVES : VN_MIN_WAVES_PER_SIMD) void env_kernel(Params p) {
+    constexpr bool PC = PCM != 0;
+    using RT = typename std::conditional<PCM == 2, uint32_t, uint64_t>::type;
+    constexpr int kAgents = (PC ? VN_PC_BLOCK : BLOCK) / GROUP;
     __shared__ float tab[TAB_SIZE];
-    __shared__ __attribute__((aligned(16))) uint64_t tiles[AGENTS_PER_BLOCK * TileGeom<PH>::STRIDE];
-    // obs rows of the step, staged per wave so HBM sees 1 KiB contiguous stores
-    __shared__ __attribute__((aligned(16))) float4 stage[AGENTS_PER_BLOCK * (VN_OBS_DIM / 4)];
+    __shared__ __attribute__((aligned(16))) uint64_t tiles[kAgents * TileGeom<PH>::STRIDE];
+    // obs rows of the step, staged per wave (STAGE_WORDS) so HBM sees 1 KiB contiguous stores
+    constexpr int kStageWords = PC ? STAGE_WORDS : STAGE_WORDS_F;
+    __shared__ __attribute__((aligned(16))) uint32_t stage[(kAgents / 16) * kStageWords];
+    __shared__ __attribute__((aligned(16))) RT psets[PC ? kAgents * PsetGeom<RT>::STRIDE : 2];
+#ifdef VN_LDS_PAD_U64            // diagnostics: occupancy at a larger LDS footprint
+    __shared__ uint64_t lds_pad[VN_LDS_PAD_U64];
+    if (p.N < 0) lds_pad[threadIdx.x] = 0ull;
+    if (p.N < 0) p.obs[0] = (float)lds_pad[threadIdx.x ^ 1];
+#endif
     for (int k = threadIdx.x; k < TAB_SIZE; k += blockDim.x) tab[k] = p.lut[k];
     __syncthreads();
+    // a wave without agents leaves (no block-wide barrier follows)
+    const int wave_agent0 = (int)((blockIdx.x * blockDim.x + (threadIdx.x & ~63)) / GROUP);
+    if (wave_agent0 >= p.N) return;
 
     const int q = threadIdx.x & (GROUP - 1);
     const int i = (int)((blockIdx.x * blockDim.x + threadIdx.x) / GROUP);
@@ -1111,14 +1322,17 @@ __global__ __launch_bounds__(BLOCK, VN_MIN_WAVES_PER_SIMD) void env_kernel(Param
     pc_.row = -1;
     pc_.w0 = 0;
     pc_.w[0] = pc_.w[1] = 0ull;
+    RT *ps = psets + (PC ? (threadIdx.x / GROUP) * PsetGeom<RT>::STRIDE : 0);
+    uint32_t pdirty = 0;
 
     if (RESET_ONLY) {
         const bool need = active && (p.mask == nullptr || p.mask[i] != 0);
         const uint32_t seed = need ? (uint32_t)p.seeds[i] : 0u;
-        group_reset<PH>(p, map, tile, dirty, pc_, need, seed, g, R, tab,
-                        need ? p.obs + (size_t)i * VN_OBS_DIM : nullptr, nullptr, q);
+        group_reset<PH, PC, RT>(p, map, tile, dirty, pc_, ps, pdirty, need, seed, g, R, tab,
+                                need ? p.obs + (size_t)i * VN_OBS_DIM : nullptr, nullptr, 0, q);
         if (need) {
             tile_flush<PH>(p, map, tile, g, R, dirty, q);
+            if (PC) pset_flush(p, map, ps, g, R, pdirty, q);
             if (q == 0) {
                 p.hot[i] = pack(g);
                 p.next_seed[i] = seed + p.seed_stride;
@@ -1127,12 +1341,67 @@ __global__ __launch_bounds__(BLOCK, VN_MIN_WAVES_PER_SIMD) void env_kernel(Param
         return;
     }
 
-    if (active) tile_fill<PH>(p, map, tile, g, R, q);
+    if (active) {
+        if (PC) pset_fill(p, map, ps, g, R, q);
+        tile_fill<PH, PC, RT>(p, map, tile, ps, g, R, q);
+    }
 #ifndef VN_STAGE_OBS
 #define VN_STAGE_OBS 1
 #endif
-    float *stage_row =
-        VN_STAGE_OBS ? reinterpret_cast<float *>(stage + (size_t)(threadIdx.x / GROUP) * (VN_OBS_DIM / 4)) : nullptr;
+    uint32_t *wst = VN_STAGE_OBS ? stage + (threadIdx.x >> 6) * kStageWords : nullptr;   // this wave's staging block
+    const int aslot = (threadIdx.x & 63) >> 2;
+
+    // Outputs of step k (the staged obs rows, reward, flags) are stored after
+    // step k+1's loads are issued (DEFER): vmcnt retires in issue order, so
+    // stores ahead of a step's loads would hold the loads' data until they
+    // complete.  The store sequence is branch-free -- the first call stores
+    // placeholders into step 0's rows (rewritten by the real store later),
+    // lanes past the wave's last agent repeat its last float4 or store to
+    // p.scratch, all 4 lanes of an agent store its reward -- so the
+    // compiler's vmcnt waits stay exact.
+#ifndef VN_DEFER_PC
+#define VN_DEFER_PC 1
+#endif
+#ifndef VN_DEFER_ALL
+#define VN_DEFER_ALL 0      // byte-mark kernels: deferring spills them (VGPRs) -- measured slower
+#endif
+    constexpr bool DEFER = (PC && VN_DEFER_PC) || VN_DEFER_ALL;
+    const int lane = threadIdx.x & 63;
+    const int nvalid = (p.N - wave_agent0) * (VN_OBS_DIM / 4);       // float4s of the wave's agents (> 0)
+    int pk = -1;                                                      // the step whose outputs are pending
+    float pr = 0.f;
+    double pr64 = 0.0;
+    uint8_t pte = 0, ptr8 = 0;
+    auto flush_obs = [&]() {
+        const size_t kk = (size_t)(pk < 0 ? 0 : pk);
+        if (VN_STAGE_OBS && !(VN_ABLATE & 16u)) {
+            float4 *dst4 = reinterpret_cast<float4 *>(p.obs + (kk * p.N + wave_agent0) * VN_OBS_DIM);
+            if constexpr (PC) {
+#pragma unroll 1
+                for (int jj = 0; jj < (64 / GROUP) * (VN_OBS_DIM / 4) / 64; ++jj) {
+                    const int f = lane + 64 * jj < nvalid ? lane + 64 * jj : nvalid - 1;
+                    obs_store(dst4 + f, stage_float4(wst, tab, f));
+                }
+            } else {
+                const float4 *ws4 = reinterpret_cast<const float4 *>(wst);
+#pragma unroll
+                for (int jj = 0; jj < (64 / GROUP) * (VN_OBS_DIM / 4) / 64; ++jj) {
+                    const int f = lane + 64 * jj < nvalid ? lane + 64 * jj : nvalid - 1;
+                    obs_store(dst4 + f, ws4[f]);
+                }
+            }
+        }
+    };
+    auto store_rewards = [&]() {
+        const size_t kk = (size_t)(pk < 0 ? 0 : pk);
+        if (!(VN_ABLATE & 128u)) {
+            const size_t o = kk * (size_t)p.N + (size_t)ai;
+            if (FAST || p.reward) *(active ? p.reward + o : p.scratch + lane) = pr;
+            if (!FAST && p.reward64) *(active ? p.reward64 + o : reinterpret_cast<double *>(p.scratch + 128) + lane) = pr64;
+            if (FAST || p.term) *(active ? p.term + o : reinterpret_cast<uint8_t *>(p.scratch + 64) + lane) = pte;
+            if (FAST || p.trunc) *(active ? p.trunc + o : reinterpret_cast<uint8_t *>(p.scratch + 96) + lane) = ptr8;
+        }
+    };
 
     // outer loop: one Philox call per agent per 4-step block of the global
     // step counter; inner loop: the steps of that block
@@ -1148,8 +1417,18 @@ __global__ __launch_bounds__(BLOCK, VN_MIN_WAVES_PER_SIMD) void env_kernel(Param
         bool finished = false;
         const size_t row = (size_t)k * (size_t)p.N + (size_t)i;
         const uint64_t tt = tb + (uint64_t)j;
+        if (!DEFER) {        // no pending outputs cross the step
+            pr = 0.f;
+            pr64 = 0.0;
+            pte = ptr8 = 0;
+        }
+        int a = 0;
+        bool moved = false, shifted = false, truncated = false;
+        ShiftLoad<PH> sl;
+        SetLoad pl;
+        uint2 rec = make_uint2(0u, 0u);
         if (active) {
-            const int a = EXT ? p.actions[row] : (int)((acts >> (8 * (uint32_t)(tt & 3u))) & 0xffu);
+            a = EXT ? p.actions[row] : (int)((acts >> (8 * (uint32_t)(tt & 3u))) & 0xffu);
             if (!FAST && p.actions_out && q == 0) p.actions_out[row] = a;
 
             // step() prologue (:111-116)
@@ -1158,7 +1437,7 @@ __global__ __launch_bounds__(BLOCK, VN_MIN_WAVES_PER_SIMD) void env_kernel(Param
                 g.near_wall = false;
             }
             if (g.step_count < 0xffffffu) ++g.step_count;
-            const bool truncated = g.step_count >= R.total_free;
+            truncated = g.step_count >= R.total_free;
 
             // do_action (:134-166): relative move table by facing -> axis dir
             int dir;
@@ -1173,26 +1452,39 @@ __global__ __launch_bounds__(BLOCK, VN_MIN_WAVES_PER_SIMD) void env_kernel(Param
             } else {
                 dir = (a == 4) ? 4 : 5;
             }
-            const bool moved = (g.move_mask >> dir) & 1u;
+            moved = (g.move_mask >> dir) & 1u;
             if (moved) {
                 g.x += (dir == 0) - (dir == 1);
                 g.y += (dir == 2) - (dir == 3);
                 g.z += (dir == 4) - (dir == 5);
             }
             // the step's loads, all in flight together: entering window
-            // columns, the new cell's ray record, its plane rows
-            const bool shifted = moved && dir < 4;
-            ShiftLoad<PH> sl;
+            // column (and plane set), the new cell's ray record, its plane rows
+            shifted = moved && dir < 4;
             if (shifted) tile_shift_issue<PH>(p, map, tile, dir, g.x, g.y, R, dirty, q, sl);
-            const uint2 rec = p.rays[R.ray_off + (uint32_t)((g.x * R.D + g.y) * R.H + g.z)];
-            plane_prefetch<PH>(p, map, pc_, g.x, g.y, g.z, q);
-            if (shifted) dirty = tile_shift_commit<PH>(tile, sl, dirty);
+            if (PC && shifted) pset_shift_issue(p, map, ps, dir, g.x, g.y, R, pdirty, q, pl);
+            rec = p.rays[R.ray_off + (uint32_t)((g.x * R.D + g.y) * R.H + g.z)];
+            if (!PC) plane_prefetch<PH>(p, map, pc_, g.x, g.y, g.z, q);
+        }
+        if (DEFER) {                                      // step k-1's outputs, behind step k's loads
+            flush_obs();
+            store_rewards();
+        }
+        if (active) {
+            if (shifted) {
+                if constexpr (PC) {
+                    pdirty = pset_shift_commit(ps, pl, pdirty, q);
+                    if (sl.in) sl.c.w[0] |= pset_known(ps, sl.ex, sl.ey);
+                }
+                dirty = tile_shift_commit<PH>(tile, sl, dirty);
+            }
 
             bool explored = false;
             const ObsDst dst{p.obs + row * VN_OBS_DIM,
-                             p.terminal_obs ? p.terminal_obs + row * VN_OBS_DIM : nullptr, stage_row,
-                             p.autoreset != 0, truncated};
-            const int vv = sense_observe<PH, false>(p, map, tile, dirty, pc_, g, R, moved, explored, tab, dst, rec, q);
+                             p.terminal_obs ? p.terminal_obs + row * VN_OBS_DIM : nullptr, wst,
+                             p.autoreset != 0, truncated, aslot};
+            const int vv = sense_observe<PH, false, PC, RT>(p, map, tile, dirty, pc_, ps, pdirty, g, R, moved,
+                                                            explored, tab, dst, rec, q);
 
             // compute_reward (:169-224), f64 in the reference's order
             double r = -0.05;
@@ -1218,39 +1510,31 @@ __global__ __launch_bounds__(BLOCK, VN_MIN_WAVES_PER_SIMD) void env_kernel(Param
             }
             if (truncated) r += -5.0;
             g.last_action = a;
-
-            if (q == 0) {
-                if (FAST || p.reward) p.reward[row] = (float)r;
-                if (!FAST && p.reward64) p.reward64[row] = r;
-                if (FAST || p.term) p.term[row] = g.done ? 1 : 0;
-                if (FAST || p.trunc) p.trunc[row] = truncated ? 1 : 0;
-            }
+            pr = (float)r;
+            pr64 = r;
+            pte = g.done ? 1 : 0;
+            ptr8 = truncated ? 1 : 0;
             finished = g.done || truncated;
         }
+        pk = k;
+        if (!DEFER) store_rewards();                      // nothing carried across the reset
         const bool need = p.autoreset && finished;
         if (__ballot(need)) {
             const uint32_t seed = next_seed;
-            group_reset<PH>(p, map, tile, dirty, pc_, need, seed, g, R, tab,
-                            need ? p.obs + row * VN_OBS_DIM : nullptr, stage_row, q);
+            group_reset<PH, PC, RT>(p, map, tile, dirty, pc_, ps, pdirty, need, seed, g, R, tab,
+                                    need ? p.obs + row * VN_OBS_DIM : nullptr, wst, aslot, q);
             if (need) next_seed = seed + p.seed_stride;
         }
-        // flush the wave's 16 staged obs rows: contiguous in [K][N][80]
-        if (VN_STAGE_OBS && !(VN_ABLATE & 16u)) {
-            const int lane = threadIdx.x & 63;
-            const int wave_agent0 = (int)((blockIdx.x * blockDim.x + (threadIdx.x & ~63)) / GROUP);
-            const float4 *ws = stage + (size_t)((threadIdx.x & ~63) / GROUP) * (VN_OBS_DIM / 4);
-            float4 *dst4 = reinterpret_cast<float4 *>(p.obs + ((size_t)k * p.N + wave_agent0) * VN_OBS_DIM);
-            const int nvalid = (p.N - wave_agent0) * (VN_OBS_DIM / 4);   // float4s of active agents
-#pragma unroll
-            for (int j = 0; j < (64 / GROUP) * (VN_OBS_DIM / 4) / 64; ++j) {
-                const int f = lane + 64 * j;
-                if (f < nvalid) obs_store(dst4 + f, ws[f]);
-            }
-        }
+        if (!DEFER) flush_obs();
     }
+    }
+    if (DEFER) {
+        flush_obs();
+        store_rewards();
     }
     if (active) {
         tile_flush<PH>(p, map, tile, g, R, dirty, q);
+        if (PC) pset_flush(p, map, ps, g, R, pdirty, q);
         if (q == 0) {
             p.hot[i] = pack(g);
             p.next_seed[i] = next_seed;
@@ -2068,8 +2352,14 @@ __global__ void export_belief_kernel(Params p, int8_t *out, int pw, int pd) {
         v = p.belief[(size_t)i * p.agent_bytes + (size_t)(x * p.pd + y) * p.ph + z];
     } else if (x < R.W && y < R.D && z < R.H) {
         const uint32_t off = (uint32_t)((((((x >> 2) * p.nby + (y >> 2)) << 4) + ((x & 3) << 2) + (y & 3)) * p.ph) + z);
-        const uint32_t b = (uint8_t)p.belief[(size_t)i * p.agent_bytes + off];
-        v = (b & KNOWN) ? ((b & 0x40u) ? (int8_t)-2 : (int8_t)(b & 0x3fu)) : (int8_t)-1;
+        const int8_t *m = p.belief + (size_t)i * p.agent_bytes;
+        const uint32_t b = (uint8_t)m[off];
+        // a cell is known if its byte says so or a marked-bit plane holds it
+        // (plane-set mode records marks outside the window only there)
+        const uint64_t xr = reinterpret_cast<const uint64_t *>(m + p.xp_off)[(size_t)(y * p.ph + z) * p.nwx + (x >> 6)];
+        const uint64_t yr = reinterpret_cast<const uint64_t *>(m + p.yp_off)[(size_t)(x * p.ph + z) * p.nwy + (y >> 6)];
+        const bool known = (b & KNOWN) || ((xr >> (x & 63)) & 1ull) || ((yr >> (y & 63)) & 1ull);
+        v = known ? ((b & 0x40u) ? (int8_t)-2 : (int8_t)(b & 0x3fu)) : (int8_t)-1;
     }
     out[gid] = v;
 }
@@ -2137,6 +2427,9 @@ struct VnEnv {
     int sb_split = 1;  // simpleEnv step with a store wave (simple_split_kernel)
     int sb_aw = 32;   // measured: 32 agents per wave 5.62 vs 64 5.43 G env-steps/s (16: 4.97)
     uint32_t sy_off = 0, sz_off = 0, qz_off = 0;
+    int pcache = 0;    // CubicEnv plane-set mode (PH 8, rooms <= 64 x 64): see pset_fill
+    int8_t *d_wimg = nullptr;
+    float *d_scratch = nullptr;   // 4 KiB: targets of inactive lanes' output stores
 };
 
 namespace {
@@ -2206,22 +2499,28 @@ Params base_params(VnEnv *e) {
     p.sy_off = e->sy_off;
     p.sz_off = e->sz_off;
     p.qz_off = e->qz_off;
+    p.wimg = e->d_wimg;
+    p.pcache = e->pcache;
+    p.scratch = e->d_scratch;
     return p;
 }
 
-template <int PH, bool RESET_ONLY>
-int launch_ph(int /*L*/, dim3 grid, dim3 block, hipStream_t s, const Params &p) {
+template <int PH, bool RESET_ONLY, int PCM>
+int launch_ph(int N, hipStream_t s, const Params &p) {
+    const int bs = PCM ? VN_PC_BLOCK : BLOCK;
+    const dim3 block((unsigned)bs);
+    const dim3 grid((unsigned)(((size_t)N * GROUP + bs - 1) / bs));
     const bool fast = p.reward && p.term && p.trunc && !p.reward64 && !p.actions_out;
     if (RESET_ONLY)
-        hipLaunchKernelGGL((env_kernel<PH, false, false, true>), grid, block, 0, s, p);
+        hipLaunchKernelGGL((env_kernel<PH, false, false, true, PCM>), grid, block, 0, s, p);
     else if (p.actions && fast)
-        hipLaunchKernelGGL((env_kernel<PH, true, true, false>), grid, block, 0, s, p);
+        hipLaunchKernelGGL((env_kernel<PH, true, true, false, PCM>), grid, block, 0, s, p);
     else if (p.actions)
-        hipLaunchKernelGGL((env_kernel<PH, true, false, false>), grid, block, 0, s, p);
+        hipLaunchKernelGGL((env_kernel<PH, true, false, false, PCM>), grid, block, 0, s, p);
     else if (fast)
-        hipLaunchKernelGGL((env_kernel<PH, false, true, false>), grid, block, 0, s, p);
+        hipLaunchKernelGGL((env_kernel<PH, false, true, false, PCM>), grid, block, 0, s, p);
     else
-        hipLaunchKernelGGL((env_kernel<PH, false, false, false>), grid, block, 0, s, p);
+        hipLaunchKernelGGL((env_kernel<PH, false, false, false, PCM>), grid, block, 0, s, p);
     VN_HIP(hipGetLastError());
     return VN_OK;
 }
@@ -2261,12 +2560,11 @@ int launch_env(VnEnv *e, const Params &p, hipStream_t s) {
         VN_HIP(hipGetLastError());
         return VN_OK;
     }
-    const dim3 block(256);
-    const dim3 grid((unsigned)(((size_t)e->N * GROUP + 255) / 256));
-    const int L = e->cfg.local_map_length;
-    if (e->ph == 8) return launch_ph<8, RESET_ONLY>(L, grid, block, s, p);
-    if (e->ph == 16) return launch_ph<16, RESET_ONLY>(L, grid, block, s, p);
-    return launch_ph<32, RESET_ONLY>(L, grid, block, s, p);
+    if (e->ph == 8 && e->pcache == 2) return launch_ph<8, RESET_ONLY, 2>(e->N, s, p);
+    if (e->ph == 8 && e->pcache == 1) return launch_ph<8, RESET_ONLY, 1>(e->N, s, p);
+    if (e->ph == 8) return launch_ph<8, RESET_ONLY, 0>(e->N, s, p);
+    if (e->ph == 16) return launch_ph<16, RESET_ONLY, 0>(e->N, s, p);
+    return launch_ph<32, RESET_ONLY, 0>(e->N, s, p);
 }
 
 void free_env(VnEnv *e) {
@@ -2281,6 +2579,8 @@ void free_env(VnEnv *e) {
     (void)hipFree(e->d_err);
     (void)hipFree(e->d_envc);
     (void)hipFree(e->d_goal);
+    (void)hipFree(e->d_wimg);
+    (void)hipFree(e->d_scratch);
     delete e;
 }
 
@@ -2452,6 +2752,12 @@ int vn_create(const VnRoomSet *rooms, int32_t n_agents, const VnConfig *cfg, int
         e->xp_off = e->map_bytes;                                        // rows (y, z): pd * ph * nwx words
         e->yp_off = e->xp_off + (uint32_t)(e->pd * e->ph * e->nwx * 8);  // rows (x, z): pw * ph * nwy words
         e->agent_bytes = (e->yp_off + (uint32_t)(e->pw * e->ph * e->nwy * 8) + 15u) & ~15u;
+        // plane-set mode: 2 = u32 LDS rows (rooms <= 32 x 32), 1 = u64 rows (<= 64 x 64), 0 = byte marks
+        e->pcache = e->ph != 8 ? 0 : (e->pw <= 32 && e->pd <= 32) ? 2 : (e->nwx == 1 && e->nwy == 1) ? 1 : 0;
+        if (const char *pc = getenv("VOXNAV_PCACHE")) {   // A/B knob: 0 off, 1 at most u64 rows
+            const int v = atoi(pc);
+            if (v >= 0 && v < e->pcache) e->pcache = v;
+        }
     }
 
     DeviceGuard dg(device);
@@ -2494,6 +2800,8 @@ int vn_create(const VnRoomSet *rooms, int32_t n_agents, const VnConfig *cfg, int
     VN_ALLOC(e->d_err, sizeof(int32_t));
     VN_ALLOC(e->d_envc, sizeof(EnvConst));
     VN_ALLOC(e->d_goal, (size_t)n_agents * sizeof(uint32_t));
+    if (e->pcache) VN_ALLOC(e->d_wimg, (size_t)nr * e->map_bytes);
+    VN_ALLOC(e->d_scratch, 4096);
 #undef VN_ALLOC
     hipError_t he = hipSuccess;
     if (he == hipSuccess) he = hipMemcpy(e->d_rooms, desc.data(), desc.size() * sizeof(uint32_t), hipMemcpyHostToDevice);
@@ -2507,6 +2815,23 @@ int vn_create(const VnRoomSet *rooms, int32_t n_agents, const VnConfig *cfg, int
     if (he == hipSuccess) he = hipMemset(e->d_belief, e->variant == VN_VARIANT_SIMPLE && !e->sbits ? 0xFF : 0x00, belief_bytes);
     if (he == hipSuccess) he = hipMemset(e->d_goal, 0, (size_t)n_agents * sizeof(uint32_t));
     if (he == hipSuccess) he = hipMemset(e->d_err, 0, sizeof(int32_t));
+    if (he == hipSuccess && e->pcache) {
+        // per room: the bricked byte map of a fresh episode -- 0x40 (latent
+        // wall, still unknown) at every wall cell, 0 elsewhere
+        std::vector<int8_t> img((size_t)nr * e->map_bytes, 0);
+        size_t wo = 0;
+        for (int r = 0; r < nr; ++r) {
+            const int W = rooms->whd[3 * r], D = rooms->whd[3 * r + 1], H = rooms->whd[3 * r + 2];
+            int8_t *m = img.data() + (size_t)r * e->map_bytes;
+            for (int x = 0; x < W; ++x)
+                for (int y = 0; y < D; ++y)
+                    for (int z = 0; z < H; ++z)
+                        if (rooms->walls[wo + ((size_t)x * D + y) * H + z])
+                            m[(((((x >> 2) * e->nby + (y >> 2)) << 4) + ((x & 3) << 2) + (y & 3)) * e->ph) + z] = 0x40;
+            wo += (size_t)W * D * H;
+        }
+        he = hipMemcpy(e->d_wimg, img.data(), img.size(), hipMemcpyHostToDevice);
+    }
     if (he == hipSuccess) {
         EnvConst ec;
         std::memset(&ec, 0, sizeof(ec));
@@ -2519,6 +2844,9 @@ int vn_create(const VnRoomSet *rooms, int32_t n_agents, const VnConfig *cfg, int
         ec.nby = e->nby;
         ec.agent_bytes = e->agent_bytes;
         ec.xp_off = e->xp_off;
+        ec.map_bytes = e->map_bytes;
+        ec.pcache = e->pcache;
+        ec.wimg = reinterpret_cast<const uint4 *>(e->d_wimg);
         he = hipMemcpy(e->d_envc, &ec, sizeof(ec), hipMemcpyHostToDevice);
     }
     if (he == hipSuccess) he = hipDeviceSynchronize();

@@ -1,6 +1,8 @@
 #!/usr/bin/env python3
 """Interleaved A/B timing of library variants in ONE process (same device,
 same state), e.g.  python scripts/ab.py --variants base:path.so,lb4:other.so
+A variant may add environment settings read at env creation:
+  --variants pc:lib.so:VOXNAV_PCACHE=1,nopc:lib.so:VOXNAV_PCACHE=0
 
 Ablation variants (VN_ABLATE bits, diagnostics only) are separate builds:
   python -c "import voxnav._build as b; b.build_variant('noobs', ['VN_ABLATE=16u'])"
@@ -28,10 +30,14 @@ def main():
     ap.add_argument("--steps", type=int, default=256)
     ap.add_argument("--rounds", type=int, default=5)
     a = ap.parse_args()
-    libs = {}
+    libs, envs = {}, {}
+    loaded = {}
     for v in a.variants.split(","):
-        name, path = v.split(":")[:2]
-        libs[name] = _native.load_variant(REPO / path if not path.startswith("/") else path)
+        name, path, *kv = v.split(":")
+        if path not in loaded:
+            loaded[path] = _native.load_variant(REPO / path if not path.startswith("/") else path)
+        libs[name] = loaded[path]
+        envs[name] = dict(x.split("=", 1) for x in kv)
     cfgs = [c.split(":") for c in a.configs.split(",")]
     # One env alive at a time, created and destroyed per measurement, so every
     # variant gets the same device allocations (HBM placement shifts the
@@ -49,8 +55,15 @@ def main():
             rs = load_archive_set(room) if room.startswith("P") else single_room_set(box_room(*map(int, room.split("x"))))
             names = list(libs) if r % 2 == 0 else list(libs)[::-1]
             for name in names:
+                saved = {k: os.environ.get(k) for k in envs[name]}
+                os.environ.update(envs[name])
                 e = BatchedGridEnv(num_agents=n, rooms=rs, local_map_length=L, autoreset=True, device="cuda:0",
                                    lib=libs[name])
+                for k, old in saved.items():
+                    if old is None:
+                        os.environ.pop(k, None)
+                    else:
+                        os.environ[k] = old
                 e.reset(seed=42)
                 o = outs[tuple(c)]
                 for _ in range(max(2, 64 // F)):

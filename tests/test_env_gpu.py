@@ -301,3 +301,39 @@ def test_gridagent_facade_matches_golden(voxnav):
             ag.reset(seed=int(d["seeds"][si]))
             si += 1
     ag.close()
+
+MIX_CASES = [("box:32x32x8", 10, 96), ("box:8x8x4", 4, 40), ("box:16x16x8", 7, 50)]
+
+
+@pytest.mark.parametrize("pcache", ["0", "1", "2"])
+@pytest.mark.parametrize("src,L,N", MIX_CASES, ids=[c[0] for c in MIX_CASES])
+def test_launch_mix_belief_matches_oracle(voxnav, monkeypatch, pcache, src, L, N):
+    """Launches of 16, 1, 5, 3 and 30 fused steps on one env in each belief
+    mode of the PH-8 kernel (VOXNAV_PCACHE: 0 byte marks, 1 plane sets in u64
+    LDS rows, 2 in u32 rows -- marks outside the window then live only in the
+    marked-bit planes and reach a column's bytes when it enters the window):
+    obs, f64 rewards, flags and every agent's exported belief map equal the
+    oracle's after 120 steps with auto-resets."""
+    monkeypatch.setenv("VOXNAV_PCACHE", pcache)
+    env = make_env(voxnav, src, L, n=N, autoreset=True)
+    env.reset(seed=42)
+    ks = [16, 1, 5, 16, 3, 16, 16, 1, 16, 30]
+    obs, rew, te, tr = [], [], [], []
+    for k in ks:
+        ro = env.step_random(k, policy_seed=7, reward_f64=True)
+        obs.append(ro.obs.cpu().numpy())
+        rew.append(ro.reward.cpu().numpy())
+        te.append(ro.terminated.cpu().numpy())
+        tr.append(ro.truncated.cpu().numpy())
+    orc_env = oracle_env(src, L, n_agents=N)
+    orc = orc_env.run_random(42 + np.arange(N, dtype=np.int64), policy_seed=7, K=sum(ks), seed_stride=N)
+    assert np.concatenate(obs).tobytes() == orc["obs"].tobytes()
+    np.testing.assert_array_equal(np.concatenate(rew), orc["reward"])
+    np.testing.assert_array_equal(np.concatenate(te), orc["terminated"])
+    np.testing.assert_array_equal(np.concatenate(tr), orc["truncated"])
+    b = env.belief().cpu().numpy().astype(np.int64)
+    st = env.export_state().cpu().numpy()
+    rooms = env.room_set.rooms
+    for a in range(N):
+        W, D, H = rooms[int(st[a, 13])].shape
+        np.testing.assert_array_equal(b[a, :W, :D, :H], np.minimum(orc_env.belief(a), 63), err_msg=f"agent {a}")
