@@ -1403,6 +1403,7 @@ __global__ __launch_bounds__(PCM ? VN_PC_BLOCK : BLOCK, PCM ? VN_PC_MIN_WAVES : 
         }
     };
 
+    if constexpr (DEFER) {
     // outer loop: one Philox call per agent per 4-step block of the global
     // step counter; inner loop: the steps of that block
     for (int k = 0; k < p.K;) {
@@ -1531,6 +1532,118 @@ __global__ __launch_bounds__(PCM ? VN_PC_BLOCK : BLOCK, PCM ? VN_PC_MIN_WAVES : 
     if (DEFER) {
         flush_obs();
         store_rewards();
+    }
+    } else {
+    // byte-mark kernels: the step's outputs are stored within the step (the
+    // deferred order needs more VGPRs than these kernels have at 4 waves/SIMD)
+    for (int k = 0; k < p.K;) {
+    const uint64_t tb = p.t0 + (uint64_t)k;
+    uint32_t acts = 0;                                    // 4 actions, 8 bits each, by (t & 3)
+    if (!EXT) {
+        const uint4 o = philox4x32_10(p.policy_seed, p.gid_base + (uint64_t)ai, tb >> 2);
+        acts = __umulhi(o.x, 6u) | (__umulhi(o.y, 6u) << 8) | (__umulhi(o.z, 6u) << 16) | (__umulhi(o.w, 6u) << 24);
+    }
+    const int jn = (4 - (int)(tb & 3u)) < (p.K - k) ? (4 - (int)(tb & 3u)) : (p.K - k);
+    for (int j = 0; j < jn; ++j, ++k) {
+        bool finished = false;
+        const size_t row = (size_t)k * (size_t)p.N + (size_t)i;
+        const uint64_t tt = tb + (uint64_t)j;
+        if (active) {
+            const int a = EXT ? p.actions[row] : (int)((acts >> (8 * (uint32_t)(tt & 3u))) & 0xffu);
+            if (!FAST && p.actions_out && q == 0) p.actions_out[row] = a;
+
+            // step() prologue (:111-116)
+            if (g.near_wall) {
+                g.was_near_wall = true;
+                g.near_wall = false;
+            }
+            if (g.step_count < 0xffffffu) ++g.step_count;
+            const bool truncated = g.step_count >= R.total_free;
+
+            // do_action (:134-166): relative move table by facing -> axis dir
+            int dir;
+            if (a < 4) {
+                constexpr uint32_t kDir = (2u << 0) | (0u << 2) | (3u << 4) | (1u << 6)       // fwd
+                                          | (0u << 8) | (3u << 10) | (1u << 12) | (2u << 14)   // right
+                                          | (3u << 16) | (1u << 18) | (2u << 20) | (0u << 22)  // back
+                                          | (1u << 24) | (2u << 26) | (0u << 28) | (3u << 30); // left
+                dir = (int)((kDir >> (2 * (a * 4 + g.facing))) & 3u);
+                g.facing = (int)((0x8Du >> (2 * dir)) & 3u);
+            } else {
+                dir = (a == 4) ? 4 : 5;
+            }
+            const bool moved = (g.move_mask >> dir) & 1u;
+            if (moved) {
+                g.x += (dir == 0) - (dir == 1);
+                g.y += (dir == 2) - (dir == 3);
+                g.z += (dir == 4) - (dir == 5);
+            }
+            const bool shifted = moved && dir < 4;
+            ShiftLoad<PH> sl;
+            if (shifted) tile_shift_issue<PH>(p, map, tile, dir, g.x, g.y, R, dirty, q, sl);
+            const uint2 rec = p.rays[R.ray_off + (uint32_t)((g.x * R.D + g.y) * R.H + g.z)];
+            plane_prefetch<PH>(p, map, pc_, g.x, g.y, g.z, q);
+            if (shifted) dirty = tile_shift_commit<PH>(tile, sl, dirty);
+
+            bool explored = false;
+            const ObsDst dst{p.obs + row * VN_OBS_DIM,
+                             p.terminal_obs ? p.terminal_obs + row * VN_OBS_DIM : nullptr, wst,
+                             p.autoreset != 0, truncated, aslot};
+            const int vv = sense_observe<PH, false, PC, RT>(p, map, tile, dirty, pc_, ps, pdirty, g, R, moved,
+                                                            explored, tab, dst, rec, q);
+
+            // compute_reward (:169-224), f64 in the reference's order
+            double r = -0.05;
+            const double pen = (double)vv * 0.02;
+            r -= (0.5 < pen) ? 0.5 : pen;
+            if (!moved) {
+                g.last_bump = true;
+                if (g.bumps < 0x3ffffffu) ++g.bumps;
+                r += p.crash_penalty;
+            } else {
+                g.last_bump = false;
+                if (g.was_near_wall) {
+                    g.was_near_wall = false;
+                    r += 0.15;
+                }
+                if (g.last_action != 2 && a == g.last_action && g.last_action < 4) r += 0.05;
+                if (g.last_action == 2 && a == 2) r -= 0.5;
+            }
+            if (explored) r += 1.0;
+            if (g.visited >= R.finish_visits) {            // visited / total >= 0.84 (:212-215)
+                g.done = true;
+                r += 100.0;
+            }
+            if (truncated) r += -5.0;
+            g.last_action = a;
+
+            if (q == 0 && !(VN_ABLATE & 128u)) {
+                if (FAST || p.reward) p.reward[row] = (float)r;
+                if (!FAST && p.reward64) p.reward64[row] = r;
+                if (FAST || p.term) p.term[row] = g.done ? 1 : 0;
+                if (FAST || p.trunc) p.trunc[row] = truncated ? 1 : 0;
+            }
+            finished = g.done || truncated;
+        }
+        const bool need = p.autoreset && finished;
+        if (__ballot(need)) {
+            const uint32_t seed = next_seed;
+            group_reset<PH, PC, RT>(p, map, tile, dirty, pc_, ps, pdirty, need, seed, g, R, tab,
+                                    need ? p.obs + row * VN_OBS_DIM : nullptr, wst, aslot, q);
+            if (need) next_seed = seed + p.seed_stride;
+        }
+        // the wave's 16 staged obs rows: contiguous in [K][N][80]
+        if (VN_STAGE_OBS && !(VN_ABLATE & 16u)) {
+            const float4 *ws4 = reinterpret_cast<const float4 *>(wst);
+            float4 *dst4 = reinterpret_cast<float4 *>(p.obs + ((size_t)k * p.N + wave_agent0) * VN_OBS_DIM);
+#pragma unroll 1
+            for (int jj = 0; jj < (64 / GROUP) * (VN_OBS_DIM / 4) / 64; ++jj) {
+                const int f = lane + 64 * jj;
+                if (f < nvalid) obs_store(dst4 + f, ws4[f]);
+            }
+        }
+    }
+    }
     }
     if (active) {
         tile_flush<PH>(p, map, tile, g, R, dirty, q);
