@@ -381,7 +381,8 @@ def main():
     achieved = bstep * N * F / (kern_ms * 1e-3) / 1e9
     roof = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": None,
-            "kernel": "env_kernel<PH=8,EXT=false,FAST=true,RESET_ONLY=false>", "kernel_avg_us": round(kern_ms * 1e3, 3),
+            "kernel": "env_kernel<PH=8,EXT=false,FAST=true,RESET_ONLY=false,PCM=2> (plane-set mode)",
+            "kernel_avg_us": round(kern_ms * 1e3, 3),
             "algorithmic_bytes_per_env_step": bstep, "env_steps_per_launch": N * F}
     prof = REPO / "profiles" / "pmc_traffic.json"
     if prof.exists():
