@@ -1360,7 +1360,7 @@ __global__ __launch_bounds__(PCM ? VN_PC_BLOCK : BLOCK, PCM ? VN_PC_MIN_WAVES : 
     // p.scratch, all 4 lanes of an agent store its reward -- so the
     // compiler's vmcnt waits stay exact.
 #ifndef VN_DEFER_PC
-#define VN_DEFER_PC 1
+#define VN_DEFER_PC 0     // deferred stores: measured slower
 #endif
 #ifndef VN_DEFER_ALL
 #define VN_DEFER_ALL 0      // byte-mark kernels: deferring spills them (VGPRs) -- measured slower
@@ -1534,8 +1534,9 @@ __global__ __launch_bounds__(PCM ? VN_PC_BLOCK : BLOCK, PCM ? VN_PC_MIN_WAVES : 
         store_rewards();
     }
     } else {
-    // byte-mark kernels: the step's outputs are stored within the step (the
-    // deferred order needs more VGPRs than these kernels have at 4 waves/SIMD)
+    // the step's outputs stored within the step (measured faster than the
+    // deferred order, which also needs more VGPRs than the byte-mark kernels
+    // have at 4 waves/SIMD)
     for (int k = 0; k < p.K;) {
     const uint64_t tb = p.t0 + (uint64_t)k;
     uint32_t acts = 0;                                    // 4 actions, 8 bits each, by (t & 3)
@@ -1578,12 +1579,22 @@ __global__ __launch_bounds__(PCM ? VN_PC_BLOCK : BLOCK, PCM ? VN_PC_MIN_WAVES : 
                 g.y += (dir == 2) - (dir == 3);
                 g.z += (dir == 4) - (dir == 5);
             }
+            // the step's loads, all in flight together: entering window
+            // column (and plane set), the new cell's ray record, its plane rows
             const bool shifted = moved && dir < 4;
             ShiftLoad<PH> sl;
+            SetLoad pl;
             if (shifted) tile_shift_issue<PH>(p, map, tile, dir, g.x, g.y, R, dirty, q, sl);
+            if (PC && shifted) pset_shift_issue(p, map, ps, dir, g.x, g.y, R, pdirty, q, pl);
             const uint2 rec = p.rays[R.ray_off + (uint32_t)((g.x * R.D + g.y) * R.H + g.z)];
-            plane_prefetch<PH>(p, map, pc_, g.x, g.y, g.z, q);
-            if (shifted) dirty = tile_shift_commit<PH>(tile, sl, dirty);
+            if (!PC) plane_prefetch<PH>(p, map, pc_, g.x, g.y, g.z, q);
+            if (shifted) {
+                if constexpr (PC) {
+                    pdirty = pset_shift_commit(ps, pl, pdirty, q);
+                    if (sl.in) sl.c.w[0] |= pset_known(ps, sl.ex, sl.ey);
+                }
+                dirty = tile_shift_commit<PH>(tile, sl, dirty);
+            }
 
             bool explored = false;
             const ObsDst dst{p.obs + row * VN_OBS_DIM,
@@ -1636,10 +1647,18 @@ __global__ __launch_bounds__(PCM ? VN_PC_BLOCK : BLOCK, PCM ? VN_PC_MIN_WAVES : 
         if (VN_STAGE_OBS && !(VN_ABLATE & 16u)) {
             const float4 *ws4 = reinterpret_cast<const float4 *>(wst);
             float4 *dst4 = reinterpret_cast<float4 *>(p.obs + ((size_t)k * p.N + wave_agent0) * VN_OBS_DIM);
+            if constexpr (PC) {
 #pragma unroll 1
-            for (int jj = 0; jj < (64 / GROUP) * (VN_OBS_DIM / 4) / 64; ++jj) {
-                const int f = lane + 64 * jj;
-                if (f < nvalid) obs_store(dst4 + f, ws4[f]);
+                for (int jj = 0; jj < (64 / GROUP) * (VN_OBS_DIM / 4) / 64; ++jj) {
+                    const int f = lane + 64 * jj;
+                    if (f < nvalid) obs_store(dst4 + f, stage_float4(wst, tab, f));
+                }
+            } else {
+#pragma unroll
+                for (int jj = 0; jj < (64 / GROUP) * (VN_OBS_DIM / 4) / 64; ++jj) {
+                    const int f = lane + 64 * jj;
+                    if (f < nvalid) obs_store(dst4 + f, ws4[f]);
+                }
             }
         }
     }
