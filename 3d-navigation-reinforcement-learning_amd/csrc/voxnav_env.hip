@@ -1649,7 +1649,10 @@ __global__ __launch_bounds__(PCM ? VN_PC_BLOCK : BLOCK, PCM ? VN_PC_MIN_WAVES : 
             const float4 *ws4 = reinterpret_cast<const float4 *>(wst);
             float4 *dst4 = reinterpret_cast<float4 *>(p.obs + ((size_t)k * p.N + wave_agent0) * VN_OBS_DIM);
             if constexpr (PC) {
-#pragma unroll 1
+#ifndef VN_PC_FLUSH_UNROLL
+#define VN_PC_FLUSH_UNROLL 1
+#endif
+#pragma unroll VN_PC_FLUSH_UNROLL
                 for (int jj = 0; jj < (64 / GROUP) * (VN_OBS_DIM / 4) / 64; ++jj) {
                     const int f = lane + 64 * jj;
                     if (f < nvalid) obs_store(dst4 + f, stage_float4(wst, tab, f));
