@@ -111,7 +111,12 @@ class _DualLSTM(torch.autograd.Function):
             dx = (dGf[0] @ w_ih_a + dGf[1] @ w_ih_c).view(L, B, D)
         dh0 = dh.clone() if need_h0 else None
         dc0 = dc.clone() if ctx.needs_input_grad[2] else None
-        return dx, dh0, dc0, d_w_ih_a, d_w_hh[0], db[0], db[0], d_w_ih_c, d_w_hh[1], db[1], db[1]
+        # b_ih and b_hh get the same gradient, but as separate tensors:
+        # autograd may keep an incoming gradient as the leaf's .grad without
+        # copying, and the in-place grad clipping would then scale a shared
+        # tensor twice
+        return (dx, dh0, dc0, d_w_ih_a, d_w_hh[0], db[0].clone(), db[0].clone(), d_w_ih_c, d_w_hh[1],
+                db[1].clone(), db[1].clone())
 
 
 def dual_lstm(policy, x: torch.Tensor, h0: torch.Tensor, c0: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
