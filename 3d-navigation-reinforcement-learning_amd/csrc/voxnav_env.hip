@@ -2703,6 +2703,29 @@ int launch_env(VnEnv *e, const Params &p, hipStream_t s) {
     return launch_ph<32, RESET_ONLY, 0>(e->N, s, p);
 }
 
+// The kernel instantiation launch_env picks for a call shape (diagnostics /
+// bench labels); kept next to launch_env so the two selections agree.
+std::string kernel_label(const VnEnv *e, bool reset_only, bool ext, bool fast, int k_steps) {
+    char buf[160];
+    if (e->variant == VN_VARIANT_SIMPLE) {
+        const int L = e->cfg.local_map_length;
+        const int lmax = L <= 4 ? 4 : L <= 8 ? 8 : L <= 10 ? 10 : 16;
+        if (!reset_only && e->sbits && e->sb_split)
+            std::snprintf(buf, sizeof(buf), "simple_split_kernel<%d>", lmax);
+        else if (e->sbits)
+            std::snprintf(buf, sizeof(buf), "simple_bits_kernel<%s, %d>", reset_only ? "true" : "false", lmax);
+        else
+            std::snprintf(buf, sizeof(buf), "simple_kernel<%s>", reset_only ? "true" : "false");
+        return buf;
+    }
+    (void)k_steps;
+    const int pcm = e->ph == 8 ? e->pcache : 0;
+    const bool x = !reset_only && ext, f = !reset_only && fast;
+    std::snprintf(buf, sizeof(buf), "env_kernel<%d, %s, %s, %s, %d>", e->ph, x ? "true" : "false",
+                  f ? "true" : "false", reset_only ? "true" : "false", pcm);
+    return buf;
+}
+
 void free_env(VnEnv *e) {
     if (!e) return;
     (void)hipFree(e->d_rooms);
@@ -3062,6 +3085,14 @@ int vn_step_random(VnEnv *env, uint64_t policy_seed, uint64_t t0, int32_t k_step
     p.trunc = truncated;
     p.terminal_obs = terminal_obs;
     return launch_env<false>(env, p, (hipStream_t)stream);
+}
+
+int vn_kernel_label(const VnEnv *env, int32_t k_steps, int32_t explicit_actions, int32_t fast, char *buf,
+                    int32_t len) {
+    if (!env || !buf || len < 1) return fail(VN_ERR_INVALID, "NULL argument");
+    const std::string s = kernel_label(env, k_steps == 0, explicit_actions != 0, fast != 0, k_steps);
+    std::snprintf(buf, (size_t)len, "%s", s.c_str());
+    return (int)s.size() < len ? VN_OK : fail(VN_ERR_INVALID, "buffer too small (%d)", (int)len);
 }
 
 int vn_export_state(VnEnv *env, int64_t *state_out, void *stream) {

@@ -64,6 +64,7 @@ _SIGS = {
     "vn_step": (C.c_int, [P, P, P, P, P, P, P, P, P]),
     "vn_step_random": (C.c_int, [P, C.c_uint64, C.c_uint64, C.c_int32, P, P, P, P, P, P, P, P]),
     "vn_export_state": (C.c_int, [P, P, P]),
+    "vn_kernel_label": (C.c_int, [P, C.c_int32, C.c_int32, C.c_int32, C.c_char_p, C.c_int32]),
     "vn_export_belief": (C.c_int, [P, P, P]),
     "vn_gae": (C.c_int, [P, P, P, P, P, C.c_int32, C.c_int32, C.c_double, C.c_double, P, P, P]),
     "vn_lstm_cell": (C.c_int, [P, C.c_int64, P, P, P, P, P, P, P, C.c_int32, C.c_int32, C.c_int32, P]),

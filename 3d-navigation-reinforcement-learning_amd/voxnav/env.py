@@ -229,6 +229,14 @@ class BatchedGridEnv:
         self._t = int(t0) + K
         return Rollout(obs, rew, te, tr, act)
 
+    def kernel_label(self, k_steps: int = 16, explicit_actions: bool = False, fast: bool = True) -> str:
+        """Name of the kernel instantiation a step call of this shape launches
+        (``k_steps=0``: reset; ``fast``: the rollout-buffer call)."""
+        buf = C.create_string_buffer(160)
+        _native.check(self.lib.vn_kernel_label(self._h, int(k_steps), int(bool(explicit_actions)), int(bool(fast)),
+                                               buf, 160), "vn_kernel_label")
+        return buf.value.decode()
+
     def export_state(self) -> torch.Tensor:
         out = torch.empty((self.num_agents, _native.VN_STATE_FIELDS), dtype=torch.int64, device=self.device)
         _native.check(self.lib.vn_export_state(self._h, _ptr(out), self._stream()), "vn_export_state")

@@ -11,22 +11,32 @@ random.choice over the one-room set), local_map_length L=10
 timed region; every step writes the full obs [N,80] f32, reward, terminated
 and truncated tensors.
 
-One "step" = one batched env step of all agents on the GPU; the default
-timed window is 5,408 steps, one full episode of the 32x32x8 box
-(episodes truncate at total_free_cells = 5,400 steps), so the number is the
-episode-average throughput rather than one phase of it.  ``--fuse F``
-advances F steps per kernel launch (obs written for every step into a
-[F, N, 80] trajectory buffer, i.e. the rollout-buffer shape); F=1 is the
-drop-in VecEnv.step call.
+One "step" = one batched env step of all agents on the GPU.  The headline
+resets a fresh env, runs exactly ``--warmup`` untimed steps, then times
+exactly ``--steps`` steps (launches of ``--fuse`` F steps into a [F, N, 80]
+rollout-chunk buffer; the last launch of each phase takes the remainder).
+``roofline`` is computed from the same timed launches (HIP events on the
+launch stream) and ``traffic`` from the PMC record of the same window
+(profiles/pmc_traffic.json, keyed by room/L/N/F/warmup/steps).  When the
+timed window is shorter than one whole 5,400-step episode of the 32x32x8
+box, ``episode_window`` adds the same measurement over one full episode
+from t=0 (every phase: early exploration, steady state, auto-reset).
+
+``--gpus N`` (N > 1) without a launcher environment starts N ranks itself
+(torch.distributed.run, one process per GPU, before any GPU call) and exits
+with their status; every rank owns 65,536 agents with global ids (no
+collective in the step), the timing is max-over-ranks, and the collector
+leg all-gathers its trajectory buffers over RCCL at the rollout boundary.
 
 Usage:  python bench.py [--gpus N] [--steps K] [--warmup W] [--fuse F]
-For N>1 launch one rank per GPU with torch.distributed.run.
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 from pathlib import Path
@@ -36,6 +46,7 @@ sys.path.insert(0, str(REPO / "3d-navigation-reinforcement-learning_amd"))
 
 METRIC = "env-steps/sec at 65536 parallel agents, 32×32×8 room, 1/2/4/8 MI355X"
 HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: 8.0 TB/s spec
+EPISODE_WINDOW = 5408   # one whole 5,400-step episode of the 32x32x8 box, in F=16 launches
 
 
 def algorithmic_bytes_per_step(L: int) -> int:
@@ -43,37 +54,69 @@ def algorithmic_bytes_per_step(L: int) -> int:
     return 1 + 64 + 6 * L + 32 + 320 + 4 + 2
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    # 5408 = one whole 5,400-step episode of the 32x32x8 box (every agent
-    # starts at t=0): the timed window covers every phase of an episode,
-    # early exploration, steady state and the auto-reset
-    ap.add_argument("--steps", type=int, default=5408)
+    ap.add_argument("--steps", type=int, default=EPISODE_WINDOW)
     ap.add_argument("--warmup", type=int, default=32)
     ap.add_argument("--agents", type=int, default=65536, help="agents per GPU")
     ap.add_argument("--room", default="32x32x8", help="WxDxH of the walled-box room")
     ap.add_argument("--L", type=int, default=10, help="local_map_length")
     ap.add_argument("--fuse", type=int, default=16, help="env steps per kernel launch (headline)")
+    ap.add_argument("--episode-window", type=int, default=1,
+                    help="when --steps < one episode, also time one whole episode (5,408 steps)")
     ap.add_argument("--single-step-check", type=int, default=1,
                     help="also time the drop-in one-step-per-launch call (vn_step_random k=1)")
-    ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline sample budget (0 = skip)")
+    ap.add_argument("--cpu-seconds", type=float, default=8.0,
+                    help="CPU baseline sample per leg in seconds (0 = skip)")
     ap.add_argument("--simple", type=int, default=1,
                     help="also time the simpleEnv variant (envs/simpleEnv.py) on the same agents/room, L=4")
-    ap.add_argument("--collector", default="lstm", choices=["lstm", "mlp", "none"],
-                    help="also time the policy-in-the-loop rollout collector (PPO-LSTM / PPO-MLP)")
-    ap.add_argument("--collector-rooms", default="P3_training", help="reference room set for the collector leg")
+    ap.add_argument("--collector", default="lstm,mlp",
+                    help="policy-in-the-loop rollout collector legs: any of lstm (PPO-LSTM, P3_training, "
+                         "BASELINE config C4) and mlp (PPO-MLP, P2_training, config C3), or none")
     ap.add_argument("--collector-T", type=int, default=128, help="rollout length (n_steps) of the collector leg")
     ap.add_argument("--collector-rollouts", type=int, default=2, help="timed rollouts of the collector leg")
     ap.add_argument("--collector-bf16", type=int, default=1,
-                    help="also time the collector with bf16 policy GEMMs (the reference's policy is f32)")
+                    help="also time the PPO-LSTM collector with bf16 policy GEMMs (the reference's policy is f32)")
     ap.add_argument("--learner-batch", type=int, default=65536,
-                    help="PPO learner leg: minibatch size (0 = skip); runs on the f32 PPO-LSTM collector's buffer")
+                    help="PPO learner legs: minibatch size (0 = skip); run on each f32 collector's buffer")
     ap.add_argument("--learner-minibatches", type=int, default=16, help="timed learner minibatch updates")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="launch/rendezvous rehearsal without a GPU: ranks init gloo, time a barrier, print the line")
     ap.add_argument("--json-out", default=None)
-    return ap.parse_args()
+    return ap.parse_args(argv)
 
 
+# ---------------------------------------------------------------- launch
+def _free_port() -> int:
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(args) -> int:
+    """``--gpus N`` without a launcher: start N ranks (one process per GPU)
+    through torch.distributed.run as a child process -- nothing here has
+    touched the GPU -- and return their exit status.  This replaces the
+    reference's process-level env parallelism (train/Grid_Train.py:191-192)."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr", "127.0.0.1", f"--master-port={_free_port()}", str(Path(__file__).resolve())]
+    cmd += sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    return subprocess.call(cmd, env=env)
+
+
+def launches(total: int, F: int):
+    """Launch sizes covering exactly ``total`` steps: F-step launches, the
+    remainder last."""
+    out = [F] * (total // F)
+    if total % F:
+        out.append(total % F)
+    return out
+
+
+# ---------------------------------------------------------------- CPU baseline
 def cpu_model() -> str:
     try:
         for line in open("/proc/cpuinfo"):
@@ -84,17 +127,43 @@ def cpu_model() -> str:
     return "unknown"
 
 
-def cpu_baseline(room_whd, L, seconds, threads_override=None):
-    """The CPU oracle (C restatement of envs/CubicEnv.py step/reset) on the
-    host cores, same room / L / policy / seed schedule, bounded sample."""
+def host_cores() -> int:
+    """CPU share of this job: the affinity set, capped by OMP_NUM_THREADS
+    (the GPU box exposes the whole machine's CPUs but gives a job 16)."""
+    cores = len(os.sched_getaffinity(0))
+    return max(1, min(cores, int(os.environ.get("OMP_NUM_THREADS", cores))))
+
+
+def python_numpy_baseline(room, L, seconds, procs):
+    """The reference's Python/NumPy step loop in its SubprocVecEnv shape
+    (train/Grid_Train.py:191-192: one env per process): ``procs`` processes
+    of oracle/py_cubic.py (a per-agent restatement of envs/CubicEnv.py, the
+    reference itself cannot travel to this box), each one env under a
+    uniform random policy with auto-reset, all stepping between the same two
+    wall-clock instants.  Returns aggregate env-steps/s."""
+    start = time.time() + 1.5 + 0.02 * procs   # let every child import numpy first
+    stop = start + seconds
+    ps = [subprocess.Popen([sys.executable, "-m", "oracle.py_cubic", "--room", room, "--L", str(L),
+                            "--seed", str(42 + i), "--start-at", repr(start), "--stop-at", repr(stop)],
+                           cwd=str(REPO), stdout=subprocess.PIPE, text=True) for i in range(procs)]
+    steps = episodes = 0
+    for p in ps:
+        out, _ = p.communicate(timeout=seconds + 120)
+        if p.returncode != 0:
+            raise RuntimeError("python baseline child failed")
+        rec = json.loads(out.strip().splitlines()[-1])
+        steps += rec["steps"]
+        episodes += rec["episodes"]
+    return steps / (stop - start), steps, episodes
+
+
+def c_port_baseline(room_whd, L, seconds, threads):
+    """The C restatement (oracle/voxnav_oracle.c) of the same workload,
+    OpenMP over agents: a second, stronger CPU reference point."""
     import numpy as np
     sys.path.insert(0, str(REPO))
     from oracle.oracle import OracleEnv, parse_room_text
     from voxnav.rooms import box_room, room_to_text
-    cores = len(os.sched_getaffinity(0))
-    threads = max(1, min(cores, int(os.environ.get("OMP_NUM_THREADS", cores))))
-    if threads_override is not None:
-        threads = int(threads_override)
     N = 512 * threads
     W, D, H = room_whd
     env = OracleEnv([parse_room_text(room_to_text(box_room(W, D, H)))], n_agents=N, local_map_length=L,
@@ -111,11 +180,38 @@ def cpu_baseline(room_whd, L, seconds, threads_override=None):
         if el >= seconds:
             break
         k = min(1024, k * 2)
-    return {"value": steps / el, "unit": "env-steps/s", "cores": threads, "kind": "port",
-            "sample": f"{N} agents x {steps // N} steps of the same workload ({el:.1f} s) through "
-                      f"oracle/voxnav_oracle.c (C restatement of envs/CubicEnv.py, OpenMP over agents)"}
+    return steps / el, N, steps // N, el
 
 
+def cpu_baseline(room_whd, L, seconds):
+    W, D, H = room_whd
+    room = f"{W}x{D}x{H}"
+    P = host_cores()
+    v, steps, ep = python_numpy_baseline(room, L, seconds, P)
+    v1, steps1, _ = python_numpy_baseline(room, L, max(2.0, seconds / 2), 1)
+    cv, cn, ck, cel = c_port_baseline(room_whd, L, seconds, P)
+    cv1, _, _, _ = c_port_baseline(room_whd, L, max(2.0, seconds / 4), 1)
+    rec = {"value": round(v, 1), "unit": "env-steps/s", "cores": P, "kind": "port",
+           "sample": f"{P} processes x 1 env (SubprocVecEnv shape), {steps} env-steps in {seconds:.0f} s, "
+                     f"{ep} auto-resets: oracle/py_cubic.py, a per-agent Python/NumPy restatement of "
+                     f"envs/CubicEnv.py (pinned bit-exact to the reference's golden trajectories), "
+                     f"{room} box, L={L}, uniform random actions",
+           "single_core_value": round(v1, 1), "cpu_model": cpu_model(),
+           "c_openmp_port": {"value": round(cv, 1), "single_core_value": round(cv1, 1), "threads": P,
+                             "sample": f"{cn} agents x {ck} steps ({cel:.1f} s) through oracle/voxnav_oracle.c "
+                                       f"(C restatement of envs/CubicEnv.py, OpenMP over agents)"}}
+    cal = REPO / "profiles" / "py_baseline_calibration.json"
+    if cal.exists():
+        c = json.loads(cal.read_text())
+        rec["reference_calibration"] = {
+            "restatement_over_reference": c["restatement_over_reference"],
+            "reference_single_core_build_container": c["reference_envs_CubicEnv_steps_per_s"],
+            "source": "tests/golden/calibrate_py_baseline.py: the unmodified envs/CubicEnv.py vs "
+                      "oracle/py_cubic.py, one process each, build container " + c.get("cpu_model", "")}
+    return rec
+
+
+# ---------------------------------------------------------------- policy legs
 def simple_bytes_per_step(L: int) -> int:
     """simpleEnv variant: action 1 + ray cells 6L + state 2*16 + goal 4 +
     obs 4*(6L+7) + reward 4 + flags 2."""
@@ -143,17 +239,27 @@ def mlp_flops_per_agent_step(obs=80, arch=(256, 256, 128), A=6) -> int:
     return 2 * macs
 
 
-def collector_leg(args, torch, dist, dev, rank, world, N, dtype="f32"):
-    """Policy-in-the-loop rollouts (RecurrentPPO.collect_rollouts + GAE) on
-    the GPU: BASELINE.json config C4 shape (P3_training rooms, PPO-LSTM,
-    seq 128) at N agents per GPU.  One untimed rollout, then timed ones."""
+def _max_over_ranks(torch, dist, dev, world, *vals):
+    if world == 1:
+        return vals
+    t = torch.tensor(list(vals), dtype=torch.float64, device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return tuple(float(v) for v in t.tolist())
+
+
+def collector_leg(args, torch, dist, dev, rank, world, N, kind, dtype="f32"):
+    """Policy-in-the-loop rollouts (RecurrentPPO / PPO collect_rollouts +
+    GAE) on the GPU at N agents per GPU: kind "lstm" = BASELINE config C4
+    (P3_training rooms, PPO-LSTM, seq 128), "mlp" = config C3 (P2_training,
+    PPO-MLP).  One untimed rollout, then timed ones; then the learner."""
     from voxnav.collector import RolloutCollector
     from voxnav.env import BatchedGridEnv
     from voxnav.policy import ActorCriticPolicy, RecurrentActorCriticPolicy
     from voxnav.rooms import load_archive_set
-    rooms = load_archive_set(args.collector_rooms)
+    rooms_name = "P3_training" if kind == "lstm" else "P2_training"
+    rooms = load_archive_set(rooms_name)
     torch.manual_seed(42)
-    pol = (RecurrentActorCriticPolicy() if args.collector == "lstm" else ActorCriticPolicy()).to(dev)
+    pol = (RecurrentActorCriticPolicy() if kind == "lstm" else ActorCriticPolicy()).to(dev)
     env = BatchedGridEnv(num_agents=N, rooms=rooms, local_map_length=args.L, autoreset=True, device=dev,
                          agent_id_base=rank * N, seed_stride=N * world)
     col = RolloutCollector(env, pol, n_steps=args.collector_T, sample_seed=42, reset_seed=42, policy_dtype=dtype)
@@ -167,33 +273,30 @@ def collector_leg(args, torch, dist, dev, rank, world, N, dtype="f32"):
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
-    el = time.perf_counter() - t0
-    if world > 1:
-        t = torch.tensor([el], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        el = float(t[0].item())
+    el, = _max_over_ranks(torch, dist, dev, world, time.perf_counter() - t0)
     assert torch.isfinite(buf.advantages).all().item()
     gather = None
     if world > 1 and dtype == "f32" and dist.get_backend() == "nccl":   # not under the gloo rehearsal knob
         gather = allgather_leg(torch, dist, dev, rank, world, buf)
     learner = None
-    if dtype == "f32" and args.collector == "lstm" and args.learner_batch > 0:
-        learner = learner_leg(args, torch, dist, dev, world, pol, buf)
+    if dtype == "f32" and args.learner_batch > 0:
+        learner = learner_leg(args, torch, dist, dev, world, pol, buf, kind)
     steps = args.collector_T * args.collector_rollouts
-    fl = lstm_flops_per_agent_step() if args.collector == "lstm" else mlp_flops_per_agent_step()
+    fl = lstm_flops_per_agent_step() if kind == "lstm" else mlp_flops_per_agent_step()
     tflops = fl * N * steps / el / 1e12
-    name = ("PPO-LSTM (MlpLstmPolicy: actor+critic LSTM 256, pi/vf [256,256,128] Tanh)" if args.collector == "lstm"
+    name = ("PPO-LSTM (MlpLstmPolicy: actor+critic LSTM 256, pi/vf [256,256,128] Tanh)" if kind == "lstm"
             else "PPO-MLP (MlpPolicy: pi/vf [256,256,128] Tanh)")
     peak = 157.3 if dtype == "f32" else 2500.0     # dense MFMA peak for the GEMM dtype (MI355X_MICROARCH.md)
     env.close()
     del col, env
     out = {"value": round(N * world * steps / el, 1), "unit": "env-steps/s", "policy": name, "dtype": dtype,
-            "rooms": args.collector_rooms, "agents_per_gpu": N, "rollout_steps": args.collector_T,
-            "timed_rollouts": args.collector_rollouts, "ms_per_step": round(el * 1e3 / steps, 4),
-            "includes": "policy forward, Categorical draw, env step + auto-reset, truncation bootstrap, "
-                        "LSTM-state buffer stores, last values, GAE",
-            "policy_flops_per_agent_step": fl, "policy_tflops": round(tflops, 2),
-            "policy_frac_of_mfma_peak": round(tflops / peak, 4), "mfma_peak_tflops": peak}
+           "config": "C4" if kind == "lstm" else "C3",
+           "rooms": rooms_name, "agents_per_gpu": N, "rollout_steps": args.collector_T,
+           "timed_rollouts": args.collector_rollouts, "ms_per_step": round(el * 1e3 / steps, 4),
+           "includes": "policy forward, Categorical draw, env step + auto-reset, truncation bootstrap, "
+                       + ("LSTM-state buffer stores, " if kind == "lstm" else "") + "last values, GAE",
+           "policy_flops_per_agent_step": fl, "policy_tflops": round(tflops, 2),
+           "policy_frac_of_mfma_peak": round(tflops / peak, 4), "mfma_peak_tflops": peak}
     if learner is not None:
         out["learner"] = learner
     if gather is not None:
@@ -247,11 +350,12 @@ def allgather_leg(torch, dist, dev, rank, world, buf, reps=3):
             "collective": "all_gather_into_tensor per buffer (RCCL over xGMI)", "reps": reps}
 
 
-def learner_leg(args, torch, dist, dev, world, pol, buf):
-    """PPO learner: sb3_contrib RecurrentPPO.train
-    minibatch updates (packed-sequence LSTM re-run, clipped surrogate, value
-    MSE, entropy, grad clip, Adam; gradient all-reduce over RCCL when N>1)
-    on the collector's buffer.  Timed over a bounded number of minibatches."""
+def learner_leg(args, torch, dist, dev, world, pol, buf, kind):
+    """PPO learner: RecurrentPPO.train (kind lstm:
+    packed-sequence LSTM re-run) / PPO.train (kind mlp) minibatch updates --
+    clipped surrogate, value MSE, entropy, grad clip, Adam; gradient
+    all-reduce over RCCL when N>1 -- on the collector's buffer, timed over a
+    bounded number of minibatches."""
     from voxnav.ppo import PPOLearner
     T, N = buf.actions.shape
     B = min(args.learner_batch, T * N)
@@ -259,6 +363,8 @@ def learner_leg(args, torch, dist, dev, world, pol, buf):
     ln = PPOLearner(pol, n_epochs=1, batch_size=B, seed=0,
                     process_group=dist.group.WORLD if world > 1 else None)
     perm = torch.roll(torch.arange(T * N, device=dev), -12345 % (T * N))
+    if kind == "mlp":
+        perm = torch.randperm(T * N, device=dev, generator=torch.Generator(device=dev).manual_seed(0))
     for m in range(2):
         ln.update(buf, perm[m * B:(m + 1) * B])
     torch.cuda.synchronize(dev)
@@ -270,34 +376,136 @@ def learner_leg(args, torch, dist, dev, world, pol, buf):
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
-    el = time.perf_counter() - t0
-    if world > 1:
-        t = torch.tensor([el], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        el = float(t[0].item())
+    el, = _max_over_ranks(torch, dist, dev, world, time.perf_counter() - t0)
     sps = n * B * world / el
-    fl = 3 * lstm_flops_per_agent_step()        # forward + backward ~ 3x forward
+    fl = 3 * (lstm_flops_per_agent_step() if kind == "lstm" else mlp_flops_per_agent_step())  # fwd + bwd ~ 3x fwd
+    inc = ("sequence packing, actor+critic LSTM re-run (dual-LSTM: library GEMMs + HIP cell kernels), MLPs, "
+           if kind == "lstm" else "minibatch gather, actor/critic MLPs, ")
     return {"value": round(sps, 1), "unit": "samples/s", "batch_size": B, "minibatches": n,
             "ms_per_minibatch": round(el * 1e3 / n, 3), "tflops": round(fl * sps / 1e12, 2),
-            "includes": "sequence packing, actor+critic LSTM re-run (dual-LSTM: library GEMMs + HIP cell kernels), MLPs, "
-                        "losses, backward, "
-                        "grad clip, Adam" + (", RCCL gradient all-reduce" if world > 1 else "")}
+            "includes": inc + "losses, backward, grad clip, Adam"
+            + (f", gradient all-reduce ({'RCCL' if dist.get_backend() == 'nccl' else dist.get_backend()})"
+               if world > 1 else "")}
+
+
+# ---------------------------------------------------------------- env window
+def time_window(torch, dist, dev, world, env, N, F, warmup, steps, policy_seed=42):
+    """Reset already done by the caller.  Run exactly ``warmup`` untimed
+    steps, then time exactly ``steps`` steps in launches of F (remainder
+    last).  Returns (elapsed_s max-over-ranks, kernel_ms_total max-over-ranks,
+    launch sizes, out)."""
+    from voxnav.env import Rollout
+    out = Rollout(torch.empty((F, N, env.obs_dim), dtype=torch.float32, device=dev),
+                  torch.empty((F, N), dtype=torch.float32, device=dev),
+                  torch.empty((F, N), dtype=torch.uint8, device=dev),
+                  torch.empty((F, N), dtype=torch.uint8, device=dev), None)
+
+    def view(k):
+        return Rollout(out.obs[:k], out.reward[:k], out.terminated[:k], out.truncated[:k], None)
+
+    for k in launches(warmup, F):
+        env.step_random(k, policy_seed=policy_seed, out=view(k))
+    timed = launches(steps, F)
+    stream = torch.cuda.current_stream(dev)
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in timed]
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for (a, b), k in zip(ev, timed):
+        a.record(stream)
+        env.step_random(k, policy_seed=policy_seed, out=view(k))
+        b.record(stream)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    kern_ms = sum(a.elapsed_time(b) for a, b in ev)
+    elapsed, kern_ms = _max_over_ranks(torch, dist, dev, world, elapsed, kern_ms)
+    return elapsed, kern_ms, timed, out
+
+
+def roofline_block(bstep, N, F, steps, timed, kern_ms, traffic_rec, kernel_label):
+    """Roofline of the dominant kernel over ONE window: algorithmic bytes of
+    the window's env-steps / the window's summed launch time.  Per-launch
+    figures are per F-step launch (window totals x F / steps)."""
+    achieved = bstep * N * steps / (kern_ms * 1e-3) / 1e9
+    full = [k for k in timed if k == F]
+    roof = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": None, "kernel": kernel_label,
+            "kernel_avg_us": round(kern_ms * 1e3 / len(timed), 3),
+            "kernel_us_per_F_launch": round(kern_ms * 1e3 * F / steps, 3),
+            "launches": len(timed), "full_launches": len(full), "steps_per_launch": F,
+            "algorithmic_bytes_per_env_step": bstep, "env_steps_per_launch": N * F}
+    if traffic_rec is not None:
+        roof["traffic"] = traffic_rec["hbm_bytes_per_launch"]
+        roof["traffic_bytes_per_env_step"] = round(traffic_rec["hbm_bytes_per_launch"] / (N * F), 1)
+        roof["traffic_source"] = traffic_rec.get("source")
+    return roof
+
+
+def traffic_for(W, D, H, L, N, F, warmup, steps):
+    prof = REPO / "profiles" / "pmc_traffic.json"
+    if not prof.exists():
+        return None
+    try:
+        pm = json.loads(prof.read_text())
+    except ValueError:
+        return None
+    return pm.get(f"{W}x{D}x{H}_L{L}_N{N}_F{F}_W{warmup}_K{steps}")
+
+
+# ---------------------------------------------------------------- main
+def dry_run(args, world, rank):
+    """Launch / rendezvous rehearsal on CPU (gloo): the --gpus N path up to
+    the first GPU call, with the bench's barrier + max-over-ranks timing."""
+    import torch
+    import torch.distributed as dist
+    if world > 1:
+        dist.init_process_group("gloo")
+    t0 = time.perf_counter()
+    if world > 1:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    ranks = [rank]
+    if world > 1:
+        t = torch.tensor([el], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+        got = [None] * world
+        dist.all_gather_object(got, rank)
+        ranks = got
+    if rank == 0:
+        print(json.dumps({"metric": METRIC, "value": None, "unit": "env-steps/s", "n_gpus": world, "steps": 0,
+                          "warmup": 0, "dry_run": True, "ranks": ranks, "barrier_s": el,
+                          "agents_global": args.agents * world}), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
 
 
 def main():
     args = parse()
-    import torch
-    import torch.distributed as dist
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(args))
+    if world != args.gpus:
+        raise SystemExit(f"--gpus {args.gpus} but the launcher started WORLD_SIZE={world} ranks")
+    if args.dry_run:
+        return dry_run(args, world, rank)
+    import torch
+    import torch.distributed as dist
     # rehearsal knob for the multi-rank path on a one-GPU box: every rank on
     # cuda:0 over gloo (RCCL refuses two ranks on one device); not for numbers
-    if os.environ.get("VOXNAV_BENCH_SHARED_DEVICE") == "1":
+    shared = os.environ.get("VOXNAV_BENCH_SHARED_DEVICE") == "1"
+    if shared:
         local = 0
     if world > 1:
+        if not shared and torch.cuda.device_count() < world:
+            raise SystemExit(f"--gpus {world} needs {world} visible GPUs, found {torch.cuda.device_count()}")
         torch.cuda.set_device(local)
-        if os.environ.get("VOXNAV_BENCH_SHARED_DEVICE") == "1":
+        if shared:
             dist.init_process_group("gloo")
         else:
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
@@ -310,123 +518,101 @@ def main():
     W, D, H = (int(v) for v in args.room.split("x"))
     N = args.agents
     F = max(1, args.fuse)
-    env = BatchedGridEnv(num_agents=N, rooms=single_room_set(box_room(W, D, H)), local_map_length=args.L,
-                         autoreset=True, device=dev, agent_id_base=rank * N, seed_stride=N * world)
-    env.reset(seed=42)
-    from voxnav.env import Rollout
+    if args.steps < 1 or args.warmup < 0:
+        raise SystemExit("--steps must be >= 1 and --warmup >= 0")
+    bstep = algorithmic_bytes_per_step(args.L)
 
-    def run(F, steps, warmup, env=env):
-        out = Rollout(torch.empty((F, N, env.obs_dim), dtype=torch.float32, device=dev),
-                      torch.empty((F, N), dtype=torch.float32, device=dev),
-                      torch.empty((F, N), dtype=torch.uint8, device=dev),
-                      torch.empty((F, N), dtype=torch.uint8, device=dev), None)
-        launches_w = max(1, warmup // F)
-        launches = max(1, steps // F)
-        for _ in range(launches_w):
-            env.step_random(F, policy_seed=42, out=out)
-        stream = torch.cuda.current_stream(dev)
-        ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(launches)]
-        if world > 1:
-            dist.barrier()
-        torch.cuda.synchronize(dev)
-        t0 = time.perf_counter()
-        for i in range(launches):
-            ev[i][0].record(stream)
-            env.step_random(F, policy_seed=42, out=out)
-            ev[i][1].record(stream)
-        torch.cuda.synchronize(dev)
-        if world > 1:
-            dist.barrier()
-        elapsed = time.perf_counter() - t0
-        kern_ms = sum(a.elapsed_time(b) for a, b in ev) / launches
-        if world > 1:
-            t = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device=dev)
-            dist.all_reduce(t, op=dist.ReduceOp.MAX)
-            elapsed, kern_ms = float(t[0].item()), float(t[1].item())
-        return out, launches_w * F, launches * F, elapsed, kern_ms
+    def make_env(L=args.L, variant="cubic"):
+        e = BatchedGridEnv(num_agents=N, rooms=single_room_set(box_room(W, D, H)), local_map_length=L,
+                           autoreset=True, device=dev, agent_id_base=rank * N, seed_stride=N * world,
+                           variant=variant)
+        e.reset(seed=42)
+        return e
+
+    # headline: a fresh env, exactly W warmup + K timed steps
+    env = make_env()
+    label = env.kernel_label(F)
+    elapsed, kern_ms, timed, out = time_window(torch, dist, dev, world, env, N, F, args.warmup, args.steps)
+    assert torch.isfinite(out.obs).all().item()   # the trajectory buffer holds real observations
+    env.close()
+    del env, out
+    roof = roofline_block(bstep, N, F, args.steps, timed, kern_ms,
+                          traffic_for(W, D, H, args.L, N, F, args.warmup, args.steps), label)
+    value = N * world * args.steps / elapsed
+
+    episode = None
+    if args.episode_window and args.steps < EPISODE_WINDOW:
+        env = make_env()
+        e_el, e_km, e_timed, _ = time_window(torch, dist, dev, world, env, N, F, 32, EPISODE_WINDOW)
+        env.close()
+        del env
+        episode = {"value": round(N * world * EPISODE_WINDOW / e_el, 1), "unit": "env-steps/s",
+                   "warmup": 32, "steps": EPISODE_WINDOW,
+                   "ms_per_step": round(e_el * 1e3 / EPISODE_WINDOW, 5),
+                   "window": "one whole 5,400-step episode of every agent from t=0 (incl. the auto-reset)",
+                   "roofline": roofline_block(bstep, N, F, EPISODE_WINDOW, e_timed, e_km,
+                                              traffic_for(W, D, H, args.L, N, F, 32, EPISODE_WINDOW), label)}
 
     single = None
     if args.single_step_check and F != 1:
-        _, _, st1, el1, km1 = run(1, min(args.steps, 100), 10)
-        single = {"value": round(N * world * st1 / el1, 1), "steps": st1, "kernel_avg_us": round(km1 * 1e3, 3)}
-    out, warm_steps, steps_timed, elapsed, kern_ms = run(F, args.steps, args.warmup)
+        env = make_env()
+        s_el, s_km, s_timed, _ = time_window(torch, dist, dev, world, env, N, 1, 10, 100)
+        single = {"value": round(N * world * 100 / s_el, 1), "steps": 100, "warmup": 10,
+                  "kernel_avg_us": round(s_km * 1e3 / len(s_timed), 3),
+                  "kernel": env.kernel_label(1)}
+        env.close()
+        del env
+
     simple = None
     if args.simple:
-        senv = BatchedGridEnv(num_agents=N, rooms=single_room_set(box_room(W, D, H)), local_map_length=4,
-                              autoreset=True, device=dev, agent_id_base=rank * N, seed_stride=N * world,
-                              variant="simple")
-        senv.reset(seed=42)
-        _, _, st_s, el_s, km_s = run(F, args.steps, args.warmup, env=senv)
+        senv = make_env(L=4, variant="simple")
+        st_steps = max(args.steps, EPISODE_WINDOW if args.episode_window else 0)
+        s_el, s_km, s_timed, _ = time_window(torch, dist, dev, world, senv, N, F, 32, st_steps)
         sb = simple_bytes_per_step(4)
-        sach = sb * N * F / (km_s * 1e-3) / 1e9
-        simple = {"value": round(N * world * st_s / el_s, 1), "unit": "env-steps/s", "variant": "envs/simpleEnv.py",
-                  "room": f"{W}x{D}x{H}", "local_map_length": 4, "steps": st_s, "steps_per_launch": F,
-                  "kernel_avg_us": round(km_s * 1e3, 3),
+        sach = sb * N * st_steps / (s_km * 1e-3) / 1e9
+        simple = {"value": round(N * world * st_steps / s_el, 1), "unit": "env-steps/s",
+                  "variant": "envs/simpleEnv.py", "room": f"{W}x{D}x{H}", "local_map_length": 4, "warmup": 32,
+                  "steps": st_steps, "steps_per_launch": F, "kernel_avg_us": round(s_km * 1e3 / len(s_timed), 3),
+                  "kernel": senv.kernel_label(F),
                   "roofline": {"bound": "hbm", "achieved": round(sach, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                                "frac": round(sach / HBM_PEAK_GBS, 5), "algorithmic_bytes_per_env_step": sb}}
         senv.close()
         del senv
-    coll = coll_bf = None
-    if args.collector != "none":
-        coll = collector_leg(args, torch, dist, dev, rank, world, N)
-        if args.collector_bf16:
-            coll_bf = collector_leg(args, torch, dist, dev, rank, world, N, dtype="bf16")
 
-    # sanity: the trajectory buffer holds real observations
-    assert torch.isfinite(out.obs).all().item()
-
-    total_steps = N * world * steps_timed
-    value = total_steps / elapsed
-    bstep = algorithmic_bytes_per_step(args.L)
-    achieved = bstep * N * F / (kern_ms * 1e-3) / 1e9
-    roof = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": None,
-            "kernel": "env_kernel<PH=8,EXT=false,FAST=true,RESET_ONLY=false,PCM=2> (plane-set mode)",
-            "kernel_avg_us": round(kern_ms * 1e3, 3),
-            "algorithmic_bytes_per_env_step": bstep, "env_steps_per_launch": N * F}
-    prof = REPO / "profiles" / "pmc_traffic.json"
-    if prof.exists():
-        try:
-            pm = json.loads(prof.read_text())
-            key = f"{W}x{D}x{H}_L{args.L}_N{N}_F{F}"
-            if key in pm:
-                roof["traffic"] = pm[key]["hbm_bytes_per_launch"]
-                roof["traffic_source"] = pm[key].get("source")
-        except Exception:  # noqa: BLE001
-            pass
+    legs = {}
+    kinds = [k for k in args.collector.split(",") if k and k != "none"]
+    for kind in kinds:
+        if kind not in ("lstm", "mlp"):
+            raise SystemExit(f"--collector: unknown leg {kind!r}")
+        legs[f"collector_{kind}"] = collector_leg(args, torch, dist, dev, rank, world, N, kind)
+        if kind == "lstm" and args.collector_bf16:
+            legs["collector_lstm_bf16"] = collector_leg(args, torch, dist, dev, rank, world, N, kind, dtype="bf16")
 
     if rank == 0:
         rec = {
             "metric": METRIC, "value": round(value, 1), "unit": "env-steps/s", "n_gpus": world,
-            "steps": steps_timed, "warmup": warm_steps, "ms_per_step": round(elapsed * 1e3 / steps_timed, 5),
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(elapsed * 1e3 / args.steps, 5),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "int8",
             "data": "synthetic (walled-box room in the reference room-file grammar; Philox uniform random policy)",
             "config": {"workload": f"C3 env step: {N} agents/GPU, {W}x{D}x{H} room, L={args.L}, "
                                    f"random policy, SB3 auto-reset", "agents_per_gpu": N,
                        "global_agents": N * world, "room": f"{W}x{D}x{H}", "local_map_length": args.L,
-                       "steps_per_launch": F, "parallelism": f"agent-sharded x{world} (no collective in the step)"},
+                       "steps_per_launch": F,
+                       "window": f"fresh env, {args.warmup} untimed steps, then exactly {args.steps} timed steps "
+                                 f"in {len(timed)} launches (episode steps {args.warmup + 1}-"
+                                 f"{args.warmup + args.steps}); roofline and traffic from these launches",
+                       "parallelism": f"agent-sharded x{world} (no collective in the step)"},
             "roofline": roof,
         }
+        if episode is not None:
+            rec["episode_window"] = episode
         if single is not None:
             rec["drop_in_single_step"] = single   # vn_step-shaped call: one env step per launch
         if simple is not None:
             rec["simple_env"] = simple            # goal-seeking variant
-        if coll_bf is not None:
-            rec["collector_bf16"] = coll_bf
-        if coll is not None:
-            rec["collector"] = coll               # policy in the loop
+        rec.update(legs)                          # policy in the loop
         if world == 1 and args.cpu_seconds > 0:
-            cb = cpu_baseline((W, D, H), args.L, args.cpu_seconds)
-            one = cpu_baseline((W, D, H), args.L, max(2.0, args.cpu_seconds / 4), threads_override=1)
-            cb["single_core_value"] = one["value"]
-            cb["cpu_model"] = cpu_model()
-            # the reference itself (Python, envs/CubicEnv.py) cannot travel to this
-            # box; its step rate as measured in the build container
-            cb["reference_python_build_container"] = {
-                "single_core": 7.0e3, "eight_processes": 4.95e4, "unit": "env-steps/s",
-                "workload": "32x32x8 box, L=10, random actions, 1 env per process",
-                "source": "SURVEY.md §6 (Intel Xeon, 8 vCPU; not this box)"}
-            rec["cpu_baseline"] = cb
+            rec["cpu_baseline"] = cpu_baseline((W, D, H), args.L, args.cpu_seconds)
         line = json.dumps(rec)
         print(line, flush=True)
         if args.json_out:

@@ -148,6 +148,15 @@ int vn_step_random(VnEnv *env, uint64_t policy_seed, uint64_t t0, int32_t k_step
  * n visits; simpleEnv: -1 unknown, 0 free, 1 visited, 2 wall;
  * visit counts saturate at 63), cells outside the agent's room read -128.
  */
+/*
+ * Name of the kernel instantiation a call of this shape launches
+ * (k_steps = 0: vn_reset; explicit_actions: vn_step; fast: reward, terminated
+ * and truncated requested, no f64 reward or action record).  Diagnostics:
+ * lets bench.py and rocprofv3 summaries name the kernel they time.  No
+ * reference counterpart.
+ */
+int vn_kernel_label(const VnEnv *env, int32_t k_steps, int32_t explicit_actions, int32_t fast, char *buf,
+                    int32_t len);
 int vn_export_state(VnEnv *env, int64_t *state_out, void *stream);
 int vn_export_belief(VnEnv *env, int8_t *belief_out, void *stream);
 
