@@ -179,7 +179,7 @@ def lib():
         L.or_random_action.argtypes = [c.c_uint64, c.c_uint64, c.c_uint64]
         L.or_random_action.restype = c.c_int32
         L.or_run_random.argtypes = [P, P, c.c_int, c.c_int64, c.c_uint64, c.c_uint64, c.c_uint64, c.c_int,
-                                    c.c_int, P, P, P, P, P, P, P, c.c_int]
+                                    c.c_int, P, P, P, P, P, P, P, c.c_int, P]
         L.or_run_random.restype = c.c_int64
         L.or_gae.argtypes = [P, P, P, P, P, c.c_int, c.c_int, c.c_double, c.c_double, P, P]
         _lib = L
@@ -252,8 +252,10 @@ class OracleEnv:
 
     def run_random(self, seeds, policy_seed: int, K: int, t0: int = 0, gid_base: int = 0,
                    seed_stride: Optional[int] = None, autoreset: bool = True, initial_reset: bool = True,
-                   record: bool = True, threads: int = 0, actions=None, terminal_obs: bool = False):
-        """K batched steps (Philox random policy, or `actions` [K, N]) with SB3-style autoreset."""
+                   record: bool = True, threads: int = 0, actions=None, terminal_obs: bool = False, gids=None):
+        """K batched steps (Philox random policy, or `actions` [K, N]) with SB3-style autoreset.
+        Agent i's random-policy stream is keyed by ``gids[i]`` when given (a
+        sample of a larger batch), else by ``gid_base + i``."""
         N = self.n_agents
         seeds = np.ascontiguousarray(np.asarray(seeds, dtype=np.int64).reshape(N))
         stride = N if seed_stride is None else int(seed_stride)
@@ -267,9 +269,11 @@ class OracleEnv:
             obs = rew = te = tr = act = None
         tob = np.zeros((K, N, self.obs_dim), np.float32) if terminal_obs else None
         ain = None if actions is None else np.ascontiguousarray(np.asarray(actions, np.int32).reshape(K, N))
+        gid = None if gids is None else np.ascontiguousarray(np.asarray(gids, np.int64).reshape(N))
         resets = lib().or_run_random(self._h, _ptr(seeds), int(bool(initial_reset)), stride, int(gid_base),
                                      int(policy_seed), int(t0), int(K), int(bool(autoreset)), _ptr(obs),
-                                     _ptr(rew), _ptr(te), _ptr(tr), _ptr(act), _ptr(tob), _ptr(ain), int(threads))
+                                     _ptr(rew), _ptr(te), _ptr(tr), _ptr(act), _ptr(tob), _ptr(ain), int(threads),
+                                     _ptr(gid))
         return dict(obs=obs, reward=rew, terminated=te, truncated=tr, actions=act, terminal_obs=tob,
                     resets=int(resets))
 

@@ -65,16 +65,31 @@ def _policy(kind):
     return pol
 
 
-@pytest.mark.parametrize("kind,T,rollouts,dtype", [("lstm", 48, 2, "f32"), ("mlp", 80, 1, "f32"),
-                                                   ("lstm", 48, 2, "bf16"), ("mlp", 48, 1, "bf16")])
-def test_collector_matches_oracle(voxnav, kind, T, rollouts, dtype):
+def _set_rooms(name):
+    from helpers import product_room_set, set_members
+    from oracle.oracle import parse_room_text
+    return product_room_set(f"set:{name}"), [parse_room_text(t, n) for n, t in set_members(name)]
+
+
+COLLECT_CASES = [
+    # (policy, T, rollouts, dtype, rooms, L, N)
+    ("lstm", 48, 2, "f32", "boxes", 4, 64), ("mlp", 80, 1, "f32", "boxes", 4, 64),
+    ("lstm", 48, 2, "bf16", "boxes", 4, 64), ("mlp", 48, 1, "bf16", "boxes", 4, 64),
+    # BASELINE configs at the reference's settings, a few hundred agents:
+    # C4 = PPO-LSTM on P3_training (L=10, n_steps 128), C3 = PPO-MLP on P2_training
+    ("lstm", 128, 2, "f32", "P3_training", 10, 192), ("mlp", 128, 3, "f32", "P2_training", 10, 256),
+]
+
+
+@pytest.mark.parametrize("kind,T,rollouts,dtype,rooms,L,N", COLLECT_CASES,
+                         ids=[f"{c[0]}-{c[3]}-{c[4]}-T{c[1]}" for c in COLLECT_CASES])
+def test_collector_matches_oracle(voxnav, kind, T, rollouts, dtype, rooms, L, N):
     from oracle import collector_oracle as co
     from oracle.oracle import OracleEnv, gae as gae32
     from voxnav.collector import RolloutCollector
     from voxnav.env import BatchedGridEnv
     from voxnav.policy import numpy_weights
-    N, L = 64, 4
-    prod, orooms = _rooms()
+    prod, orooms = _rooms() if rooms == "boxes" else _set_rooms(rooms)
     pol = _policy(kind)
     env = BatchedGridEnv(num_agents=N, rooms=prod, local_map_length=L, device="cuda:0")
     col = RolloutCollector(env, pol.to("cuda:0"), n_steps=T, sample_seed=1234, reset_seed=42, policy_dtype=dtype)

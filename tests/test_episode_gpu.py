@@ -1,0 +1,149 @@
+"""Full-episode parity of the benched kernel instantiations at the headline
+room (32x32x8 box, L=10) -- every agent crosses the 5,400-step truncation
+and the SB3 auto-reset (plane clear at full u32 row width, wall-image
+re-copy), against the CPU oracle (oracle/voxnav_oracle.c, pinned to the
+reference's golden trajectories by tests/test_oracle_golden.py).
+
+* the bench's call: ``step_random(out=...)`` in F=16 launches, f32 reward,
+  no action record -> ``env_kernel<8, false, true, false, 2>``;
+* the collector's call: ``step_into`` with explicit actions, f32 reward,
+  one step per launch -> ``env_kernel<8, true, true, false, 2>``;
+* the full BASELINE batch (65,536 agents) with one sampled agent from every
+  64-agent block, through a whole episode.
+
+Bar: obs bytes, f32 reward (the oracle's f64 reward rounded), terminated /
+truncated flags bit-exact at every step; exported belief maps equal the
+oracle's (visit counts saturating at 63) at three points of the episode.
+"""
+import numpy as np
+import pytest
+
+from helpers import oracle_env, product_room_set
+
+torch = pytest.importorskip("torch")
+pytestmark = pytest.mark.gpu
+
+SRC, L = "box:32x32x8", 10
+EPISODE = 5400                 # total_free_cells of the 32x32x8 box
+K_TOTAL = 5504                 # 344 launches of 16: the truncation at 5,400 and 104 steps of the next episode
+BELIEF_AT = (2000, 5408, K_TOTAL)
+
+
+@pytest.fixture(scope="module")
+def voxnav():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    import voxnav
+    voxnav.load_library()
+    return voxnav
+
+
+def make_env(n):
+    from voxnav.env import BatchedGridEnv
+    return BatchedGridEnv(num_agents=n, rooms=product_room_set(SRC), local_map_length=L, autoreset=True,
+                          device="cuda:0")
+
+
+def check_beliefs(env, orc_env, sample, step):
+    b = env.belief()
+    b = b.index_select(0, torch.as_tensor(sample, device=b.device)).cpu().numpy().astype(np.int64)
+    for j in range(len(sample)):
+        ref = np.minimum(orc_env.belief(j), 63)
+        W, D, H = ref.shape
+        np.testing.assert_array_equal(b[j, :W, :D, :H], ref, err_msg=f"belief of agent {sample[j]} at step {step}")
+
+
+def run_random_episode(env, N, sample, F=16):
+    """Bench-shaped launches; compare the sampled agents launch by launch."""
+    from voxnav.env import Rollout
+    dev = env.device
+    out = Rollout(torch.empty((F, N, 80), dtype=torch.float32, device=dev),
+                  torch.empty((F, N), dtype=torch.float32, device=dev),
+                  torch.empty((F, N), dtype=torch.uint8, device=dev),
+                  torch.empty((F, N), dtype=torch.uint8, device=dev), None)
+    assert env.kernel_label(F) == "env_kernel<8, false, true, false, 2>"
+    idx = torch.as_tensor(sample, device=dev)
+    orc_env = oracle_env(SRC, L, n_agents=len(sample))
+    seeds = 42 + np.asarray(sample, dtype=np.int64)
+    env.reset(seed=42)
+    t = 0
+    truncations = 0
+    while t < K_TOTAL:
+        k = min(F, K_TOTAL - t)
+        env.step_random(k, policy_seed=42, t0=t,
+                        out=Rollout(out.obs[:k], out.reward[:k], out.terminated[:k], out.truncated[:k], None))
+        orc = orc_env.run_random(seeds, policy_seed=42, K=k, t0=t, seed_stride=N, initial_reset=(t == 0),
+                                 gids=sample, threads=8)
+        obs = out.obs[:k].index_select(1, idx).cpu().numpy()
+        if obs.tobytes() != orc["obs"].tobytes():
+            bad = np.argwhere((obs.view(np.uint32) != orc["obs"].view(np.uint32)).any(-1))
+            raise AssertionError(f"obs mismatch at (step, sampled agent) {(bad[:5] + [t, 0]).tolist()}")
+        np.testing.assert_array_equal(out.reward[:k].index_select(1, idx).cpu().numpy(),
+                                      orc["reward"].astype(np.float32), err_msg=f"reward, steps {t}..{t + k}")
+        np.testing.assert_array_equal(out.terminated[:k].index_select(1, idx).cpu().numpy(), orc["terminated"])
+        tr = out.truncated[:k].index_select(1, idx).cpu().numpy()
+        np.testing.assert_array_equal(tr, orc["truncated"])
+        truncations += int(tr.sum())
+        t += k
+        if t in BELIEF_AT:
+            check_beliefs(env, orc_env, sample, t)
+    return truncations
+
+
+def test_bench_kernel_full_episode_matches_oracle(voxnav):
+    """The benched instantiation, 256 agents, 5,504 steps: every agent's
+    5,400-step episode truncates and auto-resets inside the run."""
+    N = 256
+    env = make_env(N)
+    tr = run_random_episode(env, N, np.arange(N, dtype=np.int64))
+    assert tr == N        # each agent truncated exactly once, at step 5,400
+    env.close()
+
+
+def test_full_batch_sampled_blocks_full_episode(voxnav):
+    """65,536 agents (the headline batch): one agent from every 64-agent
+    block (each block of the kernel), position varied, through the whole
+    episode and the auto-reset."""
+    N = 65536
+    blocks = np.arange(N // 64, dtype=np.int64)
+    sample = blocks * 64 + (blocks * 37 + 11) % 64
+    env = make_env(N)
+    tr = run_random_episode(env, N, sample)
+    assert tr == len(sample)
+    env.close()
+
+
+def test_step_into_full_episode_matches_oracle(voxnav):
+    """The collector's call (explicit actions, one step per launch, f32
+    reward, terminal_obs) over a whole 32x32x8 episode and its auto-reset."""
+    N, K, CH = 128, 5410, 541
+    env = make_env(N)
+    dev = env.device
+    assert env.kernel_label(1, explicit_actions=True) == "env_kernel<8, true, true, false, 2>"
+    acts = np.random.default_rng(17).integers(0, 6, size=(K, N)).astype(np.int32)
+    at = torch.as_tensor(acts, device=dev)
+    obs = torch.empty((CH, N, 80), dtype=torch.float32, device=dev)
+    rew = torch.empty((CH, N), dtype=torch.float32, device=dev)
+    te = torch.empty((CH, N), dtype=torch.uint8, device=dev)
+    tr = torch.empty((CH, N), dtype=torch.uint8, device=dev)
+    tob = torch.zeros((CH, N, 80), dtype=torch.float32, device=dev)
+    orc_env = oracle_env(SRC, L, n_agents=N)
+    seeds = 42 + np.arange(N, dtype=np.int64)
+    env.reset(seed=42)
+    ended = 0
+    for c0 in range(0, K, CH):
+        for j in range(CH):
+            env.step_into(at[c0 + j], obs[j], rew[j], te[j], tr[j], tob[j])
+        orc = orc_env.run_random(seeds, policy_seed=0, K=CH, t0=c0, seed_stride=N, initial_reset=(c0 == 0),
+                                 actions=acts[c0:c0 + CH], terminal_obs=True, threads=8)
+        assert obs.cpu().numpy().tobytes() == orc["obs"].tobytes(), f"obs, steps {c0}..{c0 + CH}"
+        np.testing.assert_array_equal(rew.cpu().numpy(), orc["reward"].astype(np.float32))
+        np.testing.assert_array_equal(te.cpu().numpy(), orc["terminated"])
+        trn = tr.cpu().numpy()
+        np.testing.assert_array_equal(trn, orc["truncated"])
+        done = (te.cpu().numpy() | trn).astype(bool)
+        ended += int(done.sum())
+        np.testing.assert_array_equal(tob.cpu().numpy()[done], orc["terminal_obs"][done])
+    assert ended == N
+    check_beliefs(env, orc_env, np.arange(N), K)
+    env.close()
