@@ -641,6 +641,29 @@ int policy_head_launch(const T *latent_pi, const T *latent_vf, int32_t N, int32_
 
 }  // namespace
 
+
+// SB3 Monitor (stable_baselines3/common/monitor.py, wrapping every worker at
+// train/Grid_Train.py:125): per agent the running episode return (f64, summed
+// in step order from 0 like Monitor's sum(self.rewards)) and length; on
+// terminated | truncated the finished episode's (return, length) goes to this
+// step's record row and the counters restart (Monitor.reset via the VecEnv
+// auto-reset).  rec_len 0 = no episode ended at this step.
+__global__ __launch_bounds__(256) void monitor_kernel(const double *__restrict__ r64, const float *__restrict__ r32,
+                                                      const uint8_t *__restrict__ term,
+                                                      const uint8_t *__restrict__ trunc, int N,
+                                                      double *__restrict__ ep_ret, int32_t *__restrict__ ep_len,
+                                                      double *__restrict__ rec_ret, int32_t *__restrict__ rec_len) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= N) return;
+    const double r = ep_ret[i] + (r64 ? r64[i] : (double)r32[i]);
+    const int32_t l = ep_len[i] + 1;
+    const bool done = (term[i] | trunc[i]) != 0;
+    rec_ret[i] = done ? r : 0.0;
+    rec_len[i] = done ? l : 0;
+    ep_ret[i] = done ? 0.0 : r;
+    ep_len[i] = done ? 0 : l;
+}
+
 extern "C" {
 
 int vn_lstm_cell(const float *gx, int64_t gx_row_stride, const float *gh, const float *b_ih, const float *b_hh,
@@ -729,6 +752,19 @@ int vn_episode_start(const uint8_t *terminated, const uint8_t *truncated, int32_
     const int64_t threads = n_lstm ? (int64_t)n_lstm * N * (H / 4) : (int64_t)N;
     hipLaunchKernelGGL(episode_start_kernel, dim3(blocks_for(threads)), dim3(256), 0, (hipStream_t)stream,
                        terminated, truncated, (int)N, episode_starts, h, c, h_bf16, (int)n_lstm, (int)H);
+    VN_HIP(hipGetLastError());
+    return VN_OK;
+}
+
+int vn_monitor_step(const double *reward64, const float *reward, const uint8_t *terminated, const uint8_t *truncated,
+                    int32_t N, double *ep_return, int32_t *ep_length, double *rec_return, int32_t *rec_length,
+                    void *stream) {
+    if ((!reward64 && !reward) || !terminated || !truncated || !ep_return || !ep_length || !rec_return || !rec_length)
+        return fail(VN_ERR_INVALID, "NULL argument");
+    if (N < 1) return fail(VN_ERR_INVALID, "bad size N=%d", N);
+    hipLaunchKernelGGL(monitor_kernel, dim3(blocks_for(N)), dim3(256), 0, (hipStream_t)stream, reward64,
+                       reward64 ? nullptr : reward, terminated, truncated, (int)N, ep_return, ep_length, rec_return,
+                       rec_length);
     VN_HIP(hipGetLastError());
     return VN_OK;
 }

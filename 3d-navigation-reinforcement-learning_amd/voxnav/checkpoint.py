@@ -10,11 +10,17 @@ and counters, and ``_stable_baselines3_version``.
 
 ``save_checkpoint`` writes those members; the policy ``state_dict`` keys
 are SB3's own (``lstm_actor.weight_ih_l0``, ``mlp_extractor.policy_net.0
-.weight``, ``action_net.weight`` ...), so ``policy.pth`` moves between this
-package and an SB3 ``RecurrentPPO`` in both directions.  ``data`` here is
-plain JSON (SB3 stores cloudpickled objects there); ``load_checkpoint``
-reads only JSON and ``torch.load(..., weights_only=True)`` -- nothing in a
-checkpoint is executed.
+.weight``, ``action_net.weight`` ...).  ``data`` here is plain JSON (SB3
+stores cloudpickled objects there); ``load_checkpoint`` reads only JSON and
+``torch.load(..., weights_only=True)`` -- nothing in a checkpoint is
+executed.
+
+Interop is one-way at the zip level: ``load_checkpoint`` reads the
+reference's SB3 zips (policy.pth only, architecture from the tensor
+shapes), but SB3's ``RecurrentPPO.load`` (Train_Further.py:145,
+evaluate_grid.py:165) cannot read these zips' JSON ``data``; an SB3 model
+takes this package's weights with
+``model.policy.load_state_dict(torch.load(policy_pth, weights_only=True))``.
 """
 from __future__ import annotations
 
@@ -93,18 +99,73 @@ def save_checkpoint(path: Union[str, Path], policy, optimizer: Optional[torch.op
     return path
 
 
+# Keys an SB3 policy state_dict may hold that this package's modules do not:
+# none carry parameters for MlpLstmPolicy / MlpPolicy (Flatten feature
+# extractors), so this allow-list only guards against future SB3 versions
+# registering buffers under these prefixes.  Anything else missing or
+# unexpected is an error (strict load), never silently random weights.
+SB3_IGNORED_PREFIXES = ("features_extractor.", "pi_features_extractor.", "vf_features_extractor.")
+
+
+def load_policy_state(policy: torch.nn.Module, state_dict: Dict[str, torch.Tensor]) -> None:
+    """``policy.load_state_dict`` for an SB3 (or voxnav) ``policy.pth``:
+    strict over every parameter, after dropping only the allow-listed
+    parameterless SB3 extractor keys."""
+    sd = {k: v for k, v in state_dict.items() if not k.startswith(SB3_IGNORED_PREFIXES)}
+    policy.load_state_dict(sd, strict=True)
+
+
+def policy_from_state_dict(state_dict: Dict[str, torch.Tensor]) -> torch.nn.Module:
+    """Build the policy a ``policy.pth`` describes from its tensor shapes
+    alone (an SB3 zip's ``data`` member is cloudpickled and never read):
+    LSTM hidden size from ``lstm_actor.weight_hh_l0``, MLP widths from
+    ``mlp_extractor.{policy,value}_net.<i>.weight``, obs / action dims from
+    the first layer and ``action_net``."""
+    sd = state_dict
+
+    def widths(branch):
+        ks = sorted((int(k.split(".")[2]), k) for k in sd if k.startswith(f"mlp_extractor.{branch}.")
+                    and k.endswith(".weight"))
+        return [int(sd[k].shape[0]) for _, k in ks]
+
+    arch = dict(pi=widths("policy_net"), vf=widths("value_net"))
+    n_actions = int(sd["action_net.weight"].shape[0])
+    if "lstm_actor.weight_ih_l0" in sd:
+        H = int(sd["lstm_actor.weight_hh_l0"].shape[1])
+        obs_dim = int(sd["lstm_actor.weight_ih_l0"].shape[1])
+        pol = RecurrentActorCriticPolicy(obs_dim=obs_dim, n_actions=n_actions, lstm_hidden_size=H, net_arch=arch,
+                                         ortho_init=False)
+    else:
+        first = sd["mlp_extractor.policy_net.0.weight"]
+        pol = ActorCriticPolicy(obs_dim=int(first.shape[1]), n_actions=n_actions, net_arch=arch, ortho_init=False)
+    load_policy_state(pol, sd)
+    return pol
+
+
 def load_checkpoint(path: Union[str, Path], device="cpu") -> Tuple[torch.nn.Module, Dict[str, object]]:
-    """-> (policy on ``device``, data dict).  The optimizer state is restored
-    separately (``load_optimizer_state``) into an optimizer built over the
-    returned policy's parameters."""
+    """-> (policy on ``device``, data dict).
+
+    Reads this package's zips (JSON ``data``) and SB3 / sb3_contrib zips
+    (``model.save`` of the reference, train/Grid_Train.py:233): for those
+    only ``policy.pth`` is loaded (``weights_only``) and the architecture is
+    inferred from its shapes; ``data`` is returned as ``{"sb3": True}``
+    without decoding SB3's cloudpickled fields.  The optimizer state is
+    restored separately (``load_optimizer_state``) into an optimizer built
+    over the returned policy's parameters."""
     with zipfile.ZipFile(path) as z:
-        data = json.loads(z.read("data"))
+        raw = z.read("data")
         sd = torch.load(io.BytesIO(z.read("policy.pth")), map_location="cpu", weights_only=True)
+    try:
+        data = json.loads(raw)
+    except ValueError:
+        data = None
+    if not isinstance(data, dict) or data.get("format") != FORMAT_VERSION:
+        return policy_from_state_dict(sd).to(device), {"sb3": True}
     kw = dict(data["policy_kwargs"])
     kw.pop("n_lstm_layers", None)
     cls = RecurrentActorCriticPolicy if data.get("policy_class") == "MlpLstmPolicy" else ActorCriticPolicy
     pol = cls(ortho_init=False, **kw)
-    pol.load_state_dict(sd, strict=True)
+    load_policy_state(pol, sd)
     return pol.to(device), data
 
 

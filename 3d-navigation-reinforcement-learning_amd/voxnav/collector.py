@@ -21,8 +21,12 @@ per step t
   4. ``vn_episode_start`` -> episode_starts[t+1] = done, zero the (h, c) of
      those agents (``_process_sequence``'s ``(1 - episode_start)`` mask)
 
+  5. ``vn_monitor_step`` -> the SB3 Monitor's per-agent episode return
+     (f64) / length and the episodes that ended at step t (voxnav.monitor)
+
 after T steps: V(obs[T]) under the current critic states, then the GAE scan
-(``vn_gae``) -> advantages, returns.
+(``vn_gae``) -> advantages, returns; the finished episodes go to
+``monitor.ep_info_buffer`` (``ep_rew_mean`` / ``ep_len_mean``).
 
 ``policy_dtype="bf16"`` runs the policy GEMMs in bf16 (f32 accumulation,
 bf16 activations; LSTM cell state, heads, sampling and everything after
@@ -44,6 +48,7 @@ import torch
 
 from . import _native
 from .env import OBS_DIM, BatchedGridEnv
+from .monitor import EpisodeMonitor
 from .policy import ActorCriticPolicy, RecurrentActorCriticPolicy
 
 
@@ -137,7 +142,7 @@ class RolloutCollector:
 
     def __init__(self, env: BatchedGridEnv, policy, n_steps: int = 128, gamma: float = 0.99, gae_lambda: float = 0.95,
                  sample_seed: int = 42, deterministic: bool = False, store_lstm_states: bool = True,
-                 reset_seed: int = 42, policy_dtype: str = "f32"):
+                 reset_seed: int = 42, policy_dtype: str = "f32", monitor: bool = True):
         if not isinstance(policy, (ActorCriticPolicy, RecurrentActorCriticPolicy)):
             raise TypeError("policy must be an ActorCriticPolicy or RecurrentActorCriticPolicy")
         if getattr(policy, "obs_dim", OBS_DIM) != env.obs_dim:
@@ -186,6 +191,10 @@ class RolloutCollector:
             self.store = bool(store_lstm_states)
             self._hs = z(T + 1, 2, N, H) if self.store else None
             self._cs = z(T + 1, 2, N, H) if self.store else None
+        # SB3 Monitor on every worker (train/Grid_Train.py:125): it sums the env's
+        # f64 rewards, so the env step also writes them (voxnav.monitor)
+        self.monitor = EpisodeMonitor(self.lib, N, T, dev) if monitor else None
+        self._r64 = z(N, dt=torch.float64) if monitor else None
         # learn() start: reset every env, episode_starts = ones, zero states
         self._obs[0] = env.reset(seed=reset_seed)
         self._starts[0].fill_(1.0)
@@ -296,10 +305,15 @@ class RolloutCollector:
         s = self._stream
         if self._carry:
             self._carry_over()
+        mon = self.monitor
+        if mon is not None:
+            mon.begin()
         for t in range(T):
             self._forward(self._obs[t], t)
             self.env.step_into(self.actions[t], self._obs[t + 1], self.rewards[t], self._term, self._trunc,
-                               self._tobs)
+                               self._tobs, reward64=self._r64)
+            if mon is not None:
+                mon.step(t, self._term, self._trunc, reward64=self._r64)
             _native.check(lib.vn_collect_compact(_p(self._term), _p(self._trunc), N, _p(self._boot_idx),
                                                  _p(self._boot_cnt), s()), "vn_collect_compact")
             self._boot_cnt_host.copy_(self._boot_cnt, non_blocking=True)
@@ -335,6 +349,8 @@ class RolloutCollector:
                                  _p(self._starts[T]), T, N, self.gamma, self.gae_lambda, _p(adv), _p(ret), s()),
                       "vn_gae")
         self._carry = True
+        if mon is not None:
+            mon.harvest()
         hs = self._hs[:T] if self.recurrent and self.store else None
         cs = self._cs[:T] if self.recurrent and self.store else None
         return RolloutBuffer(obs=self._obs[:T], actions=self.actions, rewards=self.rewards,

@@ -188,10 +188,13 @@ class BatchedGridEnv:
         return StepResult(obs, rew, te.bool(), tr.bool(), tob)
 
     def step_into(self, actions: torch.Tensor, obs: torch.Tensor, reward: torch.Tensor, terminated: torch.Tensor,
-                  truncated: torch.Tensor, terminal_obs: Optional[torch.Tensor] = None):
+                  truncated: torch.Tensor, terminal_obs: Optional[torch.Tensor] = None,
+                  reward64: Optional[torch.Tensor] = None):
         """``step`` writing into caller-owned device buffers (no allocation):
         actions i32 [N], obs f32 [N, obs_dim], reward f32 (or f64) [N],
-        terminated / truncated u8 [N], terminal_obs f32 [N, obs_dim] or None."""
+        terminated / truncated u8 [N], terminal_obs f32 [N, obs_dim] or None;
+        ``reward64`` (f64 [N], with an f32 ``reward``) also receives the exact
+        f64 reward (what the Monitor sums)."""
         if not self._was_reset:
             raise RuntimeError("call reset() before step()")
         N = self.num_agents
@@ -203,8 +206,12 @@ class BatchedGridEnv:
         if reward.dtype not in (torch.float32, torch.float64) or tuple(reward.shape) != (N,) or not reward.is_contiguous():
             raise ValueError("reward: expected contiguous f32/f64 [N]")
         f64 = reward.dtype == torch.float64
+        if reward64 is not None:
+            if f64 or reward64.dtype != torch.float64 or tuple(reward64.shape) != (N,) or not reward64.is_contiguous():
+                raise ValueError("reward64: expected contiguous f64 [N] next to an f32 reward")
+        r64 = reward if f64 else reward64
         _native.check(self.lib.vn_step(self._h, _ptr(actions), _ptr(obs), None if f64 else _ptr(reward),
-                                       _ptr(reward) if f64 else None, _ptr(terminated), _ptr(truncated),
+                                       _ptr(r64), _ptr(terminated), _ptr(truncated),
                                        _ptr(terminal_obs), self._stream()), "vn_step")
 
     def step_random(self, k_steps: int, policy_seed: int = 42, t0: Optional[int] = None, record_actions: bool = False,

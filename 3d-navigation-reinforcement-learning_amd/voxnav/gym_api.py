@@ -25,10 +25,10 @@ from typing import Optional
 import numpy as np
 
 from .env import BatchedGridEnv
-from .spaces import Box, Discrete
+from .spaces import Box, Discrete, EnvBase
 
 
-class GridAgent:
+class GridAgent(EnvBase):
     metadata = {"render_modes": ["human"]}
 
     def __init__(self, grid=None, max_steps=2000, width: int = 20, depth: int = 20, height: int = 12,

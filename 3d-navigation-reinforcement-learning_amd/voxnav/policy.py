@@ -9,7 +9,8 @@ critic LSTM(80 -> 256) -> Tanh MLPs 256-256-256-128 -> action_net(128 -> 6)
 and value_net(128 -> 1).  Parameter names follow SB3's state_dict keys
 (``lstm_actor.weight_ih_l0``, ``mlp_extractor.policy_net.0.weight``,
 ``action_net.weight`` ...) so an SB3 checkpoint's ``policy.pth`` loads with
-``load_state_dict(torch.load(path, weights_only=True), strict=False)``.
+``voxnav.checkpoint.load_policy_state`` (strict, with an explicit allow-list
+of parameterless SB3-only keys).
 
 ``ActorCriticPolicy`` is the feed-forward ``MlpPolicy`` of BASELINE config
 C3 (PPO-MLP, same pi/vf MLPs on the observation).

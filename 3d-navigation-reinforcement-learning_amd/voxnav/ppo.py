@@ -198,24 +198,48 @@ class PPOLearner:
 
 
 def learn(collector, learner: PPOLearner, total_timesteps: int, callback=None) -> List[Dict[str, float]]:
-    """``model.learn(total_timesteps)`` (OnPolicyAlgorithm.learn): alternate
-    ``collector.collect()`` and ``learner.train()`` until ``total_timesteps``
-    env steps (agents x steps, summed over this rank) were collected, pushing
-    the updated weights into the collector after every update.
-    ``callback(iteration, num_timesteps, stats)`` returning False stops early
-    (SB3 callback semantics).  Returns the per-iteration train stats."""
+    """``model.learn(total_timesteps, callback=...)`` (OnPolicyAlgorithm.learn):
+    alternate ``collector.collect()`` and ``learner.train()`` until
+    ``total_timesteps`` env steps (agents x steps, summed over this rank)
+    were collected, pushing the updated weights into the collector after
+    every update.
+
+    ``callback``: one callback or a list.  Objects with ``on_rollout_end``
+    (``voxnav.evaluate.EvalCallback``, Grid_Train.py:218-226) run after each
+    rollout, before the update -- the weights the rollout was collected
+    with; plain callables ``callback(iteration, num_timesteps, stats)`` run
+    after the update, returning False stops early (SB3 semantics).
+
+    Returns the per-iteration stats: the train losses, ``num_timesteps``,
+    the Monitor's ``ep_rew_mean`` / ``ep_len_mean`` over the last 100
+    finished episodes (SB3's ``rollout/`` logger keys, when any episode has
+    finished) and the evaluation's ``eval/*`` keys when one ran."""
     if collector.policy is not learner.policy:
         raise ValueError("collector and learner must share the policy module")
+    cbs = [] if callback is None else (list(callback) if isinstance(callback, (list, tuple)) else [callback])
     per_rollout = collector.n_steps * collector.N
     done, it, history = 0, 0, []
     while done < total_timesteps:
         buf = collector.collect()
         done += per_rollout
         it += 1
+        evals = {}
+        for cb in cbs:
+            if hasattr(cb, "on_rollout_end"):
+                evals.update(cb.on_rollout_end(learner.policy, done, collector.n_steps, learner.optimizer) or {})
         st = learner.train(buf)
         collector.sync_weights()
         st["num_timesteps"] = done
+        mon = getattr(collector, "monitor", None)
+        if mon is not None and mon.ep_info_buffer:
+            st["ep_rew_mean"] = mon.ep_rew_mean()
+            st["ep_len_mean"] = mon.ep_len_mean()
+        st.update(evals)
         history.append(st)
-        if callback is not None and callback(it, done, st) is False:
+        stop = False
+        for cb in cbs:
+            if not hasattr(cb, "on_rollout_end") and callable(cb) and cb(it, done, st) is False:
+                stop = True
+        if stop:
             break
     return history

@@ -8,8 +8,26 @@ from __future__ import annotations
 import numpy as np
 
 try:  # pragma: no cover - exercised only where gymnasium is installed
+    from gymnasium import Env as EnvBase  # type: ignore
     from gymnasium.spaces import Box, Discrete  # type: ignore
+    HAVE_GYMNASIUM = True
 except Exception:  # noqa: BLE001
+    HAVE_GYMNASIUM = False
+
+    class EnvBase:
+        """Stand-in for ``gymnasium.Env`` (the reference subclasses it,
+        envs/CubicEnv.py:15): with gymnasium installed, GridAgent is a real
+        ``gymnasium.Env`` and passes SB3's ``check_env``
+        (train/Grid_Train.py:138-147)."""
+        metadata = {"render_modes": []}
+        render_mode = None
+        spec = None
+
+        @property
+        def unwrapped(self):
+            return self
+
+
     class Discrete:
         def __init__(self, n: int, seed=None):
             self.n = int(n)

@@ -262,6 +262,18 @@ int vn_collect_bootstrap(const int32_t *boot_idx, const float *terminal_values, 
 int vn_episode_start(const uint8_t *terminated, const uint8_t *truncated, int32_t N, float *episode_starts,
                      float *h, float *c, uint16_t *h_bf16, int32_t n_lstm, int32_t H, void *stream);
 
+/*
+ * SB3 Monitor (train/Grid_Train.py:125 wraps every worker) for N agents, one
+ * env step: ep_return (f64) += reward (reward64 when non-NULL, else the f32
+ * reward), ep_length += 1; where terminated | truncated the finished
+ * episode's (return, length) goes to rec_return / rec_length [N] (the
+ * caller's row for this step; rec_length 0 = no episode ended) and the
+ * counters restart, as Monitor.reset does under the VecEnv auto-reset.
+ */
+int vn_monitor_step(const double *reward64, const float *reward, const uint8_t *terminated, const uint8_t *truncated,
+                    int32_t N, double *ep_return, int32_t *ep_length, double *rec_return, int32_t *rec_length,
+                    void *stream);
+
 /* ------------------------------------------------------------------------
  * PPO learner: the LSTM re-run of sb3_contrib RecurrentPPO.train
  * (RecurrentActorCriticPolicy.evaluate_actions -> _process_sequence, from

@@ -112,3 +112,108 @@ def test_evaluate_policy_matches_oracle_replay(kind):
         assert e["score"] == pytest.approx(score, rel=0, abs=1e-9), i
     assert checked > n * 10
     assert r["avg_steps"] == pytest.approx(np.mean([e["steps"] for e in r["episodes"]]))
+
+
+def test_eval_cadence_counts_crossed_multiples():
+    from voxnav.evaluate import evals_due
+    assert evals_due(0, 32, 48) == 0 and evals_due(32, 64, 48) == 1 and evals_due(64, 96, 48) == 1
+    assert evals_due(0, 128, 1) == 128 and evals_due(5, 6, 0) == 0
+    # Grid_Train: eval_freq = max(100_000 // NUM_ENVS, 1) vectorized steps
+    assert evals_due(0, 12500, max(100_000 // 8, 1)) == 1
+
+
+def test_learn_callback_plumbing_cpu():
+    from voxnav.ppo import learn
+
+    class Col:
+        n_steps, N, monitor = 4, 2, None
+
+        def __init__(self, pol):
+            self.policy = pol
+
+        def collect(self):
+            return None
+
+        def sync_weights(self):
+            pass
+
+    class Ln:
+        optimizer = None
+
+        def __init__(self, pol):
+            self.policy = pol
+
+        def train(self, buf):
+            return {"loss": 0.0}
+
+    seen = []
+
+    class Hook:
+        def on_rollout_end(self, policy, num_timesteps, n_steps, optimizer=None):
+            seen.append((num_timesteps, n_steps))
+            return {"eval/mean_reward": 1.0} if num_timesteps == 16 else None
+
+    pol = object()
+    calls = []
+    hist = learn(Col(pol), Ln(pol), total_timesteps=40, callback=[Hook(), lambda i, n, st: calls.append(n)])
+    assert [h["num_timesteps"] for h in hist] == [8, 16, 24, 32, 40]
+    assert seen == [(8, 4), (16, 4), (24, 4), (32, 4), (40, 4)]
+    assert calls == [8, 16, 24, 32, 40]
+    assert "eval/mean_reward" in hist[1] and "eval/mean_reward" not in hist[0]
+
+
+def _sb3_style_zip(path, policy):
+    """An SB3-layout zip (the reference's model.save, Grid_Train.py:233): a
+    `data` member whose fields SB3 serializes as base64 cloudpickle blobs
+    (never decoded here) and the policy state_dict under SB3's key names."""
+    import io
+    import json
+    import zipfile
+    data = {"policy_class": {":type:": "<class 'abc.ABCMeta'>", ":serialized:": "gAWVOw=="},
+            "num_timesteps": 1234, "policy_kwargs": {":type:": "<class 'dict'>", ":serialized:": "gAWV"}}
+    b = io.BytesIO()
+    torch.save({k: v.detach().cpu() for k, v in policy.state_dict().items()}, b)
+    with zipfile.ZipFile(path, "w") as z:
+        z.writestr("data", json.dumps(data))
+        z.writestr("policy.pth", b.getvalue())
+        z.writestr("_stable_baselines3_version", "2.3.2")
+    return path
+
+
+@pytest.mark.parametrize("kind", ["lstm", "mlp"])
+def test_load_reference_sb3_zip_infers_architecture(tmp_path, kind):
+    from voxnav.checkpoint import load_checkpoint
+    from voxnav.policy import ActorCriticPolicy, RecurrentActorCriticPolicy
+    torch.manual_seed(2)
+    arch = dict(pi=[64, 32], vf=[48, 32])
+    pol = (RecurrentActorCriticPolicy(lstm_hidden_size=32, net_arch=arch) if kind == "lstm"
+           else ActorCriticPolicy(net_arch=arch))
+    p = _sb3_style_zip(tmp_path / "rppo_hp1_s1234_view10.zip", pol)
+    got, data = load_checkpoint(p)
+    assert data == {"sb3": True} and type(got) is type(pol)
+    sd, sd2 = pol.state_dict(), got.state_dict()
+    assert sd.keys() == sd2.keys() and all(torch.equal(sd[k], sd2[k]) for k in sd)
+
+
+def test_policy_state_load_is_strict():
+    from voxnav.checkpoint import load_policy_state
+    from voxnav.policy import RecurrentActorCriticPolicy
+    torch.manual_seed(0)
+    arch = dict(pi=[16], vf=[16])
+    pol = RecurrentActorCriticPolicy(lstm_hidden_size=8, net_arch=arch)
+    sd = {k: v.clone() for k, v in pol.state_dict().items()}
+    load_policy_state(pol, {**sd, "features_extractor.flatten.dummy": torch.zeros(1)})   # allow-listed prefix
+    bad = dict(sd)
+    bad["lstm_actor.weight_ih_l1"] = bad.pop("lstm_actor.weight_ih_l0")                 # renamed key
+    with pytest.raises(RuntimeError):
+        load_policy_state(pol, bad)
+    missing = dict(sd)
+    missing.pop("action_net.bias")
+    with pytest.raises(RuntimeError):
+        load_policy_state(pol, missing)
+
+
+def test_gridagent_is_a_gym_env_class():
+    from voxnav.gym_api import GridAgent
+    from voxnav.spaces import EnvBase
+    assert issubclass(GridAgent, EnvBase)
