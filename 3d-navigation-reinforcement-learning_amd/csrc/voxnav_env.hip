@@ -564,20 +564,28 @@ struct ObsDst {
 // then each agent's 16 tail floats.  The flush expands the bytes through the
 // LUT, so the block is 2 KiB per wave instead of the 5 KiB of float rows (the
 // byte-mark kernels' format, STAGE_WORDS_F).
-constexpr int STAGE_WORDS = 16 * 16 + 16 * 16;
+constexpr int STAGE_WORDS = 16 * 20;
 constexpr int STAGE_WORDS_F = 16 * VN_OBS_DIM;
-
-// float4 f (of the wave's 16 rows x 20) of the staged obs rows
-__device__ __forceinline__ float4 stage_float4(const uint32_t *ws, const float *tab, int f) {
-    const int a = f / 20, r = f - 20 * a;
-    if (r < 16) {
-        const uint32_t wb = ws[a * 16 + r];
-        return make_float4(tab[wb & 0xffu], tab[(wb >> 8) & 0xffu], tab[(wb >> 16) & 0xffu], tab[wb >> 24]);
-    }
-    return reinterpret_cast<const float4 *>(ws + 256)[a * 4 + (r - 16)];
+// Plane-set staging: each obs row is 20 words of 4 byte codes, so the flush
+// expands every float4 the same way (no division, no divergence) and stores
+// 1 KiB contiguous per instruction.  The window words hold belief bytes; the
+// tail words (obs[64..79], get_obs :278-291) hold codes from the belief-byte
+// values that never occur (bit7 clear but not 0x00 / 0x40; 0xC1..0xFF), whose
+// LUT entries are the tail's values: 0.0, 1.0, f32(a/5), f32(c/L).  obs[72]
+// (a quotient with many values) gets a code per agent of the block whose LUT
+// entry the agent rewrites each step (tc_slot).
+constexpr uint32_t TC_ZERO = 0x01u, TC_ONE = 0x02u, TC_ACT = 0x08u, TC_CID = 0x10u;
+constexpr uint32_t TC_ZERO4 = TC_ZERO * 0x01010101u;
+__device__ __forceinline__ uint32_t tc_slot(int agent_in_block) {        // 64 codes: 0x41..0x60, 0xC1..0xE0
+    return agent_in_block < 32 ? 0x41u + (uint32_t)agent_in_block : 0xC1u + (uint32_t)(agent_in_block - 32);
 }
 
 typedef float F4v __attribute__((ext_vector_type(4)));
+
+// float4 of a staged code word (plane-set mode): 4 LUT lookups
+__device__ __forceinline__ float4 code_float4(uint32_t wb, const float *tab) {
+    return make_float4(tab[wb & 0xffu], tab[(wb >> 8) & 0xffu], tab[(wb >> 16) & 0xffu], tab[wb >> 24]);
+}
 
 // Streaming store of one obs float4 to HBM.  VN_OBS_STORE: 0 plain, 1
 // non-temporal, 2 sc1 (write-through; the line is dropped from L2, so the
@@ -1121,7 +1129,9 @@ __device__ __forceinline__ int sense_observe(const Params &p, int8_t *map, uint6
                    : dst.stage     ? nullptr
                                    : reinterpret_cast<float4 *>(dst.row);
     float4 tail;                                                  // obs[64 + 4q .. +3]
-    if (q == 0) {
+    if (PC && to_stage) {
+        tail = make_float4((float)((double)g.visited / (double)R.total_free), 0.f, 0.f, 0.f);      // (:291)
+    } else if (q == 0) {
         tail = make_float4(g.facing == 0 ? 1.0f : 0.0f, g.facing == 1 ? 1.0f : 0.0f, g.facing == 2 ? 1.0f : 0.0f,
                            g.facing == 3 ? 1.0f : 0.0f);                                            // (:279-280)
     } else if (q == 1) {
@@ -1133,11 +1143,16 @@ __device__ __forceinline__ int sense_observe(const Params &p, int8_t *map, uint6
         tail = make_float4(0.f, 0.f, 0.f, 0.f);
     }
     if (to_stage && PC) {
-        // window bytes in obs order + the tail; the flush expands the bytes (stage_float4)
-        LdsU32 *l = (LdsU32 *)dst.stage;
+        // the row's 20 code words: window bytes in obs order, then lane q's tail word
+        LdsU32 *l = (LdsU32 *)dst.stage + dst.aslot * 20;
 #pragma unroll
-        for (int i = 0; i < 4; ++i) l[dst.aslot * 16 + 4 * i + q] = col_window<PH>(col[i], z);
-        ((LdsF4 *)(dst.stage + 256))[dst.aslot * 4 + q] = f4v(tail);
+        for (int i = 0; i < 4; ++i) l[4 * i + q] = col_window<PH>(col[i], z);
+        const uint32_t w0 = TC_ZERO4 + ((TC_ONE - TC_ZERO) << (8 * g.facing));
+        const uint32_t w1 = (TC_ACT + (uint32_t)g.last_action) | ((g.was_near_wall ? TC_ONE : TC_ZERO) << 8) |
+                            ((g.last_bump ? TC_ONE : TC_ZERO) << 16) | ((TC_CID + (uint32_t)g.cid) << 24);
+        const uint32_t c72 = tc_slot((int)(threadIdx.x >> 2));
+        if (q == 2) const_cast<float *>(tab)[c72] = tail.x;
+        l[16 + q] = q == 0 ? w0 : q == 1 ? w1 : q == 2 ? (c72 | (TC_ZERO4 & 0xffffff00u)) : TC_ZERO4;
     } else if (to_stage) {
         // float rows (20 float4 per agent): the LDS this costs is free in the
         // byte-mark kernels, whose occupancy the VGPRs set
@@ -1149,14 +1164,15 @@ __device__ __forceinline__ int sense_observe(const Params &p, int8_t *map, uint6
         }
         l[16 + q] = f4v(tail);
     } else if (glb4) {
-        // explicit address space: no flat stores
+        // explicit address space: no flat stores; non-temporal like the flush
         GlbF4 *gp = (GlbF4 *)glb4;
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
             const uint32_t wb = col_window<PH>(col[i], z);
-            gp[4 * i + q] = F4v{tab[wb & 0xffu], tab[(wb >> 8) & 0xffu], tab[(wb >> 16) & 0xffu], tab[wb >> 24]};
+            __builtin_nontemporal_store(
+                F4v{tab[wb & 0xffu], tab[(wb >> 8) & 0xffu], tab[(wb >> 16) & 0xffu], tab[wb >> 24]}, gp + 4 * i + q);
         }
-        gp[16 + q] = f4v(tail);
+        __builtin_nontemporal_store(f4v(tail), gp + 16 + q);
     }
     return t;
 }
@@ -1292,6 +1308,7 @@ __global__ __launch_bounds__(PCM ? VN_PC_BLOCK : BLOCK, PCM ? VN_PC_MIN_WAVES : 
     constexpr bool PC = PCM != 0;
     using RT = typename std::conditional<PCM == 2, uint32_t, uint64_t>::type;
     constexpr int kAgents = (PC ? VN_PC_BLOCK : BLOCK) / GROUP;
+    static_assert(!PC || kAgents <= 64, "tc_slot has 64 obs[72] codes per block");
     __shared__ float tab[TAB_SIZE];
     __shared__ __attribute__((aligned(16))) uint64_t tiles[kAgents * TileGeom<PH>::STRIDE];
     // obs rows of the step, staged per wave (STAGE_WORDS) so HBM sees 1 KiB contiguous stores
@@ -1381,7 +1398,7 @@ __global__ __launch_bounds__(PCM ? VN_PC_BLOCK : BLOCK, PCM ? VN_PC_MIN_WAVES : 
 #pragma unroll 1
                 for (int jj = 0; jj < (64 / GROUP) * (VN_OBS_DIM / 4) / 64; ++jj) {
                     const int f = lane + 64 * jj < nvalid ? lane + 64 * jj : nvalid - 1;
-                    obs_store(dst4 + f, stage_float4(wst, tab, f));
+                    obs_store(dst4 + f, code_float4(wst[f], tab));
                 }
             } else {
                 const float4 *ws4 = reinterpret_cast<const float4 *>(wst);
@@ -1649,13 +1666,11 @@ __global__ __launch_bounds__(PCM ? VN_PC_BLOCK : BLOCK, PCM ? VN_PC_MIN_WAVES : 
             const float4 *ws4 = reinterpret_cast<const float4 *>(wst);
             float4 *dst4 = reinterpret_cast<float4 *>(p.obs + ((size_t)k * p.N + wave_agent0) * VN_OBS_DIM);
             if constexpr (PC) {
-#ifndef VN_PC_FLUSH_UNROLL
-#define VN_PC_FLUSH_UNROLL 1
-#endif
-#pragma unroll VN_PC_FLUSH_UNROLL
+                // staged word f = float4 f of the wave's contiguous [16][80] rows: 1 KiB per store
+#pragma unroll
                 for (int jj = 0; jj < (64 / GROUP) * (VN_OBS_DIM / 4) / 64; ++jj) {
                     const int f = lane + 64 * jj;
-                    if (f < nvalid) obs_store(dst4 + f, stage_float4(wst, tab, f));
+                    if (f < nvalid) obs_store(dst4 + f, code_float4(wst[f], tab));
                 }
             } else {
 #pragma unroll
@@ -2936,6 +2951,12 @@ int vn_create(const VnRoomSet *rooms, int32_t n_agents, const VnConfig *cfg, int
         volatile float num = (float)(v + 2);
         lut[b] = num / 22.0f;
     }
+    // plane-set staging codes (bytes no belief cell holds): tail values
+    lut[TC_ZERO] = 0.0f;
+    lut[TC_ONE] = 1.0f;
+    for (int a = 0; a < 6; ++a) lut[TC_ACT + a] = (float)((double)a / 5.0);
+    for (int c = 0; c <= cfg->local_map_length; ++c)
+        lut[TC_CID + c] = (float)((double)c / (double)cfg->local_map_length);
     for (int a = 0; a < 6; ++a) lut[TAB_ACTION + a] = (float)((double)a / 5.0);
     for (int c = 0; c <= cfg->local_map_length; ++c)
         lut[TAB_CID + c] = (float)((double)c / (double)cfg->local_map_length);
