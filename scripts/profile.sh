@@ -9,9 +9,11 @@ cd "${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
 mkdir -p gpurun_out
 export TMPDIR=/tmp
 BARGS="${BENCH_ARGS:-} --single-step-check 0 --collector none --simple 0"
-TAG=${TAG:-r01}
+TAG=${TAG:-r02}
+PASSES=${PASSES:-trace,trace_f1,fetch,write,l2,sq,sqw,tcp}
 step() {
   local name=$1 t=$2; shift 2
+  [[ ",$PASSES," == *",$name,"* ]] || return 0
   timeout -k 10 "$t" "$@" > "gpurun_out/${TAG}_$name.log" 2>&1
   local rc=$?
   echo "[$name] rc=$rc"; grep -h '"metric"' "gpurun_out/${TAG}_$name.log" | cut -c1-200
