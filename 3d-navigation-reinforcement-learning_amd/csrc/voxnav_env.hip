@@ -277,7 +277,9 @@ struct MtBlock {            // returned by value: stays in VGPRs across the call
     uint32_t w[MT_C];
 };
 
-__device__ MtBlock mt_outputs(uint32_t seed, int j0) {
+__device__ __forceinline__ MtBlock mt_outputs_inl(uint32_t seed, int j0);
+__device__ MtBlock mt_outputs(uint32_t seed, int j0) { return mt_outputs_inl(seed, j0); }
+__device__ __forceinline__ MtBlock mt_outputs_inl(uint32_t seed, int j0) {
     MtBlock out;
     uint32_t p = mix1(c_mt_g[1], c_mt_g[0], seed);
     const uint32_t m1_1 = p;
@@ -340,7 +342,10 @@ __device__ __noinline__ MtBlock mt_refill(uint32_t seed, int j0, int32_t *err) {
     return mt_outputs(seed, j0);
 }
 
-struct MtStream {
+// INL: the refill inlined (no call: a kernel whose step loop must not spill
+// around a call site)
+template <bool INL = false>
+struct MtStreamT {
     uint32_t seed;
     uint32_t buf[MT_C];
     int used;
@@ -348,7 +353,18 @@ struct MtStream {
 
     __device__ uint32_t next() {
         if (used > 0 && (used % MT_C) == 0) {
-            const MtBlock b = mt_refill(seed, used, err);
+            MtBlock b;
+            if constexpr (INL) {
+                if (used + MT_C > MT_N - 397) {
+                    atomicOr(err, 1);
+#pragma unroll
+                    for (int j = 0; j < MT_C; ++j) b.w[j] = 0u;
+                } else {
+                    b = mt_outputs_inl(seed, used);
+                }
+            } else {
+                b = mt_refill(seed, used, err);
+            }
 #pragma unroll
             for (int j = 0; j < MT_C; ++j) buf[j] = b.w[j];
         }
@@ -366,6 +382,7 @@ struct MtStream {
         return r;
     }
 };
+using MtStream = MtStreamT<false>;
 
 // ----------------------------------------------------------------------------
 // Philox4x32-10 random policy (build-defined): one call per
@@ -582,8 +599,18 @@ __device__ __forceinline__ uint32_t tc_slot(int agent_in_block) {        // 64 c
 
 typedef float F4v __attribute__((ext_vector_type(4)));
 
-// float4 of a staged code word (plane-set mode): 4 LUT lookups
+// LDS position of LUT entry b: the common belief bytes 0x00 / 0x40 / 0x80 /
+// 0xC0 (unknown, latent wall, free, wall) would all sit in LDS bank 0 and a
+// 32-lane lookup would serialise over them; XOR-ing the low 2 bits with the
+// top 2 puts them in banks 0-3 (a permutation inside every aligned 4-group).
+#ifndef VN_TAB_SWZ
+#define VN_TAB_SWZ 1
+#endif
+__device__ __forceinline__ uint32_t tab_ix(uint32_t b) { return VN_TAB_SWZ ? b ^ ((b >> 6) & 3u) : b; }
+
+// float4 of a code word (4 belief bytes or tail codes): 4 LUT lookups
 __device__ __forceinline__ float4 code_float4(uint32_t wb, const float *tab) {
+    if (VN_TAB_SWZ) wb ^= (wb >> 6) & 0x03030303u;        // tab_ix of all 4 bytes
     return make_float4(tab[wb & 0xffu], tab[(wb >> 8) & 0xffu], tab[(wb >> 16) & 0xffu], tab[wb >> 24]);
 }
 
@@ -778,10 +805,31 @@ __device__ __forceinline__ void tile_write(uint64_t *tile, int slot, const Col<P
 
 __device__ __forceinline__ int tslot(int x, int y) { return ((x & 3) << 2) | (y & 3); }
 
+// Exchanges inside an agent group (4 lanes = one DPP quad): a quad_perm DPP
+// move is one VALU instruction, where __shfl is an LDS permute with its
+// latency on the step's dependency chain.  QP = quad_perm control
+// (2 bits per destination lane: the source lane in the quad).
+#ifndef VN_DPP
+#define VN_DPP 1
+#endif
+template <int QP>
+__device__ __forceinline__ uint32_t quad_perm(uint32_t v) {
+#if VN_DPP
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, QP, 0xf, 0xf, false);
+#else
+    const int lane = (int)(threadIdx.x & 3u);
+    return (uint32_t)__shfl((int)v, (QP >> (2 * lane)) & 3, GROUP);
+#endif
+}
+template <int SRC>
+__device__ __forceinline__ uint32_t group_bcast(uint32_t v) { return quad_perm<SRC * 0x55>(v); }
+template <int SRC>
+__device__ __forceinline__ int group_bcast(int v) { return (int)quad_perm<SRC * 0x55>((uint32_t)v); }
+
 // OR a 16-bit slot mask over the 4 lanes of the agent group
 __device__ __forceinline__ uint32_t group_or(uint32_t m) {
-    m |= (uint32_t)__shfl_xor((int)m, 1, GROUP);
-    m |= (uint32_t)__shfl_xor((int)m, 2, GROUP);
+    m |= quad_perm<0xB1>(m);      // lane ^ 1: [1, 0, 3, 2]
+    m |= quad_perm<0x4E>(m);      // lane ^ 2: [2, 3, 0, 1]
     return m;
 }
 
@@ -1018,7 +1066,7 @@ __device__ __forceinline__ int sense_observe(const Params &p, int8_t *map, uint6
     } else {                            // column dx = 0: -y s=2 (q0), -y s=1 (q1), +y s=1 (q3)
         chg |= (uint32_t)mark<PH>(col[2], z, ry, q == 3 ? 2 : 3, q == 0 ? 2 : 1) << 2;
     }
-    cold = (uint32_t)__shfl((int)cold, 2, GROUP);
+    cold = group_bcast<2>(cold);
     int t;
     if (FRESH) {
         t = 1;                                                                  // start cell (:85)
@@ -1090,11 +1138,11 @@ __device__ __forceinline__ int sense_observe(const Params &p, int8_t *map, uint6
         rel &= ~(c >= 2 ? (0xfull << (c - 2)) : ((1ull << (c + 2)) - 1ull));
     }
     {
-        const uint32_t rxl = (uint32_t)__shfl((int)(uint32_t)rel, 0, GROUP);
-        const uint32_t rxh = (uint32_t)__shfl((int)(uint32_t)(rel >> 32), 0, GROUP);
-        const uint32_t ryl = (uint32_t)__shfl((int)(uint32_t)rel, 1, GROUP);
-        const uint32_t ryh = (uint32_t)__shfl((int)(uint32_t)(rel >> 32), 1, GROUP);
-        const int pax = __shfl(pa, 0, GROUP), pay = __shfl(pa, 1, GROUP);
+        const uint32_t rxl = group_bcast<0>((uint32_t)rel);
+        const uint32_t rxh = group_bcast<0>((uint32_t)(rel >> 32));
+        const uint32_t ryl = group_bcast<1>((uint32_t)rel);
+        const uint32_t ryh = group_bcast<1>((uint32_t)(rel >> 32));
+        const int pax = group_bcast<0>(pa), pay = group_bcast<1>(pa);
         const uint64_t lane_sel = 0x1111111111111111ull << q;
         uint64_t mx = (VN_ABLATE & 96u) ? 0ull : (((uint64_t)rxh << 32) | rxl) & lane_sel;
         uint64_t my = (VN_ABLATE & 96u) ? 0ull : (((uint64_t)ryh << 32) | ryl) & lane_sel;
@@ -1151,7 +1199,7 @@ __device__ __forceinline__ int sense_observe(const Params &p, int8_t *map, uint6
         const uint32_t w1 = (TC_ACT + (uint32_t)g.last_action) | ((g.was_near_wall ? TC_ONE : TC_ZERO) << 8) |
                             ((g.last_bump ? TC_ONE : TC_ZERO) << 16) | ((TC_CID + (uint32_t)g.cid) << 24);
         const uint32_t c72 = tc_slot((int)(threadIdx.x >> 2));
-        if (q == 2) const_cast<float *>(tab)[c72] = tail.x;
+        if (q == 2) const_cast<float *>(tab)[tab_ix(c72)] = tail.x;
         l[16 + q] = q == 0 ? w0 : q == 1 ? w1 : q == 2 ? (c72 | (TC_ZERO4 & 0xffffff00u)) : TC_ZERO4;
     } else if (to_stage) {
         // float rows (20 float4 per agent): the LDS this costs is free in the
@@ -1160,7 +1208,7 @@ __device__ __forceinline__ int sense_observe(const Params &p, int8_t *map, uint6
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
             const uint32_t wb = col_window<PH>(col[i], z);
-            l[4 * i + q] = F4v{tab[wb & 0xffu], tab[(wb >> 8) & 0xffu], tab[(wb >> 16) & 0xffu], tab[wb >> 24]};
+            l[4 * i + q] = f4v(code_float4(wb, tab));
         }
         l[16 + q] = f4v(tail);
     } else if (glb4) {
@@ -1170,7 +1218,7 @@ __device__ __forceinline__ int sense_observe(const Params &p, int8_t *map, uint6
         for (int i = 0; i < 4; ++i) {
             const uint32_t wb = col_window<PH>(col[i], z);
             __builtin_nontemporal_store(
-                F4v{tab[wb & 0xffu], tab[(wb >> 8) & 0xffu], tab[(wb >> 16) & 0xffu], tab[wb >> 24]}, gp + 4 * i + q);
+                f4v(code_float4(wb, tab)), gp + 4 * i + q);
         }
         __builtin_nontemporal_store(f4v(tail), gp + 16 + q);
     }
@@ -1282,8 +1330,54 @@ __device__ __forceinline__ void group_reset(const Params &p, int8_t *map, uint64
 // ----------------------------------------------------------------------------
 // the step kernel: 4 lanes per agent, K fused steps, SB3 auto-reset
 // ----------------------------------------------------------------------------
+#ifndef VN_PHILOX16
+#define VN_PHILOX16 1        // one Philox call per lane per 16 steps (striped over the quad)
+#endif
+#ifndef VN_REWARD_STRIPE
+#define VN_REWARD_STRIPE 1   // rollout-buffer call: rewards evaluated and stored per 4-step block
+#endif
+
+// compute_reward (envs/CubicEnv.py:169-224) from a step's events, f64 in the
+// reference's order, rounded to the f32 rollout buffer.  ev: bits 0-4
+// min(center visit count, 25) (pen = min(0.5, 0.02 n) is 0.5 from n = 25 on:
+// 25 * 0.02 rounds to 0.5 in f64), 5 moved, 6 was_near_wall, 7 repeated
+// non-back move, 8 back after back, 9 explored, 10 done, 11 truncated.
+__device__ __forceinline__ float reward_of_events(uint32_t ev, double crash_penalty) {
+    double r = -0.05;
+    const double pen = (double)(ev & 31u) * 0.02;
+    r -= (0.5 < pen) ? 0.5 : pen;
+    if (!(ev & 32u)) {
+        r += crash_penalty;
+    } else {
+        if (ev & 64u) r += 0.15;
+        if (ev & 128u) r += 0.05;
+        if (ev & 256u) r -= 0.5;
+    }
+    if (ev & 512u) r += 1.0;
+    if (ev & 1024u) r += 100.0;
+    if (ev & 2048u) r += -5.0;
+    return (float)r;
+}
+
 constexpr int BLOCK = 256;
 constexpr int AGENTS_PER_BLOCK = BLOCK / GROUP;
+
+#ifndef VN_ENV_PROF
+#define VN_ENV_PROF 0   // diagnostics build: per-section shader-clock totals of the step loop (vn_debug_env_prof)
+#endif
+#if VN_ENV_PROF
+__device__ unsigned long long g_env_prof[16];
+#define ENV_T(k)                                                   \
+    do {                                                           \
+        const uint64_t t_ = __builtin_amdgcn_s_memtime();          \
+        eprof[k] += t_ - tprev;                                    \
+        tprev = t_;                                                \
+    } while (0)
+#else
+#define ENV_T(k) \
+    do {         \
+    } while (0)
+#endif
 
 // EXT: actions come from p.actions (else the Philox random policy).  A
 // separate instantiation: with both sources in one loop the action register
@@ -1300,12 +1394,24 @@ constexpr int AGENTS_PER_BLOCK = BLOCK / GROUP;
 #ifndef VN_PC_MIN_WAVES
 #define VN_PC_MIN_WAVES 4   // waves per SIMD the VGPR budget is set for
 #endif
+#ifndef VN_DEFER_PC
+#define VN_DEFER_PC 0     // deferred stores: measured slower (DESIGN 7.4)
+#endif
+#ifndef VN_DEFER_ALL
+#define VN_DEFER_ALL 0      // byte-mark kernels: deferring spills them (VGPRs) -- measured slower
+#endif
+// rows fwd, right, back, left; cols facing N,E,S,W; dirs 0 +x, 1 -x, 2 +y, 3 -y
+constexpr uint32_t kMoveDir = (2u << 0) | (0u << 2) | (3u << 4) | (1u << 6)       // fwd
+                              | (0u << 8) | (3u << 10) | (1u << 12) | (2u << 14)   // right
+                              | (3u << 16) | (1u << 18) | (2u << 20) | (0u << 22)  // back
+                              | (1u << 24) | (2u << 26) | (0u << 28) | (3u << 30); // left
 template <int PH, bool EXT, bool FAST, bool RESET_ONLY, int PCM>
 #ifndef VN_MIN_WAVES_PER_SIMD
 #define VN_MIN_WAVES_PER_SIMD 4   // <= 128 VGPRs: the 16 waves of 256 agents per CU resident at once
 #endif
 __global__ __launch_bounds__(PCM ? VN_PC_BLOCK : BLOCK, PCM ? VN_PC_MIN_WAVES : VN_MIN_WAVES_PER_SIMD) void env_kernel(Params p) {
     constexpr bool PC = PCM != 0;
+    constexpr bool DEFER_K = (PC && VN_DEFER_PC) || VN_DEFER_ALL;
     using RT = typename std::conditional<PCM == 2, uint32_t, uint64_t>::type;
     constexpr int kAgents = (PC ? VN_PC_BLOCK : BLOCK) / GROUP;
     static_assert(!PC || kAgents <= 64, "tc_slot has 64 obs[72] codes per block");
@@ -1320,20 +1426,22 @@ __global__ __launch_bounds__(PCM ? VN_PC_BLOCK : BLOCK, PCM ? VN_PC_MIN_WAVES : 
     if (p.N < 0) lds_pad[threadIdx.x] = 0ull;
     if (p.N < 0) p.obs[0] = (float)lds_pad[threadIdx.x ^ 1];
 #endif
-    for (int k = threadIdx.x; k < TAB_SIZE; k += blockDim.x) tab[k] = p.lut[k];
+    const int q = threadIdx.x & (GROUP - 1);
+    const int i = (int)((blockIdx.x * blockDim.x + threadIdx.x) / GROUP);
+    const bool active = i < p.N;
+    const int ai = active ? i : 0;
+    // the agent's state loads are in flight while the block stages its LUT
+    const uint4 hot0 = p.hot[ai];
+    uint32_t next_seed = p.next_seed[ai];
+    for (int k = threadIdx.x; k < TAB_SIZE; k += blockDim.x) tab[k < 256 ? tab_ix((uint32_t)k) : k] = p.lut[k];
     __syncthreads();
     // a wave without agents leaves (no block-wide barrier follows)
     const int wave_agent0 = (int)((blockIdx.x * blockDim.x + (threadIdx.x & ~63)) / GROUP);
     if (wave_agent0 >= p.N) return;
 
-    const int q = threadIdx.x & (GROUP - 1);
-    const int i = (int)((blockIdx.x * blockDim.x + threadIdx.x) / GROUP);
-    const bool active = i < p.N;
-    const int ai = active ? i : 0;
     uint64_t *tile = tiles + (threadIdx.x / GROUP) * TileGeom<PH>::STRIDE;
-    Agent g = unpack(p.hot[ai]);
+    Agent g = unpack(hot0);
     Room R = load_room(p, active ? g.room : 0);
-    uint32_t next_seed = p.next_seed[ai];
     int8_t *map = p.belief + (size_t)ai * p.agent_bytes;
     uint32_t dirty = 0;
     PlaneCache pc_;
@@ -1359,10 +1467,57 @@ __global__ __launch_bounds__(PCM ? VN_PC_BLOCK : BLOCK, PCM ? VN_PC_MIN_WAVES : 
         return;
     }
 
+    // Step 0's move needs no memory: the hot state holds the move mask of the
+    // agent's cell and the first action is the Philox draw (or p.actions[i]).
+    // VN_PREMOVE: the window is filled around the cell after that move, so the
+    // first step has no shift (one dependent load round trip less per launch;
+    // a one-step launch has three left: state, window, the new cell's ray
+    // record).  The move itself still runs in step 0 as usual.
+#ifndef VN_PREMOVE
+#define VN_PREMOVE 1
+#endif
+    constexpr bool PREMOVE = VN_PREMOVE && !DEFER_K;
+    uint32_t a16[4] = {0u, 0u, 0u, 0u};          // VN_PHILOX16: the actions of the current 16-step chunk
+    auto philox_chunk = [&](uint64_t tb) {
+        const uint4 o = philox4x32_10(p.policy_seed, p.gid_base + (uint64_t)ai, ((tb >> 2) & ~3ull) + (uint64_t)q);
+        const uint32_t mine = __umulhi(o.x, 6u) | (__umulhi(o.y, 6u) << 8) | (__umulhi(o.z, 6u) << 16) |
+                              (__umulhi(o.w, 6u) << 24);
+        a16[0] = group_bcast<0>(mine);
+        a16[1] = group_bcast<1>(mine);
+        a16[2] = group_bcast<2>(mine);
+        a16[3] = group_bcast<3>(mine);
+    };
+    if (!EXT && VN_PHILOX16 && !DEFER_K) philox_chunk(p.t0);
     if (active) {
-        if (PC) pset_fill(p, map, ps, g, R, q);
-        tile_fill<PH, PC, RT>(p, map, tile, ps, g, R, q);
+        Agent gf = g;                               // the fill's window center
+        if (PREMOVE && p.K > 0) {
+            int a;
+            if (EXT) {
+                a = p.actions[i];
+            } else if (VN_PHILOX16) {
+                const uint32_t w = a16[(uint32_t)(p.t0 >> 2) & 3u];
+                a = (int)((w >> (8u * ((uint32_t)p.t0 & 3u))) & 0xffu);
+            } else {
+                const uint4 o = philox4x32_10(p.policy_seed, p.gid_base + (uint64_t)ai, p.t0 >> 2);
+                const uint32_t t3 = (uint32_t)p.t0 & 3u;
+                a = (int)__umulhi(t3 == 0u ? o.x : t3 == 1u ? o.y : t3 == 2u ? o.z : o.w, 6u);
+            }
+            if (a < 4) {
+                const int dir = (int)((kMoveDir >> (2 * (a * 4 + g.facing))) & 3u);
+                if ((g.move_mask >> dir) & 1u) {
+                    gf.x += (dir == 0) - (dir == 1);
+                    gf.y += (dir == 2) - (dir == 3);
+                }
+            }
+        }
+        if (PC) pset_fill(p, map, ps, gf, R, q);
+        tile_fill<PH, PC, RT>(p, map, tile, ps, gf, R, q);
     }
+#if VN_ENV_PROF
+    uint64_t eprof[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    uint64_t tprev = __builtin_amdgcn_s_memtime();
+    const uint64_t tstart = tprev;
+#endif
 #ifndef VN_STAGE_OBS
 #define VN_STAGE_OBS 1
 #endif
@@ -1377,13 +1532,7 @@ __global__ __launch_bounds__(PCM ? VN_PC_BLOCK : BLOCK, PCM ? VN_PC_MIN_WAVES : 
     // lanes past the wave's last agent repeat its last float4 or store to
     // p.scratch, all 4 lanes of an agent store its reward -- so the
     // compiler's vmcnt waits stay exact.
-#ifndef VN_DEFER_PC
-#define VN_DEFER_PC 0     // deferred stores: measured slower (DESIGN 7.4)
-#endif
-#ifndef VN_DEFER_ALL
-#define VN_DEFER_ALL 0      // byte-mark kernels: deferring spills them (VGPRs) -- measured slower
-#endif
-    constexpr bool DEFER = (PC && VN_DEFER_PC) || VN_DEFER_ALL;
+    constexpr bool DEFER = DEFER_K;
     const int lane = threadIdx.x & 63;
     const int nvalid = (p.N - wave_agent0) * (VN_OBS_DIM / 4);       // float4s of the wave's agents (> 0)
     int pk = -1;                                                      // the step whose outputs are pending
@@ -1462,11 +1611,7 @@ __global__ __launch_bounds__(PCM ? VN_PC_BLOCK : BLOCK, PCM ? VN_PC_MIN_WAVES : 
             int dir;
             if (a < 4) {
                 // rows fwd, right, back, left; cols facing N,E,S,W; dirs 0 +x, 1 -x, 2 +y, 3 -y
-                constexpr uint32_t kDir = (2u << 0) | (0u << 2) | (3u << 4) | (1u << 6)       // fwd
-                                          | (0u << 8) | (3u << 10) | (1u << 12) | (2u << 14)   // right
-                                          | (3u << 16) | (1u << 18) | (2u << 20) | (0u << 22)  // back
-                                          | (1u << 24) | (2u << 26) | (0u << 28) | (3u << 30); // left
-                dir = (int)((kDir >> (2 * (a * 4 + g.facing))) & 3u);
+                dir = (int)((kMoveDir >> (2 * (a * 4 + g.facing))) & 3u);
                 g.facing = (int)((0x8Du >> (2 * dir)) & 3u);  // +x->E(1) -x->W(3) +y->N(0) -y->S(2)
             } else {
                 dir = (a == 4) ? 4 : 5;
@@ -1555,14 +1700,32 @@ __global__ __launch_bounds__(PCM ? VN_PC_BLOCK : BLOCK, PCM ? VN_PC_MIN_WAVES : 
     // the step's outputs stored within the step (measured faster than the
     // deferred order, which also needs more VGPRs than the byte-mark kernels
     // have at 4 waves/SIMD)
+    //
+    // Work striped over the agent's 4 lanes instead of repeated by each:
+    //  * Philox (VN_PHILOX16): lane q computes the 4-step block cb + q of the
+    //    16-step chunk cb..cb+3, so one call per lane covers 16 steps; the
+    //    four words are broadcast in the quad;
+    //  * the rollout-buffer call (FAST, VN_REWARD_STRIPE): each step records
+    //    its reward events (12 bits) and after the 4-step block lane q
+    //    evaluates step q's f64 reward and stores its reward / terminated /
+    //    truncated (one store instruction per output per block).
+    constexpr bool STRIPE_R = FAST && VN_REWARD_STRIPE;
     for (int k = 0; k < p.K;) {
     const uint64_t tb = p.t0 + (uint64_t)k;
     uint32_t acts = 0;                                    // 4 actions, 8 bits each, by (t & 3)
     if (!EXT) {
-        const uint4 o = philox4x32_10(p.policy_seed, p.gid_base + (uint64_t)ai, tb >> 2);
-        acts = __umulhi(o.x, 6u) | (__umulhi(o.y, 6u) << 8) | (__umulhi(o.z, 6u) << 16) | (__umulhi(o.w, 6u) << 24);
+        if (VN_PHILOX16) {
+            if (k != 0 && (tb & 15u) == 0u) philox_chunk(tb);   // k == 0: the prologue's chunk
+            const uint32_t sel = (uint32_t)(tb >> 2) & 3u;
+            acts = sel == 0u ? a16[0] : sel == 1u ? a16[1] : sel == 2u ? a16[2] : a16[3];
+        } else {
+            const uint4 o = philox4x32_10(p.policy_seed, p.gid_base + (uint64_t)ai, tb >> 2);
+            acts = __umulhi(o.x, 6u) | (__umulhi(o.y, 6u) << 8) | (__umulhi(o.z, 6u) << 16) | (__umulhi(o.w, 6u) << 24);
+        }
     }
     const int jn = (4 - (int)(tb & 3u)) < (p.K - k) ? (4 - (int)(tb & 3u)) : (p.K - k);
+    uint64_t ev4 = 0;                                     // STRIPE_R: reward events by slot (t & 3), 16 bits each
+    const int kb = k;
     for (int j = 0; j < jn; ++j, ++k) {
         bool finished = false;
         const size_t row = (size_t)k * (size_t)p.N + (size_t)i;
@@ -1582,11 +1745,7 @@ __global__ __launch_bounds__(PCM ? VN_PC_BLOCK : BLOCK, PCM ? VN_PC_MIN_WAVES : 
             // do_action (:134-166): relative move table by facing -> axis dir
             int dir;
             if (a < 4) {
-                constexpr uint32_t kDir = (2u << 0) | (0u << 2) | (3u << 4) | (1u << 6)       // fwd
-                                          | (0u << 8) | (3u << 10) | (1u << 12) | (2u << 14)   // right
-                                          | (3u << 16) | (1u << 18) | (2u << 20) | (0u << 22)  // back
-                                          | (1u << 24) | (2u << 26) | (0u << 28) | (3u << 30); // left
-                dir = (int)((kDir >> (2 * (a * 4 + g.facing))) & 3u);
+                dir = (int)((kMoveDir >> (2 * (a * 4 + g.facing))) & 3u);
                 g.facing = (int)((0x8Du >> (2 * dir)) & 3u);
             } else {
                 dir = (a == 4) ? 4 : 5;
@@ -1599,13 +1758,15 @@ __global__ __launch_bounds__(PCM ? VN_PC_BLOCK : BLOCK, PCM ? VN_PC_MIN_WAVES : 
             }
             // the step's loads, all in flight together: entering window
             // column (and plane set), the new cell's ray record, its plane rows
-            const bool shifted = moved && dir < 4;
+            // (PREMOVE: the launch's window was filled around step 0's cell)
+            const bool shifted = moved && dir < 4 && !(PREMOVE && k == 0);
             ShiftLoad<PH> sl;
             SetLoad pl;
             if (shifted) tile_shift_issue<PH>(p, map, tile, dir, g.x, g.y, R, dirty, q, sl);
             if (PC && shifted) pset_shift_issue(p, map, ps, dir, g.x, g.y, R, pdirty, q, pl);
             const uint2 rec = p.rays[R.ray_off + (uint32_t)((g.x * R.D + g.y) * R.H + g.z)];
             if (!PC) plane_prefetch<PH>(p, map, pc_, g.x, g.y, g.z, q);
+            ENV_T(0);
             if (shifted) {
                 if constexpr (PC) {
                     pdirty = pset_shift_commit(ps, pl, pdirty, q);
@@ -1613,6 +1774,7 @@ __global__ __launch_bounds__(PCM ? VN_PC_BLOCK : BLOCK, PCM ? VN_PC_MIN_WAVES : 
                 }
                 dirty = tile_shift_commit<PH>(tile, sl, dirty);
             }
+            ENV_T(1);
 
             bool explored = false;
             const ObsDst dst{p.obs + row * VN_OBS_DIM,
@@ -1620,7 +1782,33 @@ __global__ __launch_bounds__(PCM ? VN_PC_BLOCK : BLOCK, PCM ? VN_PC_MIN_WAVES : 
                              p.autoreset != 0, truncated, aslot};
             const int vv = sense_observe<PH, false, PC, RT>(p, map, tile, dirty, pc_, ps, pdirty, g, R, moved,
                                                             explored, tab, dst, rec, q);
+            ENV_T(2);
 
+            if constexpr (STRIPE_R) {
+                // the reward's inputs (reward_events), the state updates in place
+                uint32_t ev = (uint32_t)(vv < 25 ? vv : 25) | (moved ? 32u : 0u);
+                if (!moved) {
+                    g.last_bump = true;
+                    if (g.bumps < 0x3ffffffu) ++g.bumps;
+                } else {
+                    g.last_bump = false;
+                    if (g.was_near_wall) {
+                        g.was_near_wall = false;
+                        ev |= 64u;
+                    }
+                    if (g.last_action != 2 && a == g.last_action && g.last_action < 4) ev |= 128u;
+                    if (g.last_action == 2 && a == 2) ev |= 256u;
+                }
+                if (explored) ev |= 512u;
+                if (g.visited >= R.finish_visits) {        // visited / total >= 0.84 (:212-215)
+                    g.done = true;
+                    ev |= 1024u;
+                }
+                if (truncated) ev |= 2048u;
+                g.last_action = a;
+                ev4 |= (uint64_t)ev << (16u * ((uint32_t)tt & 3u));
+                finished = g.done || truncated;
+            } else {
             // compute_reward (:169-224), f64 in the reference's order
             double r = -0.05;
             const double pen = (double)vv * 0.02;
@@ -1653,7 +1841,9 @@ __global__ __launch_bounds__(PCM ? VN_PC_BLOCK : BLOCK, PCM ? VN_PC_MIN_WAVES : 
                 if (FAST || p.trunc) p.trunc[row] = truncated ? 1 : 0;
             }
             finished = g.done || truncated;
+            }   // !STRIPE_R
         }
+        ENV_T(3);
         const bool need = p.autoreset && finished;
         if (__ballot(need)) {
             const uint32_t seed = next_seed;
@@ -1661,10 +1851,13 @@ __global__ __launch_bounds__(PCM ? VN_PC_BLOCK : BLOCK, PCM ? VN_PC_MIN_WAVES : 
                                     need ? p.obs + row * VN_OBS_DIM : nullptr, wst, aslot, q);
             if (need) next_seed = seed + p.seed_stride;
         }
+        ENV_T(4);
         // the wave's 16 staged obs rows: contiguous in [K][N][80]
         if (VN_STAGE_OBS && !(VN_ABLATE & 16u)) {
             const float4 *ws4 = reinterpret_cast<const float4 *>(wst);
             float4 *dst4 = reinterpret_cast<float4 *>(p.obs + ((size_t)k * p.N + wave_agent0) * VN_OBS_DIM);
+            if (VN_ABLATE & 256u)      // diagnostics: the same stores into a 1.3 MB (L2-resident) region
+                dst4 = reinterpret_cast<float4 *>(p.obs) + (size_t)((wave_agent0 / 16) & 255) * 320;
             if constexpr (PC) {
                 // staged word f = float4 f of the wave's contiguous [16][80] rows: 1 KiB per store
 #pragma unroll
@@ -1680,6 +1873,21 @@ __global__ __launch_bounds__(PCM ? VN_PC_BLOCK : BLOCK, PCM ? VN_PC_MIN_WAVES : 
                 }
             }
         }
+        ENV_T(5);
+    }
+    if constexpr (STRIPE_R) {
+        // lane q: the reward of slot q of the block (steps kb .. kb + jn - 1
+        // are slots s0 .. s0 + jn - 1)
+        const int s0 = (int)(tb & 3u);
+        if (active && q >= s0 && q < s0 + jn && !(VN_ABLATE & 128u)) {
+            const uint32_t ev = (uint32_t)(ev4 >> (16 * q)) & 0xffffu;
+            const float r = reward_of_events(ev, p.crash_penalty);
+            const size_t o = (size_t)(kb + q - s0) * (size_t)p.N + (size_t)i;
+            p.reward[o] = r;
+            p.term[o] = (uint8_t)((ev >> 10) & 1u);
+            p.trunc[o] = (uint8_t)(ev >> 11);
+        }
+        ENV_T(6);
     }
     }
     }
@@ -1691,6 +1899,13 @@ __global__ __launch_bounds__(PCM ? VN_PC_BLOCK : BLOCK, PCM ? VN_PC_MIN_WAVES : 
             p.next_seed[i] = next_seed;
         }
     }
+#if VN_ENV_PROF
+    if (FAST && PC && (threadIdx.x & 63) == 0) {
+        for (int k = 0; k < 7; ++k) atomicAdd(&g_env_prof[k], (unsigned long long)eprof[k]);
+        atomicAdd(&g_env_prof[7], (unsigned long long)(tprev - tstart));
+        atomicAdd(&g_env_prof[8], 1ull);
+    }
+#endif
 }
 
 // ============================================================================
@@ -1727,12 +1942,22 @@ __device__ __forceinline__ int facing_of(int d) { return (int)((0x8Du >> (2 * d)
 // MT draws of simpleEnv's load_room (:350, :410-426): room, start (drawn if
 // absent or on a wall), goal (drawn if absent or on a wall).  Returns
 // (start | room<<24, goal).
-__device__ __noinline__ uint2 simple_draw(const EnvConst *ec, uint32_t seed) {
-    MtStream mt;
+template <bool INL>
+__device__ __attribute__((always_inline)) inline uint2 simple_draw_t(const EnvConst *ec, uint32_t seed);
+__device__ __noinline__ uint2 simple_draw(const EnvConst *ec, uint32_t seed) { return simple_draw_t<false>(ec, seed); }
+template <bool INL>
+__device__ __attribute__((always_inline)) inline uint2 simple_draw_t(const EnvConst *ec, uint32_t seed) {
+    MtStreamT<INL> mt;
     mt.seed = seed;
     mt.used = 0;
     mt.err = ec->err;
-    mt_first_outputs(seed, mt.buf);
+    if constexpr (INL) {
+        const MtBlock b0 = mt_outputs_inl(seed, 0);
+#pragma unroll
+        for (int j = 0; j < MT_C; ++j) mt.buf[j] = b0.w[j];
+    } else {
+        mt_first_outputs(seed, mt.buf);
+    }
     const int room = ec->use_room_draw ? (int)mt.below((uint32_t)ec->n_rooms) : 0;
     const Room R = load_room_c(ec, room);
     auto is_wall = [&](uint32_t c) {
@@ -2446,6 +2671,305 @@ __global__ __launch_bounds__(128) void simple_split_kernel(Params p) {
     }
 }
 
+// ----------------------------------------------------------------------------
+// The bit-plane step with 4 lanes per agent (16 agents per wave, so 65,536
+// agents make 4 waves per SIMD instead of one: the step's dependent loads --
+// the new cell's ray record and S words -- are hidden by the other waves).
+// Lane j of an agent group owns the rays along ABSOLUTE directions j and
+// j + 4 (0 +x, 1 -x, 2 +y, 3 -y, 4 +z, 5 -z; lanes 2, 3 have one ray) and
+// writes each at the obs slot the agent's facing gives it (forward, left,
+// right, backward, up, down: envs/simpleEnv.py:233); lane 3 also writes
+// last_action.  The step's control (move, visit, reward) is the same on the 4
+// lanes, and so are the addresses of a step's loads (one request per agent).
+// Edge-quirk marks (Q) are atomic ORs: the up and down rays share a QZ word.
+// Outputs: obs rows staged per wave in LDS (16 rows, contiguous in HBM);
+// reward / terminated / truncated striped -- each step records 5 event bits
+// and after a 4-step block lane j evaluates the f64 reward of the block's step
+// j and stores the three outputs.  (8 lanes per agent needs <= 64 VGPRs for its
+// 8 waves per SIMD and spilled.)
+// ----------------------------------------------------------------------------
+constexpr int SG = 4;
+constexpr int SG_APW = 64 / SG;   // agents per wave
+#ifndef VN_SG_INLINE_DRAW
+#define VN_SG_INLINE_DRAW 0
+#endif
+#ifndef VN_SG_MIN_WAVES
+#define VN_SG_MIN_WAVES 4   // <= 128 VGPRs: the 16 waves of 256 agents per CU resident
+#endif
+
+// obs slot of absolute direction j < 4 for facing f: slot k with rel_dir of
+// [fwd, left, right, back][k] == j
+constexpr uint32_t pack_obs_slot() {
+    uint32_t v = 0;
+    const int rel_of_slot[4] = {0, 3, 1, 2};   // forward, left, right, backward (action indices)
+    for (int f = 0; f < 4; ++f)
+        for (int k = 0; k < 4; ++k) v |= (uint32_t)k << (2 * (4 * f + kRelDir[rel_of_slot[k]][f]));
+    return v;
+}
+__device__ __forceinline__ int obs_slot(int j, int facing) {
+    return j >= 4 ? j : (int)((pack_obs_slot() >> (2 * (4 * facing + j))) & 3u);
+}
+
+// QZ words are OR-ed atomically (at L2) by any lane of the group: read them
+// coherently (not from a possibly stale L1 line)
+__device__ __forceinline__ uint32_t qz_load(const uint32_t *q) {
+    return __hip_atomic_load(q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// simple_ray on the bit planes for one lane's direction d (sb_ray with the
+// edge-quirk mark as an atomic OR, since two lanes may mark one QZ word)
+template <int LMAX>
+__device__ __forceinline__ float sg_ray(const Params &p, const SPlanes &pl, int gx, int gy, int gz, bool hasq,
+                                        uint64_t run, uint2 rec, int d, float *out, bool &newq) {
+    const uint32_t e8 = ray_e8(rec, d);
+    const int n = (int)(e8 & 0x7fu);
+    const int L = p.L;
+    const int m = n < L ? n : L;
+    const int ax = d >> 1;
+    const int sgn = (d & 1) ? -1 : 1;
+    const int pos = ax == 0 ? gx : ax == 1 ? gy : gz;
+#pragma unroll
+    for (int s = 0; s < LMAX; ++s) {
+        if (s >= L) break;
+        float v;
+        if (s < m) {
+            const int c = pos + sgn * (s + 1);
+            uint32_t b = (uint32_t)(run >> c) & 1u;
+            if (hasq) {
+                const int qx = ax == 0 ? c : gx, qy = ax == 1 ? c : gy, qzz = ax == 2 ? c : gz;
+                if ((qz_load(pl.qz + qx * p.pd + qy) >> qzz) & 1u) b = 2u;
+            }
+            v = (float)b;
+        } else {
+            v = s == n ? 2.0f : -1.0f;   // wall / edge terminator, then padding (:321-331)
+        }
+        out[s] = v;
+    }
+    if (n < L && !(e8 & 0x80u) && n >= 1) {   // edge quirk (:311-319)
+        const int c = pos + sgn * n;
+        const int qx = ax == 0 ? c : gx, qy = ax == 1 ? c : gy, qzz = ax == 2 ? c : gz;
+        atomicOr(pl.qz + qx * p.pd + qy, 1u << qzz);
+        newq = true;
+    }
+    return (float)m * 0.25f;                 // round(count * 0.25, 2) is exact
+}
+
+// the agent's obs row into the LDS stage (lane j: rays j and j + 4, lane 3
+// also last_action; j >= 2 * SG: nothing)
+template <int LMAX>
+__device__ __forceinline__ void sg_observe(const Params &p, const SPlanes &pl, Agent &g, const SRows &w, float *row,
+                                           int j) {
+    const int L = p.L;
+    bool newq = false;
+    const bool hasq = (g.move_mask & 1u) != 0u;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+        const int d = j + SG * h;
+        if (d < 6) {
+            const int s = obs_slot(d, g.facing);
+            const uint64_t run = d < 2 ? w.wx : d < 4 ? w.wy : (uint64_t)w.wz;
+            row[6 * L + s] = sg_ray<LMAX>(p, pl, g.x, g.y, g.z, hasq, run, w.rec, d, row + s * L, newq);
+        }
+    }
+    if (j == 3) row[6 * L + 6] = (float)g.last_action;
+    // any lane's quirk mark sets the agent's has-Q flag
+    const uint64_t qb = __ballot(newq);
+    if ((qb >> (threadIdx.x & (64u - SG))) & ((1ull << SG) - 1ull)) g.move_mask |= 1u;
+}
+
+// reset of the agents with `need` (sb_reset_wave with 8 lanes per agent)
+template <int LMAX>
+__device__ __forceinline__ void sg_reset_wave(const Params &p, const SPlanes &pl, bool need, uint32_t seed, Agent &g,
+                                              uint32_t &goal, Room &R, SRows &w, float *row, int lane, int j,
+                                              int wave_a0) {
+    uint2 drawn = make_uint2(0u, 0u);
+    // inlined: a call would make the step loop keep its state in the callee-saved
+    // registers / scratch (measured: 35 VGPR spills)
+    if (need) drawn = VN_SG_INLINE_DRAW ? simple_draw_t<true>(p.envc, seed) : simple_draw(p.envc, seed);
+    uint64_t m = __ballot(need && j == 0);
+    const uint32_t n16 = p.agent_bytes >> 4;
+    while (m) {
+        const int src = __ffsll((unsigned long long)m) - 1;
+        m &= m - 1;
+        uint4 *base = reinterpret_cast<uint4 *>(p.belief + (size_t)(wave_a0 + src / SG) * p.agent_bytes);
+        for (uint32_t q = (uint32_t)lane; q < n16; q += 64u) base[q] = make_uint4(0u, 0u, 0u, 0u);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+    if (need) {
+        g.room = (int)(drawn.x >> 24);
+        R = load_room(p, g.room);
+        g.x = drawn.x & 0xff;
+        g.y = (drawn.x >> 8) & 0xff;
+        g.z = (drawn.x >> 16) & 0xff;
+        goal = drawn.y;
+        g.facing = 0;
+        g.last_action = 0;
+        g.done = g.last_bump = g.near_wall = g.was_near_wall = false;
+        g.step_count = 0;
+        g.visited = 1;
+        g.bumps = 0;
+        g.cid = 0;
+        g.move_mask = 0;
+        w.wx = 1ull << g.x;                                                     // :86
+        w.wy = 1ull << g.y;
+        w.wz = 1u << g.z;
+        if (j == 0) pl.sx[g.y * p.ph + g.z] = w.wx;
+        if (j == 1) pl.sy[g.x * p.ph + g.z] = w.wy;
+        if (j == 2) pl.sz[g.x * p.pd + g.y] = w.wz;
+        w.rec = p.rays[R.ray_off + (uint32_t)((g.x * R.D + g.y) * R.H + g.z)];
+    }
+    sg_observe<LMAX>(p, pl, g, w, row, need ? j : 2 * SG);
+}
+
+// compute_reward (envs/simpleEnv.py:189-217) from a step's events: bit 0
+// moved, 1 a repeated-direction action (a != 2 and a < 4: last_action == a at
+// that point), 2 goal reached, 3 truncated, 4 explored; f64 in the
+// reference's order
+__device__ __forceinline__ double simple_reward(uint32_t ev) {
+    double r = -0.1;
+    if (!(ev & 1u)) r += -10.0;
+    if (ev & 2u) r += 0.05;
+    if (ev & 4u) r += 100.0;
+    if (ev & 8u) r += 0.0;
+    if (ev & 16u) r += 1.0;
+    return r;
+}
+
+template <int LMAX>
+__global__ __launch_bounds__(256, VN_SG_MIN_WAVES) void simple_group_kernel(Params p) {
+    extern __shared__ float sm[];                     // per wave: stage[SG_APW][OD]
+    const int OD = p.obs_dim, L = p.L;
+    const int lane = threadIdx.x & 63;
+    const int j = lane & (SG - 1);
+    const int slot = lane / SG;
+    const int wave_a0 = (int)((blockIdx.x * blockDim.x + (threadIdx.x & ~63u)) / SG);
+    if (wave_a0 >= p.N) return;                       // no block barrier in this kernel
+    const int i = wave_a0 + slot;
+    const bool live = i < p.N;
+    const int ai = live ? i : wave_a0;
+    const int rows = min(SG_APW, p.N - wave_a0);
+    float *stage = sm + (threadIdx.x >> 6) * (SG_APW * OD);
+    float *row = stage + slot * OD;
+    const SPlanes pl = splanes(p, ai);
+    Agent g = unpack(p.hot[ai]);
+    uint32_t goal = p.goal[ai];
+    uint32_t next_seed = p.next_seed[ai];
+    Room R = load_room(p, g.room);
+    SRows w;
+    sb_load_rows(p, pl, g, R, w);
+
+    uint32_t a16[4] = {0u, 0u, 0u, 0u};              // Philox words of the 16-step chunk (lane j: block + j)
+    uint32_t ev4 = 0;                                 // reward events of the 4-step block, 8 bits by slot t & 3
+    int kb = 0;                                       // launch step of the block's first slot
+    for (int k = 0; k < p.K; ++k) {
+        const uint64_t t = p.t0 + (uint64_t)k;
+        int a = 0;
+        if (p.actions) {
+            a = p.actions[(size_t)k * p.N + ai];
+        } else {
+            if (k == 0 || (t & 15u) == 0u) {
+                const uint4 o = philox4x32_10(p.policy_seed, p.gid_base + (uint64_t)ai, ((t >> 2) & ~3ull) + (uint64_t)j);
+                const uint32_t mine = __umulhi(o.x, 6u) | (__umulhi(o.y, 6u) << 8) | (__umulhi(o.z, 6u) << 16) |
+                                      (__umulhi(o.w, 6u) << 24);
+                a16[0] = group_bcast<0>(mine);
+                a16[1] = group_bcast<1>(mine);
+                a16[2] = group_bcast<2>(mine);
+                a16[3] = group_bcast<3>(mine);
+            }
+            const uint32_t sel = (uint32_t)(t >> 2) & 3u;
+            const uint32_t w4 = sel == 0u ? a16[0] : sel == 1u ? a16[1] : sel == 2u ? a16[2] : a16[3];
+            a = (int)((w4 >> (8u * (uint32_t)(t & 3u))) & 0xffu);
+        }
+        if (p.actions_out && j == 0 && live) p.actions_out[(size_t)k * p.N + i] = a;
+
+        // step (:109-150), the same on the agent's 8 lanes
+        g.step_count += 1;
+        const bool trunc = g.step_count >= R.total_free;             // :111, max_steps = total_free (:409)
+        const int d = a < 4 ? rel_dir(a, g.facing) : (a == 4 ? 4 : 5);
+        if (a < 4) g.facing = facing_of(d);                          // :164-171
+        const bool moved = (ray_e8(w.rec, d) & 0x7fu) >= 1u;
+        bool explored = false;
+        if (moved) {                                                  // _mark_visited (:273-298)
+            const int nx = g.x + (d == 0 ? 1 : d == 1 ? -1 : 0);
+            const int ny = g.y + (d == 2 ? 1 : d == 3 ? -1 : 0);
+            const int nz = g.z + (d == 4 ? 1 : d == 5 ? -1 : 0);
+            const int ax = d >> 1;
+            const bool seen = ax == 0 ? ((w.wx >> nx) & 1ull) : ax == 1 ? ((w.wy >> ny) & 1ull) : ((w.wz >> nz) & 1u);
+            g.x = nx;
+            g.y = ny;
+            g.z = nz;
+            sb_move_rows(p, pl, g, R, w, ax);
+            // a Q cell (internal_grid 2) is entered without counting, but it
+            // is a sensing position all the same, so S is set
+            const bool q = (g.move_mask & 1u) && ((qz_load(pl.qz + nx * p.pd + ny) >> nz) & 1u);
+            if (!seen) {
+                w.wx |= 1ull << nx;
+                w.wy |= 1ull << ny;
+                w.wz |= 1u << nz;
+                if (live && j == 0) pl.sx[ny * p.ph + nz] = w.wx;
+                if (live && j == 1) pl.sy[nx * p.ph + nz] = w.wy;
+                if (live && j == 2) pl.sz[nx * p.pd + ny] = w.wz;
+                if (!q) {
+                    g.visited += 1;
+                    explored = true;
+                }
+            }
+        }
+        g.last_action = a;                                            // :137
+        sg_observe<LMAX>(p, pl, g, w, row, live ? j : 2 * SG);        // :139
+        if (!moved) g.bumps += 1;
+        const int gx = goal & 0xff, gy = (goal >> 8) & 0xff, gz = (goal >> 16) & 0xff;
+        if (g.x == gx && g.y == gy && g.z >= gz && g.z - gz < 5) g.done = true;   // SPOT_GOAL_HEIGTH = 5 (:201-206)
+        const bool term = g.done;
+        const uint32_t ev = (moved ? 1u : 0u) | ((a != 2 && a < 4) ? 2u : 0u) | (term ? 4u : 0u) | (trunc ? 8u : 0u) |
+                            (explored ? 16u : 0u);
+        ev4 |= ev << (8u * ((uint32_t)t & 3u));
+        if (p.reward64 && j == 0 && live) p.reward64[(size_t)k * p.N + i] = simple_reward(ev);
+        const bool need = live && p.autoreset && (term || trunc);
+        if (need && p.terminal_obs) {                                 // the terminal row before the reset
+            __builtin_amdgcn_wave_barrier();
+            float *to = p.terminal_obs + ((size_t)k * p.N + i) * OD;
+            for (int q = j; q < OD; q += SG) to[q] = row[q];
+        }
+        // SB3 VecEnv auto-reset
+        if (!(VN_ABLATE & 512u) && __ballot(need)) {
+            __builtin_amdgcn_wave_barrier();
+            sg_reset_wave<LMAX>(p, pl, need, next_seed, g, goal, R, w, row, lane, j, wave_a0);
+            if (need) next_seed += p.seed_stride;
+        }
+        __builtin_amdgcn_wave_barrier();
+        float *dst = p.obs + ((size_t)k * p.N + wave_a0) * OD;
+        const int nf = rows * OD;
+        if (!(nf & 3) && !(reinterpret_cast<uintptr_t>(dst) & 15u)) {
+            const float4 *s4 = reinterpret_cast<const float4 *>(stage);
+            float4 *d4 = reinterpret_cast<float4 *>(dst);
+            for (int q = lane; q < (nf >> 2); q += 64) obs_store(d4 + q, s4[q]);
+        } else {
+            for (int q = lane; q < nf; q += 64) __builtin_nontemporal_store(stage[q], dst + q);
+        }
+        __builtin_amdgcn_wave_barrier();
+        // the 4-step block's rewards / flags, lane j for slot j
+        if ((t & 3u) == 3u || k + 1 == p.K) {
+            const int s0 = (int)((p.t0 + (uint64_t)kb) & 3u);
+            if (live && j >= s0 && j <= (int)(t & 3u)) {
+                const uint32_t e = (ev4 >> (8 * j)) & 0xffu;
+                const size_t o = (size_t)(kb + j - s0) * p.N + i;
+                if (p.reward) p.reward[o] = (float)simple_reward(e);
+                if (p.term) p.term[o] = (uint8_t)((e >> 2) & 1u);
+                if (p.trunc) p.trunc[o] = (uint8_t)((e >> 3) & 1u);
+            }
+            ev4 = 0;
+            kb = k + 1;
+        }
+    }
+    if (live && j == 0) {
+        p.hot[i] = pack(g);
+        p.goal[i] = goal;
+        p.next_seed[i] = next_seed;
+    }
+    (void)L;
+}
+
 // internal_grid value of one cell from S, Q and the walls (see the layout
 // note above the bit-plane kernel)
 __device__ int8_t sb_belief_cell(const Params &p, int i, const Room &R, int x, int y, int z) {
@@ -2575,7 +3099,8 @@ struct VnEnv {
     uint32_t ablate = 0;
     int variant = 0, obs_dim = VN_OBS_DIM;
     int sbits = 0;
-    int sb_split = 1;  // simpleEnv step with a store wave (simple_split_kernel)
+    int sb_group = 0;  // simpleEnv step with 4 lanes per agent (simple_group_kernel; measured slower, A/B knob)
+    int sb_split = 1;  // else: with a store wave (simple_split_kernel)
     int sb_aw = 32;   // measured: 32 agents per wave 5.62 vs 64 5.43 G env-steps/s (16: 4.97)
     uint32_t sy_off = 0, sz_off = 0, qz_off = 0;
     int pcache = 0;    // CubicEnv plane-set mode (PH 8, rooms <= 64 x 64): see pset_fill
@@ -2680,6 +3205,21 @@ template <bool RESET_ONLY>
 int launch_env(VnEnv *e, const Params &p, hipStream_t s) {
     if (e->variant == VN_VARIANT_SIMPLE) {
         const int L = e->cfg.local_map_length;
+        if (!RESET_ONLY && e->sbits && e->sb_group) {
+            // 8 lanes per agent (simple_group_kernel)
+            const size_t lds = (size_t)4 * SG_APW * e->obs_dim * sizeof(float);
+            const dim3 grid((unsigned)(((size_t)e->N * SG + 255) / 256));
+            if (L <= 4)
+                hipLaunchKernelGGL((simple_group_kernel<4>), grid, dim3(256), lds, s, p);
+            else if (L <= 8)
+                hipLaunchKernelGGL((simple_group_kernel<8>), grid, dim3(256), lds, s, p);
+            else if (L <= 10)
+                hipLaunchKernelGGL((simple_group_kernel<10>), grid, dim3(256), lds, s, p);
+            else
+                hipLaunchKernelGGL((simple_group_kernel<16>), grid, dim3(256), lds, s, p);
+            VN_HIP(hipGetLastError());
+            return VN_OK;
+        }
         if (!RESET_ONLY && e->sbits && e->sb_split) {
             // stepping wave + store wave per 64 agents (simple_split_kernel)
             const size_t lds = (size_t)2 * 64 * e->obs_dim * sizeof(float) + 2 * 64 * 8;
@@ -2725,7 +3265,9 @@ std::string kernel_label(const VnEnv *e, bool reset_only, bool ext, bool fast, i
     if (e->variant == VN_VARIANT_SIMPLE) {
         const int L = e->cfg.local_map_length;
         const int lmax = L <= 4 ? 4 : L <= 8 ? 8 : L <= 10 ? 10 : 16;
-        if (!reset_only && e->sbits && e->sb_split)
+        if (!reset_only && e->sbits && e->sb_group)
+            std::snprintf(buf, sizeof(buf), "simple_group_kernel<%d>", lmax);
+        else if (!reset_only && e->sbits && e->sb_split)
             std::snprintf(buf, sizeof(buf), "simple_split_kernel<%d>", lmax);
         else if (e->sbits)
             std::snprintf(buf, sizeof(buf), "simple_bits_kernel<%s, %d>", reset_only ? "true" : "false", lmax);
@@ -2896,6 +3438,7 @@ int vn_create(const VnRoomSet *rooms, int32_t n_agents, const VnConfig *cfg, int
         // bit planes: SX u64 [pd][ph], SY u64 [pw][ph], SZ u32 [pw][pd], QZ u32 [pw][pd]
         e->sbits = 1;
         if (const char *sp = getenv("VOXNAV_SIMPLE_SPLIT")) e->sb_split = sp[0] == '1';   // A/B knob
+        if (const char *sg = getenv("VOXNAV_SIMPLE_GROUP")) e->sb_group = sg[0] == '1';   // A/B knob
         if (const char *aw = getenv("VOXNAV_SIMPLE_AW")) {   // agents per wave (A/B knob)
             const int v = atoi(aw);
             if (v == 16 || v == 32 || v == 64) e->sb_aw = v;
@@ -3137,6 +3680,16 @@ int vn_export_belief(VnEnv *env, int8_t *belief_out, void *stream) {
     return VN_OK;
 }
 
+#if VN_ENV_PROF
+int vn_debug_env_prof(unsigned long long *out16, int clear) {
+    VN_HIP(hipMemcpyFromSymbol(out16, HIP_SYMBOL(g_env_prof), sizeof(unsigned long long) * 16));
+    if (clear) {
+        unsigned long long z[16] = {0};
+        VN_HIP(hipMemcpyToSymbol(HIP_SYMBOL(g_env_prof), z, sizeof(z)));
+    }
+    return 0;
+}
+#endif
 #if VN_SIMPLE_PROF
 int vn_debug_simple_prof(unsigned long long *out16, int clear) {
     VN_HIP(hipMemcpyFromSymbol(out16, HIP_SYMBOL(g_simple_prof), sizeof(unsigned long long) * 16));

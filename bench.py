@@ -15,6 +15,9 @@ One "step" = one batched env step of all agents on the GPU.  The headline
 resets a fresh env, runs exactly ``--warmup`` untimed steps, then times
 exactly ``--steps`` steps (launches of ``--fuse`` F steps into a [F, N, 80]
 rollout-chunk buffer; the last launch of each phase takes the remainder).
+F = 64 by default: a 64-step rollout chunk per launch (the reference's
+rollouts are n_steps = 2048 per env, train/Grid_Train.py:84); the same
+window at F = 16 is reported beside it (``same_window_other_fuse``).
 ``roofline`` is computed from the same timed launches (HIP events on the
 launch stream) and ``traffic`` from the PMC record of the same window
 (profiles/pmc_traffic.json, keyed by room/L/N/F/warmup/steps).  When the
@@ -62,7 +65,10 @@ def parse(argv=None):
     ap.add_argument("--agents", type=int, default=65536, help="agents per GPU")
     ap.add_argument("--room", default="32x32x8", help="WxDxH of the walled-box room")
     ap.add_argument("--L", type=int, default=10, help="local_map_length")
-    ap.add_argument("--fuse", type=int, default=16, help="env steps per kernel launch (headline)")
+    ap.add_argument("--fuse", type=int, default=64,
+                    help="env steps per kernel launch (headline): one launch fills a [F, N, 80] rollout chunk")
+    ap.add_argument("--fuse-check", type=int, default=16,
+                    help="also time the same window at this many steps per launch (0 = skip)")
     ap.add_argument("--episode-window", type=int, default=1,
                     help="when --steps < one episode, also time one whole episode (5,408 steps)")
     ap.add_argument("--single-step-check", type=int, default=1,
@@ -553,6 +559,19 @@ def main():
                    "roofline": roofline_block(bstep, N, F, EPISODE_WINDOW, e_timed, e_km,
                                               traffic_for(W, D, H, args.L, N, F, 32, EPISODE_WINDOW), label)}
 
+    fuse_alt = None
+    if args.fuse_check and args.fuse_check != F:
+        Fc = args.fuse_check
+        env = make_env()
+        c_el, c_km, c_timed, _ = time_window(torch, dist, dev, world, env, N, Fc, args.warmup, args.steps)
+        fuse_alt = {"value": round(N * world * args.steps / c_el, 1), "steps_per_launch": Fc,
+                    "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(c_el * 1e3 / args.steps, 5),
+                    "roofline": roofline_block(bstep, N, Fc, args.steps, c_timed, c_km,
+                                               traffic_for(W, D, H, args.L, N, Fc, args.warmup, args.steps),
+                                               env.kernel_label(Fc))}
+        env.close()
+        del env
+
     single = None
     if args.single_step_check and F != 1:
         env = make_env()
@@ -606,6 +625,8 @@ def main():
         }
         if episode is not None:
             rec["episode_window"] = episode
+        if fuse_alt is not None:
+            rec["same_window_other_fuse"] = fuse_alt   # the same steps in launches of --fuse-check steps
         if single is not None:
             rec["drop_in_single_step"] = single   # vn_step-shaped call: one env step per launch
         if simple is not None:

@@ -45,20 +45,22 @@ def main():
     outs = {}
     for c in cfgs:
         n, F = int(c[0]), int(c[3])
-        outs[tuple(c)] = Rollout(torch.empty((F, n, 80), device="cuda:0"), torch.empty((F, n), device="cuda:0"),
+        od = 80 if len(c) < 5 or c[4] == "cubic" else 6 * int(c[2]) + 7
+        outs[tuple(c)] = Rollout(torch.empty((F, n, od), device="cuda:0"), torch.empty((F, n), device="cuda:0"),
                                  torch.empty((F, n), dtype=torch.uint8, device="cuda:0"),
                                  torch.empty((F, n), dtype=torch.uint8, device="cuda:0"), None)
     res = {(name, tuple(c)): [] for name in libs for c in cfgs}
     for r in range(a.rounds):
         for c in cfgs:
             n, room, L, F = int(c[0]), c[1], int(c[2]), int(c[3])
+            variant = c[4] if len(c) > 4 else "cubic"      # config field 5: cubic | simple
             rs = load_archive_set(room) if room.startswith("P") else single_room_set(box_room(*map(int, room.split("x"))))
             names = list(libs) if r % 2 == 0 else list(libs)[::-1]
             for name in names:
                 saved = {k: os.environ.get(k) for k in envs[name]}
                 os.environ.update(envs[name])
                 e = BatchedGridEnv(num_agents=n, rooms=rs, local_map_length=L, autoreset=True, device="cuda:0",
-                                   lib=libs[name])
+                                   lib=libs[name], variant=variant)
                 for k, old in saved.items():
                     if old is None:
                         os.environ.pop(k, None)

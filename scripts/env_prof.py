@@ -1,0 +1,53 @@
+#!/usr/bin/env python3
+"""Per-section shader-clock profile of the CubicEnv step loop (diagnostics
+build with -DVN_ENV_PROF=1, scripts/build_variants.py eprof:VN_ENV_PROF=1):
+cycles per wave per step in each section, over a bench-shaped window."""
+import argparse
+import ctypes
+import sys
+import time
+from pathlib import Path
+
+REPO = Path(__file__).resolve().parent.parent
+sys.path.insert(0, str(REPO / "3d-navigation-reinforcement-learning_amd"))
+import torch  # noqa: E402
+
+from voxnav import _native  # noqa: E402
+from voxnav.env import BatchedGridEnv, Rollout  # noqa: E402
+from voxnav.rooms import box_room, single_room_set, load_archive_set  # noqa: E402
+
+ap = argparse.ArgumentParser()
+ap.add_argument("--lib", default="3d-navigation-reinforcement-learning_amd/voxnav/_lib/variants/libvoxnav_eprof.so")
+ap.add_argument("--N", type=int, default=65536)
+ap.add_argument("--room", default="32x32x8")
+ap.add_argument("--F", type=int, default=16)
+ap.add_argument("--steps", type=int, default=5408)
+a = ap.parse_args()
+lib = _native.load_variant(REPO / a.lib)
+raw = lib.raw if hasattr(lib, "raw") else lib
+rs = load_archive_set(a.room) if a.room.startswith("P") else single_room_set(box_room(*map(int, a.room.split("x"))))
+e = BatchedGridEnv(num_agents=a.N, rooms=rs, local_map_length=10, autoreset=True, device="cuda:0", lib=lib)
+e.reset(seed=42)
+F = a.F
+o = Rollout(torch.empty((F, a.N, 80), device="cuda:0"), torch.empty((F, a.N), device="cuda:0"),
+            torch.empty((F, a.N), dtype=torch.uint8, device="cuda:0"),
+            torch.empty((F, a.N), dtype=torch.uint8, device="cuda:0"), None)
+e.step_random(F, out=o)
+torch.cuda.synchronize()
+prof = (ctypes.c_ulonglong * 16)()
+fn = getattr(raw, "vn_debug_env_prof", None) or getattr(raw, "_lib").vn_debug_env_prof
+fn(prof, 1)
+n = a.steps // F
+t0 = time.perf_counter()
+for _ in range(n):
+    e.step_random(F, out=o)
+torch.cuda.synchronize()
+el = time.perf_counter() - t0
+fn(prof, 1)
+waves = max(1, prof[8])
+names = ["move+issue", "shift-commit", "sense+stage", "reward-ev", "reset", "obs-flush", "reward-store"]
+tot = sum(prof[k] for k in range(7))
+print(f"{a.room} F={F}: {a.N * n * F / el / 1e9:.3f} G env-steps/s (instrumented); per wave-step cycles:")
+for k, nm in enumerate(names):
+    print(f"  {nm:13s} {prof[k] / waves / F:9.1f}  ({100 * prof[k] / max(1, tot):5.1f} %)")
+print(f"  loop total    {prof[7] / waves / F:9.1f}; waves x launches = {waves}")
