@@ -136,6 +136,7 @@ struct Params {
     // simpleEnv variant
     int variant, obs_dim, pd;
     uint32_t *goal;          // per agent gx | gy<<8 | gz<<16
+    uint4 *predraw;          // simpleEnv: per agent a reset draw computed ahead {start|room<<24, goal, seed, valid}
     int sbits;               // simpleEnv bit-plane layout (rooms up to 64 x 64 x 31)
     int sb_aw;               // bit-plane kernel: agents per 64-lane wave (16, 32 or 64)
     uint32_t sy_off, sz_off, qz_off;
@@ -1944,6 +1945,8 @@ __device__ __forceinline__ int facing_of(int d) { return (int)((0x8Du >> (2 * d)
 // (start | room<<24, goal).
 template <bool INL>
 __device__ __attribute__((always_inline)) inline uint2 simple_draw_t(const EnvConst *ec, uint32_t seed);
+template <typename MT>
+__device__ __attribute__((always_inline)) inline uint2 simple_draw_from(const EnvConst *ec, MT &mt);
 __device__ __noinline__ uint2 simple_draw(const EnvConst *ec, uint32_t seed) { return simple_draw_t<false>(ec, seed); }
 template <bool INL>
 __device__ __attribute__((always_inline)) inline uint2 simple_draw_t(const EnvConst *ec, uint32_t seed) {
@@ -1958,6 +1961,77 @@ __device__ __attribute__((always_inline)) inline uint2 simple_draw_t(const EnvCo
     } else {
         mt_first_outputs(seed, mt.buf);
     }
+    return simple_draw_from(ec, mt);
+}
+
+// The first MT_W = 24 outputs of random.seed(seed) in ONE pass of the two
+// init_by_array chains (mt_outputs captures 8 per pass; a wave-wide draw of
+// 64 lanes would otherwise re-run the chains whenever any lane's rejection
+// sampling passed 8 outputs), written to the lane's LDS row (stride MT_WS).
+constexpr int MT_W = 24, MT_WS = 25;
+__device__ __noinline__ void mt_outputs_wide(uint32_t seed, uint32_t *lds_row) {
+    uint32_t p = mix1(c_mt_g[1], c_mt_g[0], seed);
+    const uint32_t m1_1 = p;
+    p = mt_loop1(p, seed);
+    const uint32_t m1b1 = mix1(m1_1, p, seed);   // wrap: i = 1 again, mt[0] = mt[623]
+    uint32_t p1 = m1_1, q = m1b1;
+    uint32_t lo[MT_W + 1], hi[MT_W];             // F[0 .. MT_W], F[397 .. 397 + MT_W - 1]
+#pragma unroll
+    for (int i = 2; i <= MT_W; ++i) {
+        p1 = mix1(c_mt_g[i], p1, seed);
+        q = mix2(p1, q, (uint32_t)i);
+        lo[i] = q;
+    }
+    mt_loop2(p1, q, MT_W + 1, 397, seed);
+#pragma unroll
+    for (int k = 0; k < MT_W; ++k) {
+        const int i = 397 + k;
+        p1 = mix1(c_mt_g[i], p1, seed);
+        q = mix2(p1, q, (uint32_t)i);
+        hi[k] = q;
+    }
+    mt_loop2(p1, q, 397 + MT_W, MT_N, seed);
+    lo[1] = mix2(m1b1, q, 1u);                   // F[1]: loop 2's wrap step
+    lo[0] = 0x80000000u;                         // F[0]
+#pragma unroll
+    for (int j = 0; j < MT_W; ++j) {
+        const uint32_t y = (lo[j] & 0x80000000u) | (lo[j + 1] & 0x7fffffffu);
+        lds_row[j] = mt_temper(hi[j] ^ (y >> 1) ^ ((y & 1u) ? 0x9908b0dfu : 0u));
+    }
+}
+
+// MT output stream over a lane's LDS row of MT_W outputs (mt_outputs_wide),
+// blocks past it recomputed one at a time (mt_refill)
+struct MtLdsStream {
+    const uint32_t *row;
+    uint32_t seed;
+    int used;
+    int32_t *err;
+    MtBlock ext;
+    __device__ uint32_t next() {
+        uint32_t r;
+        if (used < MT_W) {
+            r = row[used];
+        } else {
+            if ((used % MT_C) == 0) ext = mt_refill(seed, used, err);
+            const int j = used % MT_C;
+            r = ext.w[0];
+#pragma unroll
+            for (int t = 1; t < MT_C; ++t) r = j == t ? ext.w[t] : r;
+        }
+        ++used;
+        return r;
+    }
+    __device__ uint32_t below(uint32_t n) {
+        const int k = 32 - __clz(n);
+        uint32_t r = next() >> (32 - k);
+        while (r >= n) r = next() >> (32 - k);
+        return r;
+    }
+};
+
+template <typename MT>
+__device__ __attribute__((always_inline)) inline uint2 simple_draw_from(const EnvConst *ec, MT &mt) {
     const int room = ec->use_room_draw ? (int)mt.below((uint32_t)ec->n_rooms) : 0;
     const Room R = load_room_c(ec, room);
     auto is_wall = [&](uint32_t c) {
@@ -2379,6 +2453,12 @@ __global__ __launch_bounds__(64) void simple_bits_kernel(Params p) {
             p.goal[ai] = goal;
             p.next_seed[ai] = seed + p.seed_stride;   // modulo 2^32
         }
+        // the next episode's draw ahead (simple_pipe_kernel's sp_reset_wave)
+        if (__ballot(need)) {
+            const uint32_t s2 = seed + p.seed_stride;
+            const uint2 d = need ? simple_draw(p.envc, s2) : make_uint2(0u, 0u);
+            if (need) p.predraw[ai] = make_uint4(d.x, d.y, s2, 1u);
+        }
         return;
     }
     if (live) sb_load_rows(p, pl, g, R, w);
@@ -2528,6 +2608,24 @@ __global__ __launch_bounds__(64) void simple_bits_kernel(Params p) {
 // barrier after which wave 0 overwrites that buffer (step k+2).
 // LDS: stage[2][64][OD] f32, reward[2][64] f32, flags[2][64] u32.
 // ----------------------------------------------------------------------------
+// Block barrier that orders only LDS: lgkmcnt(0) then s_barrier.  The store
+// wave's HBM stores stay in flight across it (a __syncthreads() would wait
+// vmcnt(0), i.e. for every store of the step to complete, before the
+// stepping wave may go on).
+#ifndef VN_LDS_BARRIER
+#define VN_LDS_BARRIER 1
+#endif
+__device__ __forceinline__ void lds_handoff() {
+#if VN_LDS_BARRIER
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_s_waitcnt(0xC07F);          // lgkmcnt(0) alone
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+#else
+    lds_handoff();
+#endif
+}
+
 template <int LMAX>
 __global__ __launch_bounds__(128) void simple_split_kernel(Params p) {
     extern __shared__ float sm[];
@@ -2541,7 +2639,7 @@ __global__ __launch_bounds__(128) void simple_split_kernel(Params p) {
 
     if (threadIdx.x >= 64) {                     // ---- store wave ----
         for (int k = 0; k < p.K; ++k) {
-            __syncthreads();                     // step k staged in buffer k & 1
+            lds_handoff();                     // step k staged in buffer k & 1
             const int b = k & 1;
             const float *st = stage + b * 64 * OD;
             float *dst = p.obs + ((size_t)k * p.N + a0) * OD;
@@ -2662,13 +2760,296 @@ __global__ __launch_bounds__(128) void simple_split_kernel(Params p) {
             sb_reset_wave<LMAX>(p, pl, need, next_seed, g, goal, R, w, row, lane, a0);
             if (need) next_seed += p.seed_stride;
         }
-        __syncthreads();                         // hand buffer b to the store wave
+        lds_handoff();                         // hand buffer b to the store wave
     }
     if (live) {
         p.hot[ai] = pack(g);
         p.goal[ai] = goal;
         p.next_seed[ai] = next_seed;
     }
+}
+
+// ----------------------------------------------------------------------------
+// The bit-plane step with a store wave, software-pipelined by one step
+// (the default simpleEnv kernel for rooms <= 64 x 64 x 31).  A step's move
+// needs only the ray record of the agent's cell, which the previous step
+// loaded, so the move of step k+1 is computed -- and the loads at its target
+// cell (ray record, the two S words not along the move axis) issued --
+// BEFORE step k's observation is built.  Those loads then land while step k
+// observes; one stepping wave per SIMD no longer waits a full load round trip
+// per step.  The pending move (action, direction, facing, target) is committed
+// at the start of the next iteration (visit / S marks in the reference's
+// order, :109-150); an auto-reset recomputes it from the start cell.  The
+// stepping wave issues no output stores (the store wave does), so waiting for
+// its loads never waits for obs stores.
+// ----------------------------------------------------------------------------
+// reset of the lanes with `need` for simple_pipe_kernel: as sb_reset_wave,
+// but the MT19937 draw (a ~1.2k-step serial chain, ~15 us) is shared.  A
+// lane's draw for its next episode seed is kept in nd = {start | room << 24,
+// goal, seed, valid}.  A resetting lane whose nd is for its seed uses it; when
+// any resetting lane has none, the wave runs the chain once for EVERY live
+// lane (same instructions, so the same time as for one lane): the resetting
+// lanes take their draw and the others keep theirs for their next reset.
+// Measured: the chain was half of the kernel's time (resets ablated: 2x).
+template <int LMAX>
+__device__ __forceinline__ void sp_reset_wave(const Params &p, const SPlanes &pl, bool need, bool live, uint32_t seed,
+                                              Agent &g, uint32_t &goal, Room &R, SRows &w, float *row, int lane,
+                                              int block_agent0, uint4 &nd, uint32_t *mt_lds) {
+    const bool have = need && nd.w == 1u && nd.z == seed;
+    uint2 drawn = have ? make_uint2(nd.x, nd.y) : make_uint2(0u, 0u);
+    if (need) nd.w = 0u;                                   // consumed: the next episode has another seed
+    if (__ballot(need && !have)) {
+        // one chain pass for the wave: a resetting lane without a draw computes
+        // this episode's; one with a draw the episode after it (seed + stride);
+        // the others their next episode's if they have none
+        const uint32_t s2 = (need && have) ? seed + p.seed_stride : seed;
+        mt_outputs_wide(s2, mt_lds + lane * MT_WS);
+        MtLdsStream mt;
+        mt.row = mt_lds + lane * MT_WS;
+        mt.seed = s2;
+        mt.used = 0;
+        mt.err = p.envc->err;
+        const uint2 d2 = live ? simple_draw_from(p.envc, mt) : make_uint2(0u, 0u);
+        if (need && !have) drawn = d2;
+        else if (live) nd = make_uint4(d2.x, d2.y, s2, 1u);
+    }
+    uint64_t m = __ballot(need);
+    const uint32_t n16 = p.agent_bytes >> 4;
+    while (m) {
+        const int src = __ffsll((unsigned long long)m) - 1;
+        m &= m - 1;
+        uint4 *base = reinterpret_cast<uint4 *>(p.belief + (size_t)(block_agent0 + src) * p.agent_bytes);
+        for (uint32_t q = (uint32_t)lane; q < n16; q += 64u) base[q] = make_uint4(0u, 0u, 0u, 0u);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+    if (need) {
+        g.room = (int)(drawn.x >> 24);
+        R = load_room(p, g.room);
+        g.x = drawn.x & 0xff;
+        g.y = (drawn.x >> 8) & 0xff;
+        g.z = (drawn.x >> 16) & 0xff;
+        goal = drawn.y;
+        g.facing = 0;
+        g.last_action = 0;
+        g.done = g.last_bump = g.near_wall = g.was_near_wall = false;
+        g.step_count = 0;
+        g.visited = 1;
+        g.bumps = 0;
+        g.cid = 0;
+        g.move_mask = 0;
+        w.wx = 1ull << g.x;                                                     // :86
+        w.wy = 1ull << g.y;
+        w.wz = 1u << g.z;
+        pl.sx[g.y * p.ph + g.z] = w.wx;
+        pl.sy[g.x * p.ph + g.z] = w.wy;
+        pl.sz[g.x * p.pd + g.y] = w.wz;
+        w.rec = p.rays[R.ray_off + (uint32_t)((g.x * R.D + g.y) * R.H + g.z)];
+        sb_observe<LMAX>(p, pl, g, w, row);
+    }
+}
+
+struct SPend {
+    int a, d, facing, nx, ny, nz;
+    bool moved;
+};
+
+template <int LMAX>
+__global__ __launch_bounds__(128) void simple_pipe_kernel(Params p) {
+    extern __shared__ float sm[];
+    const int OD = p.obs_dim, L = p.L;
+    float *stage = sm;
+    float *srew = sm + 2 * 64 * OD;
+    uint32_t *sflg = reinterpret_cast<uint32_t *>(srew + 2 * 64);
+    const int lane = threadIdx.x & 63;
+    const int a0 = blockIdx.x * 64;
+    const int rows = min(64, p.N - a0);
+
+    if (threadIdx.x >= 64) {                     // ---- store wave (as simple_split_kernel) ----
+        for (int k = 0; k < p.K; ++k) {
+            lds_handoff();                     // step k staged in buffer k & 1
+            const int b = k & 1;
+            const float *st = stage + b * 64 * OD;
+            float *dst = p.obs + ((size_t)k * p.N + a0) * OD;
+            if (!((rows * OD) & 3) && !(reinterpret_cast<uintptr_t>(dst) & 15u)) {
+                const float4 *s4 = reinterpret_cast<const float4 *>(st);
+                float4 *d4 = reinterpret_cast<float4 *>(dst);
+                for (int q = lane; q < (rows * OD) >> 2; q += 64) obs_store(d4 + q, s4[q]);
+            } else {
+                for (int q = lane; q < rows * OD; q += 64) __builtin_nontemporal_store(st[q], dst + q);
+            }
+            if (lane < rows) {
+                const size_t o = (size_t)k * p.N + a0 + lane;
+                const uint32_t f = sflg[b * 64 + lane];
+                if (p.reward) p.reward[o] = srew[b * 64 + lane];
+                if (p.term) p.term[o] = (uint8_t)(f & 1u);
+                if (p.trunc) p.trunc[o] = (uint8_t)(f >> 1);
+            }
+        }
+        return;
+    }
+
+    // ---- stepping wave ----
+    const int ai = a0 + lane;
+    const bool live = ai < p.N;
+    const SPlanes pl = splanes(p, live ? ai : a0);
+    Agent g = unpack(live ? p.hot[ai] : make_uint4(0u, 0u, 0u, 0u));
+    uint32_t goal = live ? p.goal[ai] : 0u;
+    uint32_t next_seed = live ? p.next_seed[ai] : 0u;
+    uint4 nd = live ? p.predraw[ai] : make_uint4(0u, 0u, 0u, 0u);   // draw ahead (sp_reset_wave)
+    Room R = load_room(p, g.room);
+    SRows w;                                     // S words + ray record at the agent's (committed) cell
+    w.wx = w.wy = 0;
+    w.wz = 0;
+    w.rec = make_uint2(0u, 0u);
+    if (live) sb_load_rows(p, pl, g, R, w);
+
+    uint4 r4 = make_uint4(0u, 0u, 0u, 0u);      // Philox block r4blk (4 steps)
+    uint64_t r4blk = ~0ull;
+    SPend pm;                                    // the pending move
+    SRows wn;                                    // ... and the rows at its target (in flight)
+    uint64_t cbx = 0ull, cby = 0ull;             // S bits its commit adds to wn's kept rows
+    uint32_t cbz = 0u;
+    // the move of launch step k from the committed state; issues the target's loads
+    auto premove = [&](int k) {
+        const uint64_t t = p.t0 + (uint64_t)k;
+        int a;
+        if (p.actions) {
+            a = p.actions[(size_t)k * p.N + (live ? ai : a0)];
+        } else {
+            if ((t >> 2) != r4blk) {
+                r4blk = t >> 2;
+                r4 = philox4x32_10(p.policy_seed, p.gid_base + (uint64_t)(live ? ai : a0), t >> 2);
+            }
+            const uint32_t word = (t & 3) == 0 ? r4.x : (t & 3) == 1 ? r4.y : (t & 3) == 2 ? r4.z : r4.w;
+            a = (int)(((uint64_t)word * 6u) >> 32);
+        }
+        const int d = a < 4 ? rel_dir(a, g.facing) : (a == 4 ? 4 : 5);
+        pm.a = a;
+        pm.d = d;
+        pm.facing = a < 4 ? facing_of(d) : g.facing;                 // :164-171
+        pm.moved = (ray_e8(w.rec, d) & 0x7fu) >= 1u;
+        pm.nx = g.x + (pm.moved ? (d == 0 ? 1 : d == 1 ? -1 : 0) : 0);
+        pm.ny = g.y + (pm.moved ? (d == 2 ? 1 : d == 3 ? -1 : 0) : 0);
+        pm.nz = g.z + (pm.moved ? (d == 4 ? 1 : d == 5 ? -1 : 0) : 0);
+        wn = w;
+        if (pm.moved) {
+            // the S word along the move axis is the same row (kept); the other two
+            // rows and the ray record are the target's.  These rows never hold
+            // the bit the commit of this move sets (they are off the current cell).
+            const int ax = d >> 1;
+            if (ax != 0) wn.wx = pl.sx[pm.ny * p.ph + pm.nz];
+            if (ax != 1) wn.wy = pl.sy[pm.nx * p.ph + pm.nz];
+            if (ax != 2) wn.wz = pl.sz[pm.nx * p.pd + pm.ny];
+            wn.rec = p.rays[R.ray_off + (uint32_t)((pm.nx * R.D + pm.ny) * R.H + pm.nz)];
+        }
+    };
+    if (live && p.K > 0) premove(0);
+
+    for (int k = 0; k < p.K; ++k) {
+        const int b = k & 1;
+        float *row = stage + b * 64 * OD + lane * OD;
+        bool trunc = false, term = false;
+        if (live) {
+            // ---- commit step k (:109-150) ----
+            if (p.actions_out) p.actions_out[(size_t)k * p.N + ai] = pm.a;
+            g.step_count += 1;
+            trunc = g.step_count >= R.total_free;                      // :111, max_steps = total_free (:409)
+            g.facing = pm.facing;
+            const int a = pm.a;
+            const bool moved = pm.moved;
+            bool explored = false, seen = true;
+            if (moved) {                                                 // _mark_visited (:273-298)
+                const int ax = pm.d >> 1;
+                // the target's S bit from the cached word of the move axis (kept in wn)
+                seen = ax == 0 ? ((w.wx >> pm.nx) & 1ull) : ax == 1 ? ((w.wy >> pm.ny) & 1ull) : ((w.wz >> pm.nz) & 1u);
+                g.x = pm.nx;
+                g.y = pm.ny;
+                g.z = pm.nz;
+                w = wn;
+            }
+            // the bits of the previous step's mark that this move's rows were
+            // copied without (see below)
+            w.wx |= cbx;
+            w.wy |= cby;
+            w.wz |= cbz;
+            cbx = cby = 0ull;
+            cbz = 0u;
+            g.last_action = a;                                           // :137
+            // ---- the next step's move and its loads, issued before this step's
+            // S-mark stores (a wait for these loads then never waits for them) ----
+            if (k + 1 < p.K) premove(k + 1);
+            if (moved) {
+                // a Q cell (internal_grid 2) is entered without counting, but it
+                // is a sensing position all the same, so S is set
+                const bool q = (g.move_mask & 1u) && ((pl.qz[g.x * p.pd + g.y] >> g.z) & 1u);
+                if (!seen) {
+                    const uint64_t bx = 1ull << g.x, by = 1ull << g.y;
+                    const uint32_t bz = 1u << g.z;
+                    w.wx |= bx;
+                    w.wy |= by;
+                    w.wz |= bz;
+                    // the pending move copied its kept row(s) from w before this
+                    // mark (all three if it does not move): carried into its
+                    // commit (wn itself is the target of loads in flight)
+                    const int nax = pm.moved ? pm.d >> 1 : -1;
+                    if (nax <= 0) cbx = bx;
+                    if (nax == -1 || nax == 1) cby = by;
+                    if (nax == -1 || nax == 2) cbz = bz;
+                    pl.sx[g.y * p.ph + g.z] = w.wx;
+                    pl.sy[g.x * p.ph + g.z] = w.wy;
+                    pl.sz[g.x * p.pd + g.y] = w.wz;
+                    if (!q) {
+                        g.visited += 1;
+                        explored = true;
+                    }
+                }
+            }
+            if (!(VN_ABLATE & 4u)) sb_observe<LMAX>(p, pl, g, w, row);   // :139
+            // compute_reward (:189-217), f64 in the reference's order
+            double r = -0.1;
+            if (!moved) {
+                g.bumps += 1;
+                r += -10.0;
+            }
+            if (a != 2 && a < 4) r += 0.05;
+            const int gx = goal & 0xff, gy = (goal >> 8) & 0xff, gz = (goal >> 16) & 0xff;
+            if (g.x == gx && g.y == gy && g.z >= gz && g.z - gz < 5) {   // SPOT_GOAL_HEIGTH = 5 (:201-206)
+                g.done = true;
+                r += 100.0;
+            }
+            if (trunc) r += 0.0;
+            if (explored) r += 1.0;
+            term = g.done;
+            const size_t o = (size_t)k * p.N + ai;
+            srew[b * 64 + lane] = (float)r;
+            sflg[b * 64 + lane] = (term ? 1u : 0u) | (trunc ? 2u : 0u);
+            if (p.reward64) p.reward64[o] = r;
+            if ((term || trunc) && p.autoreset && p.terminal_obs) {
+                float *to = p.terminal_obs + o * OD;
+                for (int q = 0; q < OD; ++q) to[q] = row[q];
+            }
+        }
+        // SB3 VecEnv auto-reset
+        const bool need = live && p.autoreset && (term || trunc) && !(VN_ABLATE & 512u);
+        if (__ballot(need)) {
+            sp_reset_wave<LMAX>(p, pl, need, live, next_seed, g, goal, R, w, row, lane, a0, nd,
+                                reinterpret_cast<uint32_t *>(sflg + 2 * 64));
+            if (need) {
+                next_seed += p.seed_stride;
+                cbx = cby = 0ull;
+                cbz = 0u;
+                if (k + 1 < p.K) premove(k + 1);                         // from the start cell
+            }
+        }
+        lds_handoff();                         // hand buffer b to the store wave
+    }
+    if (live) {
+        p.hot[ai] = pack(g);
+        p.goal[ai] = goal;
+        p.next_seed[ai] = next_seed;
+        p.predraw[ai] = nd;
+    }
+    (void)L;
 }
 
 // ----------------------------------------------------------------------------
@@ -3096,11 +3477,13 @@ struct VnEnv {
     int32_t *d_err = nullptr;
     EnvConst *d_envc = nullptr;
     uint32_t *d_goal = nullptr;
+    uint4 *d_predraw = nullptr;
     uint32_t ablate = 0;
     int variant = 0, obs_dim = VN_OBS_DIM;
     int sbits = 0;
     int sb_group = 0;  // simpleEnv step with 4 lanes per agent (simple_group_kernel; measured slower, A/B knob)
-    int sb_split = 1;  // else: with a store wave (simple_split_kernel)
+    int sb_split = 1;  // else: with a store wave (simple_split_kernel) ...
+    int sb_pipe = 1;   // ... software-pipelined by one step (simple_pipe_kernel)
     int sb_aw = 32;   // measured: 32 agents per wave 5.62 vs 64 5.43 G env-steps/s (16: 4.97)
     uint32_t sy_off = 0, sz_off = 0, qz_off = 0;
     int pcache = 0;    // CubicEnv plane-set mode (PH 8, rooms <= 64 x 64): see pset_fill
@@ -3170,6 +3553,7 @@ Params base_params(VnEnv *e) {
     p.obs_dim = e->obs_dim;
     p.pd = e->pd;
     p.goal = e->d_goal;
+    p.predraw = e->d_predraw;
     p.sbits = e->sbits;
     p.sb_aw = e->sb_aw;
     p.sy_off = e->sy_off;
@@ -3220,6 +3604,21 @@ int launch_env(VnEnv *e, const Params &p, hipStream_t s) {
             VN_HIP(hipGetLastError());
             return VN_OK;
         }
+        if (!RESET_ONLY && e->sbits && e->sb_split && e->sb_pipe) {
+            // software-pipelined stepping wave + store wave per 64 agents (simple_pipe_kernel)
+            const size_t lds = (size_t)2 * 64 * e->obs_dim * sizeof(float) + 2 * 64 * 8 + 64 * MT_WS * 4;
+            const dim3 grid((unsigned)((e->N + 63) / 64));
+            if (L <= 4)
+                hipLaunchKernelGGL((simple_pipe_kernel<4>), grid, dim3(128), lds, s, p);
+            else if (L <= 8)
+                hipLaunchKernelGGL((simple_pipe_kernel<8>), grid, dim3(128), lds, s, p);
+            else if (L <= 10)
+                hipLaunchKernelGGL((simple_pipe_kernel<10>), grid, dim3(128), lds, s, p);
+            else
+                hipLaunchKernelGGL((simple_pipe_kernel<16>), grid, dim3(128), lds, s, p);
+            VN_HIP(hipGetLastError());
+            return VN_OK;
+        }
         if (!RESET_ONLY && e->sbits && e->sb_split) {
             // stepping wave + store wave per 64 agents (simple_split_kernel)
             const size_t lds = (size_t)2 * 64 * e->obs_dim * sizeof(float) + 2 * 64 * 8;
@@ -3267,6 +3666,8 @@ std::string kernel_label(const VnEnv *e, bool reset_only, bool ext, bool fast, i
         const int lmax = L <= 4 ? 4 : L <= 8 ? 8 : L <= 10 ? 10 : 16;
         if (!reset_only && e->sbits && e->sb_group)
             std::snprintf(buf, sizeof(buf), "simple_group_kernel<%d>", lmax);
+        else if (!reset_only && e->sbits && e->sb_split && e->sb_pipe)
+            std::snprintf(buf, sizeof(buf), "simple_pipe_kernel<%d>", lmax);
         else if (!reset_only && e->sbits && e->sb_split)
             std::snprintf(buf, sizeof(buf), "simple_split_kernel<%d>", lmax);
         else if (e->sbits)
@@ -3295,6 +3696,7 @@ void free_env(VnEnv *e) {
     (void)hipFree(e->d_err);
     (void)hipFree(e->d_envc);
     (void)hipFree(e->d_goal);
+    (void)hipFree(e->d_predraw);
     (void)hipFree(e->d_wimg);
     (void)hipFree(e->d_scratch);
     delete e;
@@ -3439,6 +3841,7 @@ int vn_create(const VnRoomSet *rooms, int32_t n_agents, const VnConfig *cfg, int
         e->sbits = 1;
         if (const char *sp = getenv("VOXNAV_SIMPLE_SPLIT")) e->sb_split = sp[0] == '1';   // A/B knob
         if (const char *sg = getenv("VOXNAV_SIMPLE_GROUP")) e->sb_group = sg[0] == '1';   // A/B knob
+        if (const char *sq = getenv("VOXNAV_SIMPLE_PIPE")) e->sb_pipe = sq[0] == '1';     // A/B knob
         if (const char *aw = getenv("VOXNAV_SIMPLE_AW")) {   // agents per wave (A/B knob)
             const int v = atoi(aw);
             if (v == 16 || v == 32 || v == 64) e->sb_aw = v;
@@ -3523,6 +3926,7 @@ int vn_create(const VnRoomSet *rooms, int32_t n_agents, const VnConfig *cfg, int
     VN_ALLOC(e->d_err, sizeof(int32_t));
     VN_ALLOC(e->d_envc, sizeof(EnvConst));
     VN_ALLOC(e->d_goal, (size_t)n_agents * sizeof(uint32_t));
+    VN_ALLOC(e->d_predraw, (size_t)n_agents * sizeof(uint4));
     if (e->pcache) VN_ALLOC(e->d_wimg, (size_t)nr * e->map_bytes);
     VN_ALLOC(e->d_scratch, 4096);
 #undef VN_ALLOC
@@ -3537,6 +3941,7 @@ int vn_create(const VnRoomSet *rooms, int32_t n_agents, const VnConfig *cfg, int
     // unknown: 0x00 in the CubicEnv byte encoding, -1 (0xFF) in the dense simpleEnv map; empty bit planes
     if (he == hipSuccess) he = hipMemset(e->d_belief, e->variant == VN_VARIANT_SIMPLE && !e->sbits ? 0xFF : 0x00, belief_bytes);
     if (he == hipSuccess) he = hipMemset(e->d_goal, 0, (size_t)n_agents * sizeof(uint32_t));
+    if (he == hipSuccess) he = hipMemset(e->d_predraw, 0, (size_t)n_agents * sizeof(uint4));
     if (he == hipSuccess) he = hipMemset(e->d_err, 0, sizeof(int32_t));
     if (he == hipSuccess && e->pcache) {
         // per room: the bricked byte map of a fresh episode -- 0x40 (latent

@@ -101,6 +101,16 @@ def test_simple_group_kernel_matches_oracle(voxnav, monkeypatch, src, L, N, K):
     _rollout_vs_oracle(src, L, N, K)
 
 
+# the stepping + store wave kernel without the one-step pipeline
+SPLIT_CASES = [("box:8x8x4", 4, 300, 200), ("set:P3_training", 10, 512, 150)]
+
+
+@pytest.mark.parametrize("src,L,N,K", SPLIT_CASES, ids=[f"{c[0]}-L{c[1]}" for c in SPLIT_CASES])
+def test_simple_split_kernel_matches_oracle(voxnav, monkeypatch, src, L, N, K):
+    monkeypatch.setenv("VOXNAV_SIMPLE_PIPE", "0")
+    _rollout_vs_oracle(src, L, N, K)
+
+
 # the one-wave bit-plane kernel; VOXNAV_SIMPLE_AW sets its agents per wave
 ONE_WAVE_CASES = [("box:8x8x4", 4, 300, 200, "32"), ("set:P2_training", 10, 1000, 150, "64"),
                   ("file:P3_training/kitchen2.txt", 16, 200, 150, "16")]
