@@ -8,9 +8,9 @@ set -u
 cd "${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-BARGS="${BENCH_ARGS:-} --single-step-check 0 --collector none --simple 0"
+BARGS="${BENCH_ARGS:-} --single-step-check 0 --collector none --simple 0 --fuse-check 0"
 TAG=${TAG:-r02}
-PASSES=${PASSES:-trace,trace_f1,fetch,write,l2,sq,sqw,tcp}
+PASSES=${PASSES:-trace,simple,simple_fetch,simple_write,trace_f1,fetch,write,l2,sq,sqw,tcp}
 step() {
   local name=$1 t=$2; shift 2
   [[ ",$PASSES," == *",$name,"* ]] || return 0
@@ -20,6 +20,9 @@ step() {
   [ $rc -eq 0 ] || exit $rc
 }
 step trace 400 rocprofv3 --kernel-trace --stats -d gpurun_out/${TAG}_trace -o trace --output-format csv -- python3 bench.py --steps 5408 --warmup 32 --cpu-seconds 0 $BARGS
+step simple 400 rocprofv3 --kernel-trace --stats -d gpurun_out/${TAG}_simple -o trace --output-format csv -- python3 bench.py --steps 5408 --warmup 32 --cpu-seconds 0 --single-step-check 0 --collector none --simple 1 --fuse-check 0 --episode-window 0
+step simple_fetch 400 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/${TAG}_simple_fetch -o fetch --output-format csv -- python3 bench.py --steps 5408 --warmup 32 --cpu-seconds 0 --single-step-check 0 --collector none --simple 1 --fuse-check 0 --episode-window 0
+step simple_write 400 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/${TAG}_simple_write -o write --output-format csv -- python3 bench.py --steps 5408 --warmup 32 --cpu-seconds 0 --single-step-check 0 --collector none --simple 1 --fuse-check 0 --episode-window 0
 step trace_f1 400 rocprofv3 --kernel-trace --stats -d gpurun_out/${TAG}_trace_f1 -o trace --output-format csv -- python3 bench.py --steps 200 --warmup 20 --cpu-seconds 0 $BARGS --fuse 1
 step fetch 400 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/${TAG}_fetch -o fetch --output-format csv -- python3 bench.py --steps 5408 --warmup 32 --cpu-seconds 0 $BARGS
 step write 400 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/${TAG}_write -o write --output-format csv -- python3 bench.py --steps 5408 --warmup 32 --cpu-seconds 0 $BARGS
