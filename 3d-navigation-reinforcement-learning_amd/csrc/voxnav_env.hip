@@ -673,35 +673,39 @@ __device__ __forceinline__ bool mark(Col<PH> &c, int z, const Rays &ry, int r, i
 // one set (written back if dirty, like a tile column), so a ray mark costs an
 // LDS word instead of an HBM row write plus one blind byte store per new cell.
 // ----------------------------------------------------------------------------
-// RT, the LDS row word: uint32_t when every room of the set is at most
-// 32 x 32 (half the LDS, so 16 waves fit a CU), else uint64_t.  The HBM
-// rows stay u64 either way.
+// RT, the plane row word: uint32_t when every room of the set is at most
+// 32 x 32 (PCM 2), else uint64_t.  It is the row width in HBM as well as in
+// LDS, so a set is 8 x sizeof(RT) bytes in HBM (32 B for PCM 2: the four sets
+// of a window axis are 128 contiguous bytes) and half the LDS for PCM 2 (16
+// waves fit a CU).
 template <typename RT>
 struct PsetGeom {
     static constexpr int STRIDE = sizeof(RT) == 4 ? 8 * 8 + 4 : 8 * 8 + 2;   // RT words per agent, 16-B aligned
 };
 
-__device__ __forceinline__ uint4 *pset_hbm(const Params &p, int8_t *map, bool xs, int c) {
-    return reinterpret_cast<uint4 *>(map + (xs ? p.xp_off : p.yp_off) + (uint32_t)c * 64u);
-}
-
-// lane q's share of a set: rows z = 2q, 2q + 1 (16 B of the HBM line)
+// lane q's share of a set: rows z = 2q, 2q + 1
 template <typename RT>
-__device__ __forceinline__ void pset_put(RT *ps, int slot, int q, uint4 v) {
-    if constexpr (sizeof(RT) == 8)
-        *reinterpret_cast<uint4 *>(ps + slot * 8 + 2 * q) = v;
-    else
-        *reinterpret_cast<uint2 *>(ps + slot * 8 + 2 * q) = make_uint2(v.x, v.z);
+using PsetShare = typename std::conditional<sizeof(RT) == 8, uint4, uint2>::type;
+
+template <typename RT>
+__device__ __forceinline__ PsetShare<RT> pset_zero() {
+    if constexpr (sizeof(RT) == 8) return make_uint4(0u, 0u, 0u, 0u);
+    else return make_uint2(0u, 0u);
 }
 
 template <typename RT>
-__device__ __forceinline__ uint4 pset_get(const RT *ps, int slot, int q) {
-    if constexpr (sizeof(RT) == 8) {
-        return *reinterpret_cast<const uint4 *>(ps + slot * 8 + 2 * q);
-    } else {
-        const uint2 w = *reinterpret_cast<const uint2 *>(ps + slot * 8 + 2 * q);
-        return make_uint4(w.x, 0u, w.y, 0u);
-    }
+__device__ __forceinline__ PsetShare<RT> *pset_hbm(const Params &p, int8_t *map, bool xs, int c) {
+    return reinterpret_cast<PsetShare<RT> *>(map + (xs ? p.xp_off : p.yp_off) + (uint32_t)c * (8u * sizeof(RT)));
+}
+
+template <typename RT>
+__device__ __forceinline__ void pset_put(RT *ps, int slot, int q, PsetShare<RT> v) {
+    *reinterpret_cast<PsetShare<RT> *>(ps + slot * 8 + 2 * q) = v;
+}
+
+template <typename RT>
+__device__ __forceinline__ PsetShare<RT> pset_get(const RT *ps, int slot, int q) {
+    return *reinterpret_cast<const PsetShare<RT> *>(ps + slot * 8 + 2 * q);
 }
 
 // the known bits (byte z: 0x80) the planes hold for column (cx, cy), both in the window
@@ -714,17 +718,17 @@ __device__ __forceinline__ uint64_t pset_known(const RT *ps, int cx, int cy) {
     return k;
 }
 
-// launch start: lane q loads 16 B of each of the 8 sets (one 64-B request per set)
+// launch start: lane q loads its share of each of the 8 sets
 template <typename RT>
 __device__ __forceinline__ void pset_fill(const Params &p, int8_t *map, RT *ps, const Agent &g, const Room &R, int q) {
-    uint4 v[8];
+    PsetShare<RT> v[8];
 #pragma unroll
     for (int s = 0; s < 4; ++s) {
         const int yy = g.y - 2 + s, xx = g.x - 2 + s;
-        v[s] = make_uint4(0u, 0u, 0u, 0u);
-        v[4 + s] = make_uint4(0u, 0u, 0u, 0u);
-        if (yy >= 0 && yy < R.D) v[s] = pset_hbm(p, map, true, yy)[q];
-        if (xx >= 0 && xx < R.W) v[4 + s] = pset_hbm(p, map, false, xx)[q];
+        v[s] = pset_zero<RT>();
+        v[4 + s] = pset_zero<RT>();
+        if (yy >= 0 && yy < R.D) v[s] = pset_hbm<RT>(p, map, true, yy)[q];
+        if (xx >= 0 && xx < R.W) v[4 + s] = pset_hbm<RT>(p, map, false, xx)[q];
     }
 #pragma unroll
     for (int s = 0; s < 4; ++s) {
@@ -741,14 +745,16 @@ __device__ __forceinline__ void pset_flush(const Params &p, int8_t *map, const R
 #pragma unroll
     for (int s = 0; s < 4; ++s) {
         const int yy = g.y - 2 + s, xx = g.x - 2 + s;
-        if (((pdirty >> (yy & 3)) & 1u) && yy >= 0 && yy < R.D) pset_hbm(p, map, true, yy)[q] = pset_get(ps, yy & 3, q);
+        if (((pdirty >> (yy & 3)) & 1u) && yy >= 0 && yy < R.D)
+            pset_hbm<RT>(p, map, true, yy)[q] = pset_get(ps, yy & 3, q);
         if (((pdirty >> (4 + (xx & 3))) & 1u) && xx >= 0 && xx < R.W)
-            pset_hbm(p, map, false, xx)[q] = pset_get(ps, 4 + (xx & 3), q);
+            pset_hbm<RT>(p, map, false, xx)[q] = pset_get(ps, 4 + (xx & 3), q);
     }
 }
 
+template <typename RT>
 struct SetLoad {
-    uint4 v;
+    PsetShare<RT> v;
     int slot;
 };
 
@@ -758,19 +764,19 @@ struct SetLoad {
 // write-back (vmcnt retires in issue order).
 template <typename RT>
 __device__ __forceinline__ void pset_shift_issue(const Params &p, int8_t *map, const RT *ps, int dir, int x, int y,
-                                                 const Room &R, uint32_t pdirty, int q, SetLoad &sl) {
+                                                 const Room &R, uint32_t pdirty, int q, SetLoad<RT> &sl) {
     const bool xm = dir < 2;
     const int e = xm ? (dir == 0 ? x + 1 : x - 2) : (dir == 2 ? y + 1 : y - 2);
     const int l = (dir == 0 || dir == 2) ? e - 4 : e + 4;
     const int lim = xm ? R.W : R.D;
     sl.slot = xm ? 4 + (e & 3) : (e & 3);
-    sl.v = make_uint4(0u, 0u, 0u, 0u);
-    if (!(VN_ABLATE & 1u) && e >= 0 && e < lim) sl.v = pset_hbm(p, map, !xm, e)[q];
-    if (((pdirty >> sl.slot) & 1u) && l >= 0 && l < lim) pset_hbm(p, map, !xm, l)[q] = pset_get(ps, sl.slot, q);
+    sl.v = pset_zero<RT>();
+    if (!(VN_ABLATE & 1u) && e >= 0 && e < lim) sl.v = pset_hbm<RT>(p, map, !xm, e)[q];
+    if (((pdirty >> sl.slot) & 1u) && l >= 0 && l < lim) pset_hbm<RT>(p, map, !xm, l)[q] = pset_get(ps, sl.slot, q);
 }
 
 template <typename RT>
-__device__ __forceinline__ uint32_t pset_shift_commit(RT *ps, const SetLoad &sl, uint32_t pdirty, int q) {
+__device__ __forceinline__ uint32_t pset_shift_commit(RT *ps, const SetLoad<RT> &sl, uint32_t pdirty, int q) {
     pset_put(ps, sl.slot, q, sl.v);
     __builtin_amdgcn_wave_barrier();
     return pdirty & ~(1u << sl.slot);
@@ -1315,7 +1321,7 @@ __device__ __forceinline__ void group_reset(const Params &p, int8_t *map, uint64
         pc_.row = -1;
         if (PC) {                         // the planes were cleared: empty sets
 #pragma unroll
-            for (int k = 0; k < 8; ++k) pset_put(ps, 2 * q + (k >> 2), k & 3, make_uint4(0u, 0u, 0u, 0u));
+            for (int k = 0; k < 8; ++k) pset_put(ps, 2 * q + (k >> 2), k & 3, pset_zero<RT>());
             pdirty = 0;
         }
     }
@@ -1594,7 +1600,7 @@ __global__ __launch_bounds__(PCM ? VN_PC_BLOCK : BLOCK, PCM ? VN_PC_MIN_WAVES : 
         int a = 0;
         bool moved = false, shifted = false, truncated = false;
         ShiftLoad<PH> sl;
-        SetLoad pl;
+        SetLoad<RT> pl;
         uint2 rec = make_uint2(0u, 0u);
         if (active) {
             a = EXT ? p.actions[row] : (int)((acts >> (8 * (uint32_t)(tt & 3u))) & 0xffu);
@@ -1762,7 +1768,7 @@ __global__ __launch_bounds__(PCM ? VN_PC_BLOCK : BLOCK, PCM ? VN_PC_MIN_WAVES : 
             // (PREMOVE: the launch's window was filled around step 0's cell)
             const bool shifted = moved && dir < 4 && !(PREMOVE && k == 0);
             ShiftLoad<PH> sl;
-            SetLoad pl;
+            SetLoad<RT> pl;
             if (shifted) tile_shift_issue<PH>(p, map, tile, dir, g.x, g.y, R, dirty, q, sl);
             if (PC && shifted) pset_shift_issue(p, map, ps, dir, g.x, g.y, R, pdirty, q, pl);
             const uint2 rec = p.rays[R.ray_off + (uint32_t)((g.x * R.D + g.y) * R.H + g.z)];
@@ -3412,8 +3418,14 @@ __global__ void export_belief_kernel(Params p, int8_t *out, int pw, int pd) {
         const uint32_t b = (uint8_t)m[off];
         // a cell is known if its byte says so or a marked-bit plane holds it
         // (plane-set mode records marks outside the window only there)
-        const uint64_t xr = reinterpret_cast<const uint64_t *>(m + p.xp_off)[(size_t)(y * p.ph + z) * p.nwx + (x >> 6)];
-        const uint64_t yr = reinterpret_cast<const uint64_t *>(m + p.yp_off)[(size_t)(x * p.ph + z) * p.nwy + (y >> 6)];
+        uint64_t xr, yr;
+        if (p.pcache == 2) {           // u32 plane rows (PsetGeom)
+            xr = reinterpret_cast<const uint32_t *>(m + p.xp_off)[(size_t)(y * p.ph + z)];
+            yr = reinterpret_cast<const uint32_t *>(m + p.yp_off)[(size_t)(x * p.ph + z)];
+        } else {
+            xr = reinterpret_cast<const uint64_t *>(m + p.xp_off)[(size_t)(y * p.ph + z) * p.nwx + (x >> 6)];
+            yr = reinterpret_cast<const uint64_t *>(m + p.yp_off)[(size_t)(x * p.ph + z) * p.nwy + (y >> 6)];
+        }
         const bool known = (b & KNOWN) || ((xr >> (x & 63)) & 1ull) || ((yr >> (y & 63)) & 1ull);
         v = known ? ((b & 0x40u) ? (int8_t)-2 : (int8_t)(b & 0x3fu)) : (int8_t)-1;
     }
@@ -3869,15 +3881,16 @@ int vn_create(const VnRoomSet *rooms, int32_t n_agents, const VnConfig *cfg, int
         e->map_bytes = (uint32_t)(e->nbx * e->nby * 16 * e->ph);
         e->nwx = (e->pw + 63) / 64;
         e->nwy = (e->pd + 63) / 64;
-        e->xp_off = e->map_bytes;                                        // rows (y, z): pd * ph * nwx words
-        e->yp_off = e->xp_off + (uint32_t)(e->pd * e->ph * e->nwx * 8);  // rows (x, z): pw * ph * nwy words
-        e->agent_bytes = (e->yp_off + (uint32_t)(e->pw * e->ph * e->nwy * 8) + 15u) & ~15u;
-        // plane-set mode: 2 = u32 LDS rows (rooms <= 32 x 32), 1 = u64 rows (<= 64 x 64), 0 = byte marks
+        // plane-set mode: 2 = u32 rows (rooms <= 32 x 32), 1 = u64 rows (<= 64 x 64), 0 = byte marks
         e->pcache = e->ph != 8 ? 0 : (e->pw <= 32 && e->pd <= 32) ? 2 : (e->nwx == 1 && e->nwy == 1) ? 1 : 0;
         if (const char *pc = getenv("VOXNAV_PCACHE")) {   // A/B knob: 0 off, 1 at most u64 rows
             const int v = atoi(pc);
             if (v >= 0 && v < e->pcache) e->pcache = v;
         }
+        const int rowb = e->pcache == 2 ? 4 : 8;                            // plane row bytes
+        e->xp_off = e->map_bytes;                                           // rows (y, z): pd * ph * nwx words
+        e->yp_off = e->xp_off + (uint32_t)(e->pd * e->ph * e->nwx * rowb);  // rows (x, z): pw * ph * nwy words
+        e->agent_bytes = (e->yp_off + (uint32_t)(e->pw * e->ph * e->nwy * rowb) + 15u) & ~15u;
     }
 
     DeviceGuard dg(device);
