@@ -2854,6 +2854,13 @@ __device__ __forceinline__ void sp_reset_wave(const Params &p, const SPlanes &pl
     }
 }
 
+// Consume values in registers (an empty asm that reads them): the compiler
+// then waits for their loads HERE, inside a conditional block, rather than
+// carrying them as "maybe pending" into a loop, where it would wait vmcnt(0)
+// -- for every load AND store in flight -- at their first use each iteration.
+__device__ __forceinline__ void vn_touch(uint32_t a) { asm volatile("" ::"v"(a)); }
+__device__ __forceinline__ void vn_touch(uint64_t a) { asm volatile("" ::"v"(a)); }
+
 struct SPend {
     int a, d, facing, nx, ny, nz;
     bool moved;
@@ -2876,7 +2883,8 @@ __global__ __launch_bounds__(128) void simple_pipe_kernel(Params p) {
             const int b = k & 1;
             const float *st = stage + b * 64 * OD;
             float *dst = p.obs + ((size_t)k * p.N + a0) * OD;
-            if (!((rows * OD) & 3) && !(reinterpret_cast<uintptr_t>(dst) & 15u)) {
+            if (VN_ABLATE & 16u) {
+            } else if (!((rows * OD) & 3) && !(reinterpret_cast<uintptr_t>(dst) & 15u)) {
                 const float4 *s4 = reinterpret_cast<const float4 *>(st);
                 float4 *d4 = reinterpret_cast<float4 *>(dst);
                 for (int q = lane; q < (rows * OD) >> 2; q += 64) obs_store(d4 + q, s4[q]);
@@ -2908,6 +2916,14 @@ __global__ __launch_bounds__(128) void simple_pipe_kernel(Params p) {
     w.wz = 0;
     w.rec = make_uint2(0u, 0u);
     if (live) sb_load_rows(p, pl, g, R, w);
+    vn_touch(w.wx);
+    vn_touch(w.wy);
+    vn_touch(w.wz);
+    vn_touch(w.rec.x);
+    vn_touch(w.rec.y);
+    vn_touch((uint32_t)R.ray_off);
+    vn_touch((uint32_t)R.total_free);
+    vn_touch((uint32_t)(R.D | (R.H << 8)));
 
     uint4 r4 = make_uint4(0u, 0u, 0u, 0u);      // Philox block r4blk (4 steps)
     uint64_t r4blk = ~0ull;
@@ -2915,6 +2931,15 @@ __global__ __launch_bounds__(128) void simple_pipe_kernel(Params p) {
     SRows wn;                                    // ... and the rows at its target (in flight)
     uint64_t cbx = 0ull, cby = 0ull;             // S bits its commit adds to wn's kept rows
     uint32_t cbz = 0u;
+    // The S words in w are write-back cached: a mark sets their dirty bits
+    // (1 x, 2 y, 4 z); a word is stored when a move replaces it (eviction:
+    // its row at the cell being left) and at the end of the launch.  The
+    // evicted words of a commit are stored after the next move's loads; a
+    // load of an evicted row takes the evicted value (forwarding).
+    uint32_t sdirty = 0u, evm = 0u;              // dirty words; evicted words pending store
+    uint64_t evx = 0ull, evy = 0ull;             // evicted values ...
+    uint32_t evz = 0u;
+    int evyx = 0, evxy = 0, evz_ = 0, evxx = 0, evyy = 0;   // ... and their rows: x (y,z)  y (x,z)  z (x,y)
     // the move of launch step k from the committed state; issues the target's loads
     auto premove = [&](int k) {
         const uint64_t t = p.t0 + (uint64_t)k;
@@ -2943,9 +2968,9 @@ __global__ __launch_bounds__(128) void simple_pipe_kernel(Params p) {
             // rows and the ray record are the target's.  These rows never hold
             // the bit the commit of this move sets (they are off the current cell).
             const int ax = d >> 1;
-            if (ax != 0) wn.wx = pl.sx[pm.ny * p.ph + pm.nz];
-            if (ax != 1) wn.wy = pl.sy[pm.nx * p.ph + pm.nz];
-            if (ax != 2) wn.wz = pl.sz[pm.nx * p.pd + pm.ny];
+            if (ax != 0) wn.wx = ((evm & 1u) && evyx == pm.ny && evz_ == pm.nz) ? evx : pl.sx[pm.ny * p.ph + pm.nz];
+            if (ax != 1) wn.wy = ((evm & 2u) && evxy == pm.nx && evz_ == pm.nz) ? evy : pl.sy[pm.nx * p.ph + pm.nz];
+            if (ax != 2) wn.wz = ((evm & 4u) && evxx == pm.nx && evyy == pm.ny) ? evz : pl.sz[pm.nx * p.pd + pm.ny];
             wn.rec = p.rays[R.ray_off + (uint32_t)((pm.nx * R.D + pm.ny) * R.H + pm.nz)];
         }
     };
@@ -2968,10 +2993,23 @@ __global__ __launch_bounds__(128) void simple_pipe_kernel(Params p) {
                 const int ax = pm.d >> 1;
                 // the target's S bit from the cached word of the move axis (kept in wn)
                 seen = ax == 0 ? ((w.wx >> pm.nx) & 1ull) : ax == 1 ? ((w.wy >> pm.ny) & 1ull) : ((w.wz >> pm.nz) & 1u);
+                // evict the dirty words this move replaces (rows at the cell left)
+                evm = sdirty & ~(1u << ax);
+                evx = w.wx;
+                evy = w.wy;
+                evz = w.wz;
+                evyx = g.y;
+                evz_ = g.z;
+                evxy = g.x;
+                evxx = g.x;
+                evyy = g.y;
+                sdirty &= 1u << ax;
                 g.x = pm.nx;
                 g.y = pm.ny;
                 g.z = pm.nz;
                 w = wn;
+            } else {
+                evm = 0u;
             }
             // the bits of the previous step's mark that this move's rows were
             // copied without (see below)
@@ -2984,6 +3022,12 @@ __global__ __launch_bounds__(128) void simple_pipe_kernel(Params p) {
             // ---- the next step's move and its loads, issued before this step's
             // S-mark stores (a wait for these loads then never waits for them) ----
             if (k + 1 < p.K) premove(k + 1);
+            if (!(VN_ABLATE & 1024u)) {                 // the evicted words, behind the loads
+                if (evm & 1u) pl.sx[evyx * p.ph + evz_] = evx;
+                if (evm & 2u) pl.sy[evxy * p.ph + evz_] = evy;
+                if (evm & 4u) pl.sz[evxx * p.pd + evyy] = evz;
+            }
+            evm = 0u;
             if (moved) {
                 // a Q cell (internal_grid 2) is entered without counting, but it
                 // is a sensing position all the same, so S is set
@@ -3001,9 +3045,7 @@ __global__ __launch_bounds__(128) void simple_pipe_kernel(Params p) {
                     if (nax <= 0) cbx = bx;
                     if (nax == -1 || nax == 1) cby = by;
                     if (nax == -1 || nax == 2) cbz = bz;
-                    pl.sx[g.y * p.ph + g.z] = w.wx;
-                    pl.sy[g.x * p.ph + g.z] = w.wy;
-                    pl.sz[g.x * p.pd + g.y] = w.wz;
+                    sdirty = 7u;
                     if (!q) {
                         g.visited += 1;
                         explored = true;
@@ -3044,12 +3086,22 @@ __global__ __launch_bounds__(128) void simple_pipe_kernel(Params p) {
                 next_seed += p.seed_stride;
                 cbx = cby = 0ull;
                 cbz = 0u;
+                sdirty = 0u;                             // the reset stored the start cell's words
+                evm = 0u;
                 if (k + 1 < p.K) premove(k + 1);                         // from the start cell
+                vn_touch(w.rec.x);
+                vn_touch(w.rec.y);
+                vn_touch((uint32_t)R.ray_off);
+                vn_touch((uint32_t)R.total_free);
+                vn_touch((uint32_t)(R.D | (R.H << 8)));
             }
         }
         lds_handoff();                         // hand buffer b to the store wave
     }
     if (live) {
+        if (sdirty & 1u) pl.sx[g.y * p.ph + g.z] = w.wx;
+        if (sdirty & 2u) pl.sy[g.x * p.ph + g.z] = w.wy;
+        if (sdirty & 4u) pl.sz[g.x * p.pd + g.y] = w.wz;
         p.hot[ai] = pack(g);
         p.goal[ai] = goal;
         p.next_seed[ai] = next_seed;
