@@ -195,6 +195,25 @@ __device__ __forceinline__ Room load_room(const Params &p, int r) {
 }
 
 
+// Consume values in registers (an empty asm that reads them): the compiler
+// then waits for their loads HERE, inside a conditional block, rather than
+// carrying them as "maybe pending" into a loop, where it would wait vmcnt(0)
+// -- for every load AND store in flight -- at their first use each iteration.
+__device__ __forceinline__ void vn_touch(uint32_t a) { asm volatile("" ::"v"(a)); }
+__device__ __forceinline__ void vn_touch(uint64_t a) { asm volatile("" ::"v"(a)); }
+
+// every field of a room descriptor (load_room)
+__device__ __forceinline__ void room_touch(const Room &R) {
+    vn_touch((uint32_t)(R.W | (R.D << 8) | (R.H << 16)));
+    vn_touch(R.total_free);
+    vn_touch(R.ray_off);
+    vn_touch(R.start_off);
+    vn_touch(R.finish_visits);
+    vn_touch((uint32_t)R.fixed_start);
+    vn_touch((uint32_t)R.fixed_goal);
+    vn_touch((uint32_t)(R.nbx | (R.nby << 16)));
+}
+
 // ----------------------------------------------------------------------------
 // CPython random: streaming MT19937 seed (init_by_array with a one-word key)
 // that keeps only the words the first MT_C outputs need, so a reset runs
@@ -1305,6 +1324,7 @@ __device__ __forceinline__ void group_reset(const Params &p, int8_t *map, uint64
         const uint32_t drawn = reset_prepare<PH, PC>(p.envc, seed, map, q);
         const int room = (int)(drawn >> 24);
         R = load_room(p, room);
+        room_touch(R);           // settled here, not as "maybe pending" in the step loop
         g.room = room;
         g.x = drawn & 0xff;
         g.y = (drawn >> 8) & 0xff;
@@ -1449,6 +1469,7 @@ __global__ __launch_bounds__(PCM ? VN_PC_BLOCK : BLOCK, PCM ? VN_PC_MIN_WAVES : 
     uint64_t *tile = tiles + (threadIdx.x / GROUP) * TileGeom<PH>::STRIDE;
     Agent g = unpack(hot0);
     Room R = load_room(p, active ? g.room : 0);
+    room_touch(R);
     int8_t *map = p.belief + (size_t)ai * p.agent_bytes;
     uint32_t dirty = 0;
     PlaneCache pc_;
@@ -2853,13 +2874,6 @@ __device__ __forceinline__ void sp_reset_wave(const Params &p, const SPlanes &pl
         sb_observe<LMAX>(p, pl, g, w, row);
     }
 }
-
-// Consume values in registers (an empty asm that reads them): the compiler
-// then waits for their loads HERE, inside a conditional block, rather than
-// carrying them as "maybe pending" into a loop, where it would wait vmcnt(0)
-// -- for every load AND store in flight -- at their first use each iteration.
-__device__ __forceinline__ void vn_touch(uint32_t a) { asm volatile("" ::"v"(a)); }
-__device__ __forceinline__ void vn_touch(uint64_t a) { asm volatile("" ::"v"(a)); }
 
 struct SPend {
     int a, d, facing, nx, ny, nz;
