@@ -154,7 +154,7 @@ __global__ __launch_bounds__(256) void lstm_cell_kernel(const T *__restrict__ gx
 //   gates[n][4H] = [x_n | h_n] @ [W_ih | W_hh]^T + (b_ih + b_hh)
 // with v_mfma_f32_32x32x16_bf16 (f32 accumulation), and the cell update as
 // the epilogue, so the 4H gate pre-activations never leave the registers.
-// Block: 4 waves, 64 agents x 64 hidden units x 4 gates; wave w owns rows
+// Block: 4 waves (VN_LF_ROWS 64), 64 agents x 64 hidden units x 4 gates; wave w owns rows
 // 32*(w&1).. and units 32*(w>>1).., one 32x32 accumulator per gate, so the
 // four gates of a (row, unit) sit in the same lane and register.  K is
 // streamed in chunks of 64 through LDS (rows padded to 72 bf16), the next
@@ -167,25 +167,37 @@ __global__ __launch_bounds__(256) void lstm_cell_kernel(const T *__restrict__ gx
 typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8_t;
 typedef __attribute__((ext_vector_type(16))) float f32x16_t;
 
-constexpr int LF_ROWS = 64, LF_UNITS = 64;
+#ifndef VN_LF_ROWS
+#define VN_LF_ROWS 64   // 128 (8 waves, 1 block per CU at 154 VGPRs) measured 358 vs 336 us
+#endif
+constexpr int LF_ROWS = VN_LF_ROWS, LF_UNITS = 64;
+constexpr int LF_WAVES = (LF_ROWS / 32) * (LF_UNITS / 32), LF_T = 64 * LF_WAVES;   // threads per block
 #ifndef VN_LF_KC
 #define VN_LF_KC 64
 #endif
 constexpr int LF_KC = VN_LF_KC;           // K per chunk (bf16 elements)
 constexpr int LF_LDK = LF_KC + 8;         // LDS row pitch (+16 B against bank conflicts)
 constexpr int LF_GPR = LF_KC / 8;         // 16-byte groups per row and chunk
-constexpr int LF_NA = LF_ROWS * LF_GPR / 256, LF_NB = 4 * LF_UNITS * LF_GPR / 256;   // groups per thread
+constexpr int LF_NA = LF_ROWS * LF_GPR / LF_T, LF_NB = 4 * LF_UNITS * LF_GPR / LF_T;   // groups per thread
 
 // gate nonlinearities of the bf16 path on the hardware exp / rcp (~1e-6
 // relative; the operands are bf16 already): 5 per (row, unit), 80 per lane
 __device__ __forceinline__ float fast_sigm(float x) { return __frcp_rn(1.0f + __expf(-x)); }
 __device__ __forceinline__ float fast_tanh(float x) { return 2.0f * fast_sigm(2.0f * x) - 1.0f; }
 
+#ifndef VN_LF_RAW_BARRIER
+#define VN_LF_RAW_BARRIER 1
+#endif
 #ifndef VN_LF_MIN_WAVES
-#define VN_LF_MIN_WAVES 3   // 3 blocks of 4 waves per CU
+#define VN_LF_MIN_WAVES (LF_ROWS == 64 ? 3 : 1)   // blocks per CU the register budget is sized for
 #endif
 template <bool VEC_X>   // obs_dim % 8 == 0: branch-free staging loads
-__global__ __launch_bounds__(256, VN_LF_MIN_WAVES) void lstm_fused_bf16_kernel(
+#ifdef VN_LF_WPE
+#define LF_WPE_ATTR __attribute__((amdgpu_waves_per_eu(VN_LF_WPE, VN_LF_WPE)))
+#else
+#define LF_WPE_ATTR
+#endif
+__global__ __launch_bounds__(LF_T, VN_LF_MIN_WAVES) LF_WPE_ATTR void lstm_fused_bf16_kernel(
     const float *__restrict__ x, int obs_dim, int kx, const uint16_t *__restrict__ hin,
     const uint16_t *__restrict__ w, int Kp, const float *__restrict__ bias, float *__restrict__ c,
     uint16_t *__restrict__ hout, float *__restrict__ h32, float *__restrict__ h_store, float *__restrict__ c_store,
@@ -219,17 +231,17 @@ __global__ __launch_bounds__(256, VN_LF_MIN_WAVES) void lstm_fused_bf16_kernel(
     const uint16_t *wb = w + (size_t)b * 4 * H * Kp;
     const uint16_t *hb = hin + (size_t)b * N * H;
 
-    static_assert(LF_NA == 2 && LF_NB == 8, "staging registers are spelled out for LF_KC = 64");
+    static_assert(LF_NA == 2 && (LF_NB == 8 || LF_NB == 4), "staging registers are spelled out for LF_KC = 64");
     // raw staging registers: an A group is 8 obs floats (x columns) or 8 bf16
     // of h (in lo); it is converted when written to LDS, so no wait sits
     // between issuing the next chunk's loads and this chunk's MFMAs
     float4 ra0lo, ra0hi, ra1lo, ra1hi;
-    uint4 rb0, rb1, rb2, rb3, rb4, rb5, rb6, rb7;
+    uint4 rb0, rb1, rb2, rb3, rb4, rb5, rb6, rb7;   // named: an indexed array would live in scratch
 #define LF_A_LOAD(lo, hi, i)                                                                                \
     if (VEC_X) {                                                                                            \
         /* unconditional loads from a clamped address, zeroed when written to LDS: */                       \
         /* a loaded value merged across branches would force a wait right here     */                       \
-        const int gi_ = tid + 256 * (i), k_ = k0_ + (gi_ % LF_GPR) * 8;                                    \
+        const int gi_ = tid + LF_T * (i), k_ = k0_ + (gi_ % LF_GPR) * 8;                                    \
         const int n_ = min(n_base + gi_ / LF_GPR, N - 1);                                                   \
         const bool isx_ = k_ < kx;                                                                          \
         const float *p_ = isx_ ? x + (size_t)n_ * obs_dim + k_                                              \
@@ -237,7 +249,7 @@ __global__ __launch_bounds__(256, VN_LF_MIN_WAVES) void lstm_fused_bf16_kernel(
         lo = *reinterpret_cast<const float4 *>(p_);                                                         \
         hi = *reinterpret_cast<const float4 *>(p_ + (isx_ ? 4 : 0));                                        \
     } else {                                                                                                \
-        const int gi_ = tid + 256 * (i), k_ = k0_ + (gi_ % LF_GPR) * 8;                                    \
+        const int gi_ = tid + LF_T * (i), k_ = k0_ + (gi_ % LF_GPR) * 8;                                    \
         const int n_ = n_base + gi_ / LF_GPR;                                                               \
         lo = make_float4(0.f, 0.f, 0.f, 0.f);                                                               \
         hi = lo;                                                                                            \
@@ -255,7 +267,7 @@ __global__ __launch_bounds__(256, VN_LF_MIN_WAVES) void lstm_fused_bf16_kernel(
     }
 #define LF_B(dst, i)                                                                                        \
     {                                                                                                       \
-        const int gi_ = tid + 256 * (i), lrow_ = gi_ / LF_GPR, gate_ = lrow_ / LF_UNITS;                   \
+        const int gi_ = tid + LF_T * (i), lrow_ = gi_ / LF_GPR, gate_ = lrow_ / LF_UNITS;                   \
         const int uu_ = lrow_ - gate_ * LF_UNITS;                                                           \
         dst = *reinterpret_cast<const uint4 *>(wb + (size_t)(gate_ * H + u_base + uu_) * Kp + k0_ +         \
                                                (gi_ % LF_GPR) * 8);                                         \
@@ -263,12 +275,13 @@ __global__ __launch_bounds__(256, VN_LF_MIN_WAVES) void lstm_fused_bf16_kernel(
 #define LF_LOAD_CHUNK(ch)                                                                                   \
     {                                                                                                       \
         const int k0_ = (ch) * LF_KC;                                                                       \
-        LF_B(rb0, 0) LF_B(rb1, 1) LF_B(rb2, 2) LF_B(rb3, 3) LF_B(rb4, 4) LF_B(rb5, 5) LF_B(rb6, 6) LF_B(rb7, 7) \
+        LF_B(rb0, 0) LF_B(rb1, 1) LF_B(rb2, 2) LF_B(rb3, 3)                                                 \
+        if (LF_NB > 4) { LF_B(rb4, 4) LF_B(rb5, 5) LF_B(rb6, 6) LF_B(rb7, 7) }                               \
         LF_A_LOAD(ra0lo, ra0hi, 0) LF_A_LOAD(ra1lo, ra1hi, 1)                                               \
     }
 #define LF_A_PUT(lo, hi, i)                                                                                 \
     {                                                                                                       \
-        const int gi_ = tid + 256 * (i), k_ = k0_ + (gi_ % LF_GPR) * 8;                                    \
+        const int gi_ = tid + LF_T * (i), k_ = k0_ + (gi_ % LF_GPR) * 8;                                    \
         uint4 v_;                                                                                           \
         if (VEC_X && (n_base + gi_ / LF_GPR >= N || k_ >= K)) {                                             \
             v_ = make_uint4(0u, 0u, 0u, 0u);                                                                \
@@ -283,7 +296,7 @@ __global__ __launch_bounds__(256, VN_LF_MIN_WAVES) void lstm_fused_bf16_kernel(
     }
 #define LF_PUT(base, src, i)                                                                                \
     {                                                                                                       \
-        const int gi_ = tid + 256 * (i);                                                                    \
+        const int gi_ = tid + LF_T * (i);                                                                    \
         *reinterpret_cast<uint4 *>(&base[(gi_ / LF_GPR) * LF_LDK + (gi_ % LF_GPR) * 8]) = src;              \
     }
 #define LF_STORE_CHUNK(ch)                                                                                   \
@@ -291,7 +304,7 @@ __global__ __launch_bounds__(256, VN_LF_MIN_WAVES) void lstm_fused_bf16_kernel(
         const int k0_ = (ch) * LF_KC;                                                                       \
         LF_A_PUT(ra0lo, ra0hi, 0) LF_A_PUT(ra1lo, ra1hi, 1)                                                 \
         LF_PUT(Bs, rb0, 0) LF_PUT(Bs, rb1, 1) LF_PUT(Bs, rb2, 2) LF_PUT(Bs, rb3, 3)                         \
-        LF_PUT(Bs, rb4, 4) LF_PUT(Bs, rb5, 5) LF_PUT(Bs, rb6, 6) LF_PUT(Bs, rb7, 7)                         \
+        if (LF_NB > 4) { LF_PUT(Bs, rb4, 4) LF_PUT(Bs, rb5, 5) LF_PUT(Bs, rb6, 6) LF_PUT(Bs, rb7, 7) }       \
     }
 
     f32x16_t acc[4];
@@ -299,14 +312,28 @@ __global__ __launch_bounds__(256, VN_LF_MIN_WAVES) void lstm_fused_bf16_kernel(
     for (int g = 0; g < 4; ++g)
 #pragma unroll
         for (int r = 0; r < 16; ++r) acc[g][r] = 0.0f;
-    const int wr = (wv & 1) * 32, wu = (wv >> 1) * 32;
+    const int wr = (wv % (LF_ROWS / 32)) * 32, wu = (wv / (LF_ROWS / 32)) * 32;
 #ifndef VN_LF_DIAG
 #define VN_LF_DIAG 0   // timing diagnostics: 1 skips the K loop, 2 a cheap epilogue (results invalid)
+#endif
+    // Block barriers that order only LDS (lgkmcnt(0) + s_barrier): a
+    // __syncthreads() also waits vmcnt(0), i.e. for the next chunk's
+    // prefetch, so that prefetch could only overlap one chunk's MFMAs
+#if VN_LF_RAW_BARRIER
+#define LF_BARRIER()                                                                                        \
+    {                                                                                                       \
+        asm volatile("" ::: "memory");                                                                      \
+        __builtin_amdgcn_s_waitcnt(0xC07F);                                                                 \
+        __builtin_amdgcn_s_barrier();                                                                       \
+        asm volatile("" ::: "memory");                                                                      \
+    }
+#else
+#define LF_BARRIER() __syncthreads();
 #endif
     LF_LOAD_CHUNK(0)
     for (int ch = 0; ch < (VN_LF_DIAG == 1 ? 0 : nchunks); ++ch) {
         LF_STORE_CHUNK(ch)
-        __syncthreads();
+        LF_BARRIER()
         // next chunk, in flight during this chunk's MFMAs (the last iteration
         // reloads its own chunk: unconditional, so the staging stays in
         // registers); the scheduling barrier keeps the loads ahead of the MFMAs
@@ -323,8 +350,9 @@ __global__ __launch_bounds__(256, VN_LF_MIN_WAVES) void lstm_fused_bf16_kernel(
                 acc[g] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, bv, acc[g], 0, 0, 0);
             }
         }
-        __syncthreads();
+        LF_BARRIER()
     }
+#undef LF_BARRIER
 #undef LF_LOAD_CHUNK
 #undef LF_STORE_CHUNK
 #undef LF_A_LOAD
@@ -334,6 +362,14 @@ __global__ __launch_bounds__(256, VN_LF_MIN_WAVES) void lstm_fused_bf16_kernel(
 
     // epilogue: lane holds unit u for 16 rows; gate g of (row, u) in acc[g][reg]
     const int u = u_base + wu + (lane & 31);
+    // the 16 cell states loaded together first: loaded row by row, each load
+    // would wait behind the previous row's five stores (vmcnt retires in order)
+    float cin[16];
+#pragma unroll
+    for (int reg = 0; reg < 16; ++reg) {
+        const int n = min(n_base + wr + (reg & 3) + 8 * (reg >> 2) + 4 * (lane >> 5), N - 1);
+        cin[reg] = c[((size_t)b * N + n) * H + u];
+    }
     const float *bb = bias + (size_t)b * 4 * H;
     const float bi = bb[u], bf = bb[H + u], bg = bb[2 * H + u], bo = bb[3 * H + u];
 #pragma unroll
@@ -347,7 +383,7 @@ __global__ __launch_bounds__(256, VN_LF_MIN_WAVES) void lstm_fused_bf16_kernel(
             const float ig = fast_sigm(acc[0][reg] + bi), fg = fast_sigm(acc[1][reg] + bf);
             const float gg = fast_tanh(acc[2][reg] + bg), og = fast_sigm(acc[3][reg] + bo);
 #endif
-            const float fc = fg * c[so], ig2 = ig * gg;
+            const float fc = fg * cin[reg], ig2 = ig * gg;
             const float cn = fc + ig2;
 #if VN_LF_DIAG == 2
             const float hn = og * cn;
@@ -693,10 +729,10 @@ int vn_lstm_fused_bf16(const float *x, int32_t obs_dim, const uint16_t *h_in, co
     const int ncombo = n_lstm * (H / LF_UNITS);
     const dim3 grid((unsigned)((N + LF_ROWS - 1) / LF_ROWS) * (unsigned)ncombo);
     if ((obs_dim & 7) == 0)
-        hipLaunchKernelGGL(lstm_fused_bf16_kernel<true>, grid, dim3(256), 0, (hipStream_t)stream, x, (int)obs_dim,
+        hipLaunchKernelGGL(lstm_fused_bf16_kernel<true>, grid, dim3(LF_T), 0, (hipStream_t)stream, x, (int)obs_dim,
                            kx, h_in, w_cat, (int)Kp, bias, c, h_out, h32, h_store, c_store, (int)N, (int)H, ncombo);
     else
-        hipLaunchKernelGGL(lstm_fused_bf16_kernel<false>, grid, dim3(256), 0, (hipStream_t)stream, x, (int)obs_dim,
+        hipLaunchKernelGGL(lstm_fused_bf16_kernel<false>, grid, dim3(LF_T), 0, (hipStream_t)stream, x, (int)obs_dim,
                            kx, h_in, w_cat, (int)Kp, bias, c, h_out, h32, h_store, c_store, (int)N, (int)H, ncombo);
     VN_HIP(hipGetLastError());
     return VN_OK;
