@@ -985,7 +985,7 @@ template <int PH, bool FRESH, bool PC, typename RT>
 __device__ __forceinline__ int sense_observe(const Params &p, int8_t *map, uint64_t *tile, uint32_t &dirty,
                                              PlaneCache &pc_, RT *ps, uint32_t &pdirty, Agent &g,
                                              const Room &R, bool moved, bool &explored, const float *tab, ObsDst dst,
-                                             uint2 rec, int q) {
+                                             uint2 rec, int q, bool lut_stale = true) {
     const int x = g.x, y = g.y, z = g.z, nby = p.nby, L = p.L;
 
     // ---- x / y marked-bit plane rows (lane 0: x row (y,z), lane 1: y row (x,z)) ----
@@ -1204,7 +1204,7 @@ __device__ __forceinline__ int sense_observe(const Params &p, int8_t *map, uint6
                                    : reinterpret_cast<float4 *>(dst.row);
     float4 tail;                                                  // obs[64 + 4q .. +3]
     if (PC && to_stage) {
-        tail = make_float4((float)((double)g.visited / (double)R.total_free), 0.f, 0.f, 0.f);      // (:291)
+        tail = make_float4(0.f, 0.f, 0.f, 0.f);       // obs[72] is the agent's LUT entry (below)
     } else if (q == 0) {
         tail = make_float4(g.facing == 0 ? 1.0f : 0.0f, g.facing == 1 ? 1.0f : 0.0f, g.facing == 2 ? 1.0f : 0.0f,
                            g.facing == 3 ? 1.0f : 0.0f);                                            // (:279-280)
@@ -1225,7 +1225,10 @@ __device__ __forceinline__ int sense_observe(const Params &p, int8_t *map, uint6
         const uint32_t w1 = (TC_ACT + (uint32_t)g.last_action) | ((g.was_near_wall ? TC_ONE : TC_ZERO) << 8) |
                             ((g.last_bump ? TC_ONE : TC_ZERO) << 16) | ((TC_CID + (uint32_t)g.cid) << 24);
         const uint32_t c72 = tc_slot((int)(threadIdx.x >> 2));
-        if (q == 2) const_cast<float *>(tab)[tab_ix(c72)] = tail.x;
+        // the entry changes only with visited (a newly explored cell, a
+        // reset) and is stale at launch start: the f64 division only then
+        if (q == 2 && (FRESH || explored || lut_stale))
+            const_cast<float *>(tab)[tab_ix(c72)] = (float)((double)g.visited / (double)R.total_free);   // (:291)
         l[16 + q] = q == 0 ? w0 : q == 1 ? w1 : q == 2 ? (c72 | (TC_ZERO4 & 0xffffff00u)) : TC_ZERO4;
     } else if (to_stage) {
         // float rows (20 float4 per agent): the LDS this costs is free in the
@@ -1676,7 +1679,7 @@ __global__ __launch_bounds__(PCM ? VN_PC_BLOCK : BLOCK, PCM ? VN_PC_MIN_WAVES : 
                              p.terminal_obs ? p.terminal_obs + row * VN_OBS_DIM : nullptr, wst,
                              p.autoreset != 0, truncated, aslot};
             const int vv = sense_observe<PH, false, PC, RT>(p, map, tile, dirty, pc_, ps, pdirty, g, R, moved,
-                                                            explored, tab, dst, rec, q);
+                                                            explored, tab, dst, rec, q, k == 0);
 
             // compute_reward (:169-224), f64 in the reference's order
             double r = -0.05;
@@ -1809,7 +1812,7 @@ __global__ __launch_bounds__(PCM ? VN_PC_BLOCK : BLOCK, PCM ? VN_PC_MIN_WAVES : 
                              p.terminal_obs ? p.terminal_obs + row * VN_OBS_DIM : nullptr, wst,
                              p.autoreset != 0, truncated, aslot};
             const int vv = sense_observe<PH, false, PC, RT>(p, map, tile, dirty, pc_, ps, pdirty, g, R, moved,
-                                                            explored, tab, dst, rec, q);
+                                                            explored, tab, dst, rec, q, k == 0);
             ENV_T(2);
 
             if constexpr (STRIPE_R) {
