@@ -22,9 +22,12 @@
 // consecutive hidden units of one (LSTM, row), float4 loads and stores.
 // f32 throughout (the reference's dtype), -ffp-contract=off like the rest.
 
+#include <dlfcn.h>
 #include <hip/hip_runtime.h>
+#include <rocblas/rocblas.h>
 
 #include <cstdint>
+#include <mutex>
 
 #include "vn_common.h"
 
@@ -158,6 +161,57 @@ int grid_for(int n_lstm, int B, int H, dim3 &grid) {
     return 0;
 }
 
+// ----------------------------------------------------------------------------
+// The whole time loop in native code (vn_lstm_seq_fwd / vn_lstm_seq_bwd): per
+// step one strided-batched rocBLAS SGEMM for both LSTMs and the cell kernel.
+// Issued from Python, the two launches of a step cost ~30 us of host time
+// against ~20 us of GPU work, so the GPU idled a third of the loop.  rocBLAS
+// is bound at run time (dlopen by soname): in a PyTorch process that is the
+// copy torch already loaded, so the process keeps one rocBLAS / HIP runtime
+// and libvoxnav.so has no link-time BLAS dependency.
+// ----------------------------------------------------------------------------
+struct Blas {
+    decltype(&rocblas_create_handle) create = nullptr;
+    decltype(&rocblas_set_stream) set_stream = nullptr;
+    decltype(&rocblas_sgemm_strided_batched) sgemm_sb = nullptr;
+    rocblas_handle handle[64] = {};   // per device
+    bool ok = false;
+};
+
+Blas &blas() {
+    static Blas b;
+    static std::once_flag once;
+    std::call_once(once, [] {
+        void *h = dlopen("librocblas.so.5", RTLD_NOW | RTLD_NOLOAD);
+        if (!h) h = dlopen("librocblas.so.5", RTLD_NOW | RTLD_LOCAL);
+        if (!h) h = dlopen("librocblas.so", RTLD_NOW | RTLD_LOCAL);
+        if (!h) return;
+        b.create = reinterpret_cast<decltype(&rocblas_create_handle)>(dlsym(h, "rocblas_create_handle"));
+        b.set_stream = reinterpret_cast<decltype(&rocblas_set_stream)>(dlsym(h, "rocblas_set_stream"));
+        b.sgemm_sb =
+            reinterpret_cast<decltype(&rocblas_sgemm_strided_batched)>(dlsym(h, "rocblas_sgemm_strided_batched"));
+        b.ok = b.create && b.set_stream && b.sgemm_sb;
+    });
+    return b;
+}
+
+std::mutex g_blas_mu;
+
+// the calling thread's device's handle, bound to `stream`
+int blas_handle(hipStream_t stream, rocblas_handle &out) {
+    Blas &b = blas();
+    if (!b.ok) return fail(VN_ERR_HIP, "rocBLAS (librocblas.so.5) could not be loaded");
+    int dev = 0;
+    VN_HIP(hipGetDevice(&dev));
+    if (dev < 0 || dev >= 64) return fail(VN_ERR_INVALID, "device %d out of range", dev);
+    std::lock_guard<std::mutex> lk(g_blas_mu);
+    if (!b.handle[dev] && b.create(&b.handle[dev]) != rocblas_status_success)
+        return fail(VN_ERR_HIP, "rocblas_create_handle failed");
+    if (b.set_stream(b.handle[dev], stream) != rocblas_status_success) return fail(VN_ERR_HIP, "rocblas_set_stream failed");
+    out = b.handle[dev];
+    return VN_OK;
+}
+
 }  // namespace
 
 extern "C" {
@@ -191,6 +245,63 @@ int vn_lstm_seq_bwd_cell(const float *dh_out, int64_t dh_out_lstm_stride, const 
     hipLaunchKernelGGL(seq_cell_bwd_kernel, grid, dim3(256), 0, (hipStream_t)stream, dh_out, dh_out_lstm_stride,
                        dh_rec, dc, act, act_lstm_stride, c_prev, c_new, state_lstm_stride, dG, dG_lstm_stride, n_lstm,
                        B, H);
+    VN_HIP(hipGetLastError());
+    return VN_OK;
+}
+
+int vn_lstm_seq_fwd(const float *gx, const float *w_hh, const float *bias, float *hs, float *cs, float *act,
+                    int32_t n_lstm, int32_t L, int32_t B, int32_t H, void *stream) {
+    if (!gx || !w_hh || !bias || !hs || !cs || !act) return fail(VN_ERR_INVALID, "NULL argument");
+    if (n_lstm < 1 || L < 1 || B < 1 || H < 4 || (H % 4)) return fail(VN_ERR_INVALID, "bad sizes n_lstm=%d L=%d B=%d H=%d", n_lstm, L, B, H);
+    const hipStream_t st = (hipStream_t)stream;
+    rocblas_handle h;
+    int rc = blas_handle(st, h);
+    if (rc) return rc;
+    const int64_t G = 4 * (int64_t)H, sstate = (int64_t)(L + 1) * B * H;
+    dim3 grid;
+    grid_for(n_lstm, B, H, grid);
+    const float one = 1.0f, zero = 0.0f;
+    for (int t = 0; t < L; ++t) {
+        // act[t][l] (B x 4H, row-major) = hs[l][t] (B x H) @ W_hh[l]^T: column-major, act^T = W_hh (op T) x hs^T
+        float *at = act + (int64_t)t * n_lstm * B * G;
+        if (blas().sgemm_sb(h, rocblas_operation_transpose, rocblas_operation_none, (rocblas_int)G, B, H, &one, w_hh, H,
+                            G * H, hs + (int64_t)t * B * H, H, sstate, &zero, at, (rocblas_int)G, (int64_t)B * G,
+                            n_lstm) != rocblas_status_success)
+            return fail(VN_ERR_HIP, "rocblas_sgemm_strided_batched (forward step %d) failed", t);
+        hipLaunchKernelGGL(seq_cell_fwd_kernel, grid, dim3(256), 0, st, gx + (int64_t)t * B * n_lstm * G,
+                           (int64_t)n_lstm * G, G, at, bias, cs + (int64_t)t * B * H, cs + (int64_t)(t + 1) * B * H,
+                           hs + (int64_t)(t + 1) * B * H, (int64_t)B * G, sstate, n_lstm, B, H);
+    }
+    VN_HIP(hipGetLastError());
+    return VN_OK;
+}
+
+int vn_lstm_seq_bwd(const float *dh_out, const float *w_hh, const float *act, const float *cs, float *dG, float *dc,
+                    float *dh, int32_t need_dh0, int32_t n_lstm, int32_t L, int32_t B, int32_t H, void *stream) {
+    if (!dh_out || !w_hh || !act || !cs || !dG || !dc || !dh) return fail(VN_ERR_INVALID, "NULL argument");
+    if (n_lstm < 1 || L < 1 || B < 1 || H < 4 || (H % 4)) return fail(VN_ERR_INVALID, "bad sizes n_lstm=%d L=%d B=%d H=%d", n_lstm, L, B, H);
+    const hipStream_t st = (hipStream_t)stream;
+    rocblas_handle h;
+    int rc = blas_handle(st, h);
+    if (rc) return rc;
+    const int64_t G = 4 * (int64_t)H, sstate = (int64_t)(L + 1) * B * H;
+    dim3 grid;
+    grid_for(n_lstm, B, H, grid);
+    const float one = 1.0f, zero = 0.0f;
+    for (int t = L - 1; t >= 0; --t) {
+        float *dgt = dG + (int64_t)t * B * G;
+        hipLaunchKernelGGL(seq_cell_bwd_kernel, grid, dim3(256), 0, st, dh_out + (int64_t)t * B * H, (int64_t)L * B * H,
+                           t < L - 1 ? dh : nullptr, dc, act + (int64_t)t * n_lstm * B * G, (int64_t)B * G,
+                           cs + (int64_t)t * B * H, cs + (int64_t)(t + 1) * B * H, sstate, dgt, (int64_t)L * B * G,
+                           n_lstm, B, H);
+        if (t > 0 || need_dh0) {
+            // dh[l] (B x H) = dG[l][t] (B x 4H) @ W_hh[l] (4H x H): column-major, dh^T = W_hh^T (as stored) x dG^T
+            if (blas().sgemm_sb(h, rocblas_operation_none, rocblas_operation_none, H, B, (rocblas_int)G, &one, w_hh, H,
+                                G * H, dgt, (rocblas_int)G, (int64_t)L * B * G, &zero, dh, H, (int64_t)B * H,
+                                n_lstm) != rocblas_status_success)
+                return fail(VN_ERR_HIP, "rocblas_sgemm_strided_batched (backward step %d) failed", t);
+        }
+    }
     VN_HIP(hipGetLastError());
     return VN_OK;
 }

@@ -83,6 +83,8 @@ _SIGS = {
                                        C.c_int32, C.c_int32, P]),
     "vn_lstm_seq_bwd_cell": (C.c_int, [P, C.c_int64, P, P, P, C.c_int64, P, P, C.c_int64, P, C.c_int64, C.c_int32,
                                        C.c_int32, C.c_int32, P]),
+    "vn_lstm_seq_fwd": (C.c_int, [P, P, P, P, P, P, C.c_int32, C.c_int32, C.c_int32, C.c_int32, P]),
+    "vn_lstm_seq_bwd": (C.c_int, [P, P, P, P, P, P, P, C.c_int32, C.c_int32, C.c_int32, C.c_int32, C.c_int32, P]),
 }
 EXPORTED_SYMBOLS = tuple(_SIGS)
 

@@ -7,16 +7,20 @@ at train/Grid_Train.py:228) and back-propagates through them.  Here both
 LSTMs run together over the padded ``[L, B]`` batch:
 
 forward   ``gx = X @ [W_ih_actor | W_ih_critic]^T`` for all steps (one GEMM);
-          per step ``h_{t-1} @ W_hh^T`` for both LSTMs (one batched GEMM)
-          and ``vn_lstm_seq_fwd_cell`` (gates, cell, h; the activations are
-          kept for the backward pass);
-backward  per step, in reverse, ``vn_lstm_seq_bwd_cell`` (gate gradients
-          dG_t, dc_{t-1}) and ``dh_{t-1} = dG_t @ W_hh`` (batched); then the
-          weight gradients over all steps at once: ``dW_hh = dG^T H_prev``
-          (batched), ``dW_ih = dG^T X``, ``db = sum dG``.
+          then ``vn_lstm_seq_fwd``: the time loop in native code, per step
+          ``h_{t-1} @ W_hh^T`` for both LSTMs (one batched rocBLAS GEMM)
+          and the cell kernel (gates, cell, h; the activations are kept for
+          the backward pass);
+backward  ``vn_lstm_seq_bwd``: per step, in reverse, the backward cell
+          kernel (gate gradients dG_t, dc_{t-1}) and ``dh_{t-1} = dG_t @
+          W_hh`` (batched); then the weight gradients over all steps at
+          once: ``dW_hh = dG^T H_prev`` (batched), ``dW_ih = dG^T X``,
+          ``db = sum dG``.
 
-The GEMMs are library GEMMs (hipBLASLt through torch), f32 -- the
-reference's dtype; the per-step cell kernels are csrc/voxnav_learn.hip.
+The GEMMs are library GEMMs (rocBLAS in the loops, hipBLASLt through torch
+outside), f32 -- the reference's dtype; the cell kernels and the loops are
+csrc/voxnav_learn.hip.  The loops are native because issued from Python
+each step's two launches cost more host time than their GPU time.
 Padded steps sit after each sequence's real steps and get zero output
 gradient from the masked losses, so they never influence the real ones --
 the same result as sb3's per-step masked loop (a sequence only begins with
@@ -64,17 +68,8 @@ class _DualLSTM(torch.autograd.Function):
         hs[:, 0] = h0
         cs[:, 0] = c0
         act = torch.empty((L, 2, B, G), dtype=torch.float32, device=dev)   # step-major: act[t] contiguous
-        w_hh_t = w_hh.transpose(1, 2)
-        s_state = (L + 1) * B * H
-        row_bytes = B * 2 * G * 4
-        gx_base = gx.data_ptr()
-        hs_base, cs_base = hs.data_ptr(), cs.data_ptr()
-        for t in range(L):
-            torch.bmm(hs[:, t], w_hh_t, out=act[t])
-            _native.check(lib.vn_lstm_seq_fwd_cell(
-                C.c_void_p(gx_base + t * row_bytes), 2 * G, G, _p(act[t]), B * G, _p(bias),
-                C.c_void_p(cs_base + t * B * H * 4), C.c_void_p(cs_base + (t + 1) * B * H * 4),
-                C.c_void_p(hs_base + (t + 1) * B * H * 4), s_state, 2, B, H, st), "vn_lstm_seq_fwd_cell")
+        _native.check(lib.vn_lstm_seq_fwd(_p(gx), _p(w_hh), _p(bias), _p(hs), _p(cs), _p(act), 2, L, B, H, st),
+                      "vn_lstm_seq_fwd")
         ctx.save_for_backward(xf, w_ih_a, w_ih_c, w_hh, hs, cs, act)
         ctx.dims = (L, B, D, H)
         return hs[:, 1:]
@@ -91,16 +86,9 @@ class _DualLSTM(torch.autograd.Function):
         dG = torch.empty((2, L, B, G), dtype=torch.float32, device=dev)
         dc = torch.zeros((2, B, H), dtype=torch.float32, device=dev)
         dh = torch.empty((2, B, H), dtype=torch.float32, device=dev)
-        s_state = (L + 1) * B * H
-        cs_base, dG_base, do_base = cs.data_ptr(), dG.data_ptr(), dh_out.data_ptr()
         need_h0 = ctx.needs_input_grad[1]
-        for t in range(L - 1, -1, -1):
-            _native.check(lib.vn_lstm_seq_bwd_cell(
-                C.c_void_p(do_base + t * B * H * 4), L * B * H, _p(dh) if t < L - 1 else None, _p(dc),
-                _p(act[t]), B * G, C.c_void_p(cs_base + t * B * H * 4), C.c_void_p(cs_base + (t + 1) * B * H * 4),
-                s_state, C.c_void_p(dG_base + t * B * G * 4), L * B * G, 2, B, H, st), "vn_lstm_seq_bwd_cell")
-            if t > 0 or need_h0:
-                torch.bmm(dG[:, t], w_hh, out=dh)                   # dh_{t-1} = dG_t @ W_hh
+        _native.check(lib.vn_lstm_seq_bwd(_p(dh_out), _p(w_hh), _p(act), _p(cs), _p(dG), _p(dc), _p(dh),
+                                          1 if need_h0 else 0, 2, L, B, H, st), "vn_lstm_seq_bwd")
         dGf = dG.view(2, L * B, G)
         d_w_hh = torch.bmm(dGf.transpose(1, 2), hs[:, :L].reshape(2, L * B, H))
         d_w_ih_a = dGf[0].t() @ xf

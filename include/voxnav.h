@@ -311,6 +311,32 @@ int vn_lstm_seq_bwd_cell(const float *dh_out, int64_t dh_out_lstm_stride, const 
                          int64_t state_lstm_stride, float *dG, int64_t dG_lstm_stride, int32_t n_lstm, int32_t B,
                          int32_t H, void *stream);
 
+/*
+ * The whole forward time loop of n_lstm LSTMs over L steps (replaces the
+ * per-step Python loop of voxnav/lstm_seq.py; sb3_contrib
+ * RecurrentActorCriticPolicy._process_sequence as called by
+ * RecurrentPPO.train, reached from train/Grid_Train.py:228).  Per step t:
+ * act[t][l] = hs[l][t] @ W_hh[l]^T (rocBLAS, both LSTMs batched), then the
+ * forward cell step above (gx row stride n_lstm*4H, lstm stride 4H).
+ *   gx    [L*B][n_lstm*4H]      w_hh  [n_lstm][4H][H]     bias [n_lstm][4H]
+ *   hs, cs [n_lstm][L+1][B][H]  (index 0: the initial state, set by the caller)
+ *   act   [L][n_lstm][B][4H]    (out: the activations)
+ * rocBLAS is bound at run time (librocblas.so.5, the already-loaded copy when
+ * there is one); VN_ERR_HIP when it cannot be loaded.
+ */
+int vn_lstm_seq_fwd(const float *gx, const float *w_hh, const float *bias, float *hs, float *cs, float *act,
+                    int32_t n_lstm, int32_t L, int32_t B, int32_t H, void *stream);
+
+/*
+ * The backward time loop: for t = L-1 .. 0 the backward cell step (dh_out
+ * [n_lstm][L][B][H], dh_rec = dh from step t+1) into dG [n_lstm][L][B][4H],
+ * then dh = dG[:, t] @ W_hh (skipped at t = 0 unless need_dh0).  dc
+ * [n_lstm][B][H] must hold dL/dc_{L-1} (zeros) on entry and holds dL/dc0 on
+ * return; dh [n_lstm][B][H] holds dL/dh0 on return when need_dh0.
+ */
+int vn_lstm_seq_bwd(const float *dh_out, const float *w_hh, const float *act, const float *cs, float *dG, float *dc,
+                    float *dh, int32_t need_dh0, int32_t n_lstm, int32_t L, int32_t B, int32_t H, void *stream);
+
 #ifdef __cplusplus
 }
 #endif
