@@ -36,7 +36,7 @@ from typing import Tuple
 
 import torch
 
-from . import _native
+from . import _native, splitk
 
 
 def _p(t: torch.Tensor):
@@ -90,9 +90,10 @@ class _DualLSTM(torch.autograd.Function):
         _native.check(lib.vn_lstm_seq_bwd(_p(dh_out), _p(w_hh), _p(act), _p(cs), _p(dG), _p(dc), _p(dh),
                                           1 if need_h0 else 0, 2, L, B, H, st), "vn_lstm_seq_bwd")
         dGf = dG.view(2, L * B, G)
-        d_w_hh = torch.bmm(dGf.transpose(1, 2), hs[:, :L].reshape(2, L * B, H))
-        d_w_ih_a = dGf[0].t() @ xf
-        d_w_ih_c = dGf[1].t() @ xf
+        # dG^T H_prev, split over the samples (hs[l, :L] is a contiguous view)
+        d_w_hh = [splitk.mm_tn(dGf[k], hs[k, :L].reshape(L * B, H)) for k in range(2)]
+        d_w_ih_a = splitk.mm_tn(dGf[0], xf)
+        d_w_ih_c = splitk.mm_tn(dGf[1], xf)
         db = dGf.sum(1)
         dx = None
         if ctx.needs_input_grad[0]:

@@ -43,6 +43,7 @@ import numpy as np
 import torch
 import torch.nn.functional as Fn
 
+from . import splitk
 from .lstm_seq import dual_lstm
 from .policy import ActorCriticPolicy, RecurrentActorCriticPolicy
 
@@ -91,8 +92,9 @@ class PPOLearner:
 
     def _heads(self, lat_pi, lat_vf, actions):
         pol = self.policy
-        logits = pol.action_net(pol.mlp_extractor.policy_net(lat_pi))
-        values = pol.value_net(pol.mlp_extractor.value_net(lat_vf)).flatten()
+        # split-K weight gradients over the minibatch (voxnav/splitk.py)
+        logits = splitk.linear(splitk.sequential(pol.mlp_extractor.policy_net, lat_pi), pol.action_net)
+        values = splitk.linear(splitk.sequential(pol.mlp_extractor.value_net, lat_vf), pol.value_net).flatten()
         logp_all = torch.log_softmax(logits, dim=-1)
         log_prob = logp_all.gather(1, actions.view(-1, 1)).flatten()
         entropy = -(logp_all.exp() * logp_all).sum(-1)
