@@ -168,7 +168,7 @@ typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8_t;
 typedef __attribute__((ext_vector_type(16))) float f32x16_t;
 
 #ifndef VN_LF_ROWS
-#define VN_LF_ROWS 64   // 128 (8 waves, 1 block per CU at 154 VGPRs) measured 358 vs 336 us
+#define VN_LF_ROWS 64   // 96 / 128 / 192 rows measured 432 / 357 / 363 vs 347 us
 #endif
 constexpr int LF_ROWS = VN_LF_ROWS, LF_UNITS = 64;
 constexpr int LF_WAVES = (LF_ROWS / 32) * (LF_UNITS / 32), LF_T = 64 * LF_WAVES;   // threads per block
@@ -178,7 +178,8 @@ constexpr int LF_WAVES = (LF_ROWS / 32) * (LF_UNITS / 32), LF_T = 64 * LF_WAVES;
 constexpr int LF_KC = VN_LF_KC;           // K per chunk (bf16 elements)
 constexpr int LF_LDK = LF_KC + 8;         // LDS row pitch (+16 B against bank conflicts)
 constexpr int LF_GPR = LF_KC / 8;         // 16-byte groups per row and chunk
-constexpr int LF_NA = LF_ROWS * LF_GPR / LF_T, LF_NB = 4 * LF_UNITS * LF_GPR / LF_T;   // groups per thread
+constexpr int LF_BTOT = 4 * LF_UNITS * LF_GPR;    // 16-byte W groups per chunk
+constexpr int LF_NA = LF_ROWS * LF_GPR / LF_T, LF_NB = (LF_BTOT + LF_T - 1) / LF_T;   // groups per thread
 
 // gate nonlinearities of the bf16 path on the hardware exp / rcp (~1e-6
 // relative; the operands are bf16 already): 5 per (row, unit), 80 per lane
@@ -189,7 +190,7 @@ __device__ __forceinline__ float fast_tanh(float x) { return 2.0f * fast_sigm(2.
 #define VN_LF_RAW_BARRIER 1
 #endif
 #ifndef VN_LF_MIN_WAVES
-#define VN_LF_MIN_WAVES (LF_ROWS == 64 ? 3 : 1)   // blocks per CU the register budget is sized for
+#define VN_LF_MIN_WAVES 3   // waves per SIMD the register budget is sized for (12 per CU)
 #endif
 template <bool VEC_X>   // obs_dim % 8 == 0: branch-free staging loads
 #ifdef VN_LF_WPE
@@ -231,7 +232,7 @@ __global__ __launch_bounds__(LF_T, VN_LF_MIN_WAVES) LF_WPE_ATTR void lstm_fused_
     const uint16_t *wb = w + (size_t)b * 4 * H * Kp;
     const uint16_t *hb = hin + (size_t)b * N * H;
 
-    static_assert(LF_NA == 2 && (LF_NB == 8 || LF_NB == 4), "staging registers are spelled out for LF_KC = 64");
+    static_assert(LF_NA == 2 && LF_NB <= 8 && LF_ROWS * LF_GPR == 2 * LF_T, "staging registers are spelled out for LF_KC = 64");
     // raw staging registers: an A group is 8 obs floats (x columns) or 8 bf16
     // of h (in lo); it is converted when written to LDS, so no wait sits
     // between issuing the next chunk's loads and this chunk's MFMAs
@@ -266,17 +267,17 @@ __global__ __launch_bounds__(LF_T, VN_LF_MIN_WAVES) LF_WPE_ATTR void lstm_fused_
         }                                                                                                   \
     }
 #define LF_B(dst, i)                                                                                        \
-    {                                                                                                       \
+    if (LF_NB > (i)) {                                                                                      \
         const int gi_ = tid + LF_T * (i), lrow_ = gi_ / LF_GPR, gate_ = lrow_ / LF_UNITS;                   \
         const int uu_ = lrow_ - gate_ * LF_UNITS;                                                           \
-        dst = *reinterpret_cast<const uint4 *>(wb + (size_t)(gate_ * H + u_base + uu_) * Kp + k0_ +         \
-                                               (gi_ % LF_GPR) * 8);                                         \
+        if (LF_BTOT % LF_T == 0 || gi_ < LF_BTOT) /* wave-uniform */                                       \
+            dst = *reinterpret_cast<const uint4 *>(wb + (size_t)(gate_ * H + u_base + uu_) * Kp + k0_ +     \
+                                                   (gi_ % LF_GPR) * 8);                                     \
     }
 #define LF_LOAD_CHUNK(ch)                                                                                   \
     {                                                                                                       \
         const int k0_ = (ch) * LF_KC;                                                                       \
-        LF_B(rb0, 0) LF_B(rb1, 1) LF_B(rb2, 2) LF_B(rb3, 3)                                                 \
-        if (LF_NB > 4) { LF_B(rb4, 4) LF_B(rb5, 5) LF_B(rb6, 6) LF_B(rb7, 7) }                               \
+        LF_B(rb0, 0) LF_B(rb1, 1) LF_B(rb2, 2) LF_B(rb3, 3) LF_B(rb4, 4) LF_B(rb5, 5) LF_B(rb6, 6) LF_B(rb7, 7) \
         LF_A_LOAD(ra0lo, ra0hi, 0) LF_A_LOAD(ra1lo, ra1hi, 1)                                               \
     }
 #define LF_A_PUT(lo, hi, i)                                                                                 \
@@ -295,16 +296,17 @@ __global__ __launch_bounds__(LF_T, VN_LF_MIN_WAVES) LF_WPE_ATTR void lstm_fused_
         *reinterpret_cast<uint4 *>(&As[(gi_ / LF_GPR) * LF_LDK + (gi_ % LF_GPR) * 8]) = v_;                 \
     }
 #define LF_PUT(base, src, i)                                                                                \
-    {                                                                                                       \
+    if (LF_NB > (i)) {                                                                                      \
         const int gi_ = tid + LF_T * (i);                                                                    \
-        *reinterpret_cast<uint4 *>(&base[(gi_ / LF_GPR) * LF_LDK + (gi_ % LF_GPR) * 8]) = src;              \
+        if (LF_BTOT % LF_T == 0 || gi_ < LF_BTOT)                                                           \
+            *reinterpret_cast<uint4 *>(&base[(gi_ / LF_GPR) * LF_LDK + (gi_ % LF_GPR) * 8]) = src;          \
     }
 #define LF_STORE_CHUNK(ch)                                                                                   \
     {                                                                                                       \
         const int k0_ = (ch) * LF_KC;                                                                       \
         LF_A_PUT(ra0lo, ra0hi, 0) LF_A_PUT(ra1lo, ra1hi, 1)                                                 \
         LF_PUT(Bs, rb0, 0) LF_PUT(Bs, rb1, 1) LF_PUT(Bs, rb2, 2) LF_PUT(Bs, rb3, 3)                         \
-        if (LF_NB > 4) { LF_PUT(Bs, rb4, 4) LF_PUT(Bs, rb5, 5) LF_PUT(Bs, rb6, 6) LF_PUT(Bs, rb7, 7) }       \
+        LF_PUT(Bs, rb4, 4) LF_PUT(Bs, rb5, 5) LF_PUT(Bs, rb6, 6) LF_PUT(Bs, rb7, 7)                         \
     }
 
     f32x16_t acc[4];
