@@ -128,8 +128,10 @@ class GridAgent(EnvBase):
         print("-" * (self.width * 2))
 
 
-class SimpleGridAgent:
-    """``envs/simpleEnv.GridAgent`` (goal-seeking variant) on the HIP path.
+class SimpleGridAgent(EnvBase):
+    """``envs/simpleEnv.GridAgent`` (goal-seeking variant) on the HIP path;
+    a ``gymnasium.Env`` when gymnasium is importable, as the reference's
+    (envs/simpleEnv.py:13).
 
     Same constructor, spaces, ``reset`` (returns None, :79-107), ``step``
     (:109-150) and ``get_obs`` as the reference.  The reference's reset
