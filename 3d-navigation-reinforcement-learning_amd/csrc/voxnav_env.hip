@@ -1554,6 +1554,7 @@ __global__ __launch_bounds__(PCM ? VN_PC_BLOCK : BLOCK, PCM ? VN_PC_MIN_WAVES : 
 #endif
     uint32_t *wst = VN_STAGE_OBS ? stage + (threadIdx.x >> 6) * kStageWords : nullptr;   // this wave's staging block
     const int aslot = (threadIdx.x & 63) >> 2;
+    float abl_sink = 0.f;                             // VN_ABLATE 4096 (diagnostics)
 
     // Outputs of step k (the staged obs rows, reward, flags) are stored after
     // step k+1's loads are issued (DEFER): vmcnt retires in issue order, so
@@ -1894,7 +1895,15 @@ __global__ __launch_bounds__(PCM ? VN_PC_BLOCK : BLOCK, PCM ? VN_PC_MIN_WAVES : 
 #pragma unroll
                 for (int jj = 0; jj < (64 / GROUP) * (VN_OBS_DIM / 4) / 64; ++jj) {
                     const int f = lane + 64 * jj;
-                    if (f < nvalid) obs_store(dst4 + f, code_float4(wst[f], tab));
+                    if (VN_ABLATE & 2048u) {          // diagnostics: the stores without the LUT
+                        const uint32_t wb = wst[f];
+                        if (f < nvalid) obs_store(dst4 + f, make_float4(__uint_as_float(wb), 0.f, 0.f, 0.f));
+                    } else if (VN_ABLATE & 4096u) {   // diagnostics: the LUT without the stores
+                        const float4 v = code_float4(wst[f], tab);
+                        abl_sink += v.x + v.y + v.z + v.w;
+                    } else if (f < nvalid) {
+                        obs_store(dst4 + f, code_float4(wst[f], tab));
+                    }
                 }
             } else {
 #pragma unroll
@@ -1930,6 +1939,7 @@ __global__ __launch_bounds__(PCM ? VN_PC_BLOCK : BLOCK, PCM ? VN_PC_MIN_WAVES : 
             p.next_seed[i] = next_seed;
         }
     }
+    if ((VN_ABLATE & 4096u) && abl_sink == 12345.f) p.obs[0] = abl_sink;
 #if VN_ENV_PROF
     if (FAST && PC && (threadIdx.x & 63) == 0) {
         for (int k = 0; k < 7; ++k) atomicAdd(&g_env_prof[k], (unsigned long long)eprof[k]);
