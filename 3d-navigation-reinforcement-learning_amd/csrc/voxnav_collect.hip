@@ -600,6 +600,42 @@ __global__ __launch_bounds__(256) void bootstrap_kernel(const int32_t *__restric
     rew[a] = rew[a] + gv;
 }
 
+// The step's truncated agents appended to the rollout's bootstrap stash, so
+// the truncation bootstrap runs once per rollout (no per-step host read of the
+// count): row base[t] + j gets agent a = idx[j]'s terminal obs, its critic
+// state (h in h_bytes-byte elements, c f32) and the flat reward index
+// t * N + a; block 0 thread 0 sets base[t + 1] = base[t] + count.  Rows past
+// `cap` are dropped (the caller checks base[T] <= cap).  One wave per row.
+__global__ __launch_bounds__(256) void collect_stash_kernel(const int32_t *__restrict__ idx,
+                                                            const int32_t *__restrict__ count,
+                                                            const int32_t *__restrict__ base_in,
+                                                            int32_t *__restrict__ base_out, int t, int N,
+                                                            const float *__restrict__ tobs, int obs_dim,
+                                                            const uint8_t *__restrict__ h, int h_bytes,
+                                                            const float *__restrict__ c, int H,
+                                                            float *__restrict__ st_obs, uint8_t *__restrict__ st_h,
+                                                            float *__restrict__ st_c, int32_t *__restrict__ st_flat,
+                                                            int cap) {
+    const int cnt = *count, base = *base_in;
+    if (blockIdx.x == 0 && threadIdx.x == 0) *base_out = base + cnt;
+    const int lane = threadIdx.x & 63;
+    const int nw = (int)(gridDim.x * blockDim.x) >> 6;
+    for (int j = (int)((blockIdx.x * blockDim.x + threadIdx.x) >> 6); j < cnt; j += nw) {
+        const int r = base + j;
+        if (r >= cap) break;
+        const int a = idx[j];
+        if (lane == 0) st_flat[r] = t * N + a;
+        for (int k = lane; k < obs_dim; k += 64) st_obs[(size_t)r * obs_dim + k] = tobs[(size_t)a * obs_dim + k];
+        if (h) {
+            const int hw = H * h_bytes / 4;          // 32-bit words of a row
+            const uint32_t *hs = reinterpret_cast<const uint32_t *>(h) + (size_t)a * hw;
+            uint32_t *hd = reinterpret_cast<uint32_t *>(st_h) + (size_t)r * hw;
+            for (int k = lane; k < hw; k += 64) hd[k] = hs[k];
+            for (int k = lane; k < H; k += 64) st_c[(size_t)r * H + k] = c[(size_t)a * H + k];
+        }
+    }
+}
+
 // episode_starts[n] = done; (h, c)[b][n][:] = 0 for done agents
 // (RecurrentActorCriticPolicy._process_sequence masks the state with
 // (1 - episode_start) before the next LSTM step).
@@ -766,6 +802,24 @@ int vn_collect_compact(const uint8_t *terminated, const uint8_t *truncated, int3
         return fail(VN_ERR_INVALID, "terminated / truncated must be 16-byte aligned");
     hipLaunchKernelGGL(boot_compact_kernel, dim3(1), dim3(1024), 0, (hipStream_t)stream, terminated, truncated,
                        (int)N, boot_idx, boot_count);
+    VN_HIP(hipGetLastError());
+    return VN_OK;
+}
+
+int vn_collect_stash(const int32_t *boot_idx, const int32_t *boot_count, const int32_t *base_in, int32_t *base_out,
+                     int32_t t, int32_t N, const float *terminal_obs, int32_t obs_dim, const void *h_critic,
+                     int32_t h_bytes, const float *c_critic, int32_t H, float *stash_obs, void *stash_h,
+                     float *stash_c, int32_t *stash_flat, int32_t cap, void *stream) {
+    if (!boot_idx || !boot_count || !base_in || !base_out || !terminal_obs || !stash_obs || !stash_flat)
+        return fail(VN_ERR_INVALID, "NULL argument");
+    if (N < 1 || t < 0 || obs_dim < 1 || cap < 0) return fail(VN_ERR_INVALID, "bad sizes N=%d t=%d obs_dim=%d", N, t, obs_dim);
+    if (h_critic && (!c_critic || !stash_h || !stash_c || H < 1 || (h_bytes != 2 && h_bytes != 4) || (H * h_bytes) % 4))
+        return fail(VN_ERR_INVALID, "critic state: c, stash rows, H and h_bytes (2 or 4) required");
+    if ((int64_t)t * N + N > 0x7fffffff) return fail(VN_ERR_INVALID, "t * N overflows the flat index");
+    hipLaunchKernelGGL(collect_stash_kernel, dim3(256), dim3(256), 0, (hipStream_t)stream, boot_idx, boot_count,
+                       base_in, base_out, (int)t, (int)N, terminal_obs, (int)obs_dim,
+                       reinterpret_cast<const uint8_t *>(h_critic), (int)h_bytes, c_critic, (int)H, stash_obs,
+                       reinterpret_cast<uint8_t *>(stash_h), stash_c, stash_flat, (int)cap);
     VN_HIP(hipGetLastError());
     return VN_OK;
 }

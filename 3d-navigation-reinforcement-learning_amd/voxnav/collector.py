@@ -4,7 +4,7 @@ Restates sb3_contrib ``RecurrentPPO.collect_rollouts`` (and SB3
 ``OnPolicyAlgorithm.collect_rollouts`` for the feed-forward policy), which
 train/Grid_Train.py reaches through ``model.learn`` (:228) with
 ``n_steps=2048, gamma=0.99, gae_lambda=0.95`` (:84-85), for N agents on one
-GPU with nothing crossing PCIe per step except one 4-byte count:
+GPU with nothing crossing PCIe per step (one 4-byte count per rollout):
 
 per step t
   1. policy forward on obs[t] (states already zeroed for agents whose
@@ -15,16 +15,19 @@ per step t
   2. ``BatchedGridEnv.step_into`` -> obs[t+1], reward[t], terminated,
      truncated, terminal_obs (SB3 auto-reset inside the env kernel)
   3. ``vn_collect_compact`` -> ordered indices of the truncated agents
-     (SB3: ``done and info["TimeLimit.truncated"]``); their terminal values
-     V(terminal_obs; critic state after step t) are computed on the gathered
-     rows and added as ``reward += gamma * V`` (``vn_collect_bootstrap``)
+     (SB3: ``done and info["TimeLimit.truncated"]``); ``vn_collect_stash``
+     appends their terminal obs and critic state after step t to a device
+     stash (the count never leaves the GPU)
   4. ``vn_episode_start`` -> episode_starts[t+1] = done, zero the (h, c) of
      those agents (``_process_sequence``'s ``(1 - episode_start)`` mask)
 
   5. ``vn_monitor_step`` -> the SB3 Monitor's per-agent episode return
      (f64) / length and the episodes that ended at step t (voxnav.monitor)
 
-after T steps: V(obs[T]) under the current critic states, then the GAE scan
+after T steps: the stashed terminal values V(terminal_obs; critic state)
+in one batch (equal to the per-step values up to the GEMMs' rounding), added
+as ``rewards[t, a] += gamma * V`` (``vn_collect_bootstrap``); V(obs[T])
+under the current critic states; then the GAE scan
 (``vn_gae``) -> advantages, returns; the finished episodes go to
 ``monitor.ep_info_buffer`` (``ep_rew_mean`` / ``ep_len_mean``).
 
@@ -41,6 +44,7 @@ independent of how agents are sharded over GPUs.
 from __future__ import annotations
 
 import ctypes as C
+import numpy as np
 from dataclasses import dataclass
 from typing import Optional
 
@@ -176,7 +180,6 @@ class RolloutCollector:
         self._tobs = z(N, env.obs_dim)
         self._boot_idx = z(N, dt=torch.int32)
         self._boot_cnt = z(1, dt=torch.int32)
-        self._boot_cnt_host = torch.zeros(1, dtype=torch.int32, pin_memory=True)
         self._last_values = z(N)
         self.recurrent = self.w.recurrent
         if self.recurrent:
@@ -191,6 +194,20 @@ class RolloutCollector:
             self.store = bool(store_lstm_states)
             self._hs = z(T + 1, 2, N, H) if self.store else None
             self._cs = z(T + 1, 2, N, H) if self.store else None
+        # truncation bootstrap stash (vn_collect_stash): the truncated agents'
+        # terminal obs and critic state, appended on the device each step and
+        # bootstrapped once per rollout.  An episode truncates when its step
+        # count reaches the room's free-cell count, so an agent truncates at
+        # most (T - 1) // min_free + 1 times per rollout.
+        fmin = max(1, int(np.min(env.total_free_cells)))
+        self._stash_cap = N * ((T - 1) // fmin + 1)
+        cap = self._stash_cap
+        self._stash_base = z(T + 1, dt=torch.int32)
+        self._stash_obs = z(cap, env.obs_dim)
+        self._stash_flat = z(cap, dt=torch.int32)
+        if self.recurrent:
+            self._stash_h = z(cap, self.w.H, dt=torch.bfloat16 if self.fused else torch.float32)
+            self._stash_c = z(cap, self.w.H)
         # SB3 Monitor on every worker (train/Grid_Train.py:125): it sums the env's
         # f64 rewards, so the env step also writes them (voxnav.monitor)
         self.monitor = EpisodeMonitor(self.lib, N, T, dev) if monitor else None
@@ -308,6 +325,10 @@ class RolloutCollector:
         mon = self.monitor
         if mon is not None:
             mon.begin()
+        self._stash_base.zero_()
+        sb = self._stash_base
+        rec = self.recurrent
+        hsrc = (self.h_bf if self.fused else self.h) if rec else None
         for t in range(T):
             self._forward(self._obs[t], t)
             self.env.step_into(self.actions[t], self._obs[t + 1], self.rewards[t], self._term, self._trunc,
@@ -316,20 +337,14 @@ class RolloutCollector:
                 mon.step(t, self._term, self._trunc, reward64=self._r64)
             _native.check(lib.vn_collect_compact(_p(self._term), _p(self._trunc), N, _p(self._boot_idx),
                                                  _p(self._boot_cnt), s()), "vn_collect_compact")
-            self._boot_cnt_host.copy_(self._boot_cnt, non_blocking=True)
-            torch.cuda.current_stream(self.device).synchronize()
-            M = int(self._boot_cnt_host[0])
-            if M:
-                idx = self._boot_idx[:M].long()
-                tv = torch.empty(M, dtype=torch.float32, device=self.device)
-                if self.recurrent:
-                    hsrc = self.h_bf if self.fused else self.h
-                    self._critic(self._tobs.index_select(0, idx), hsrc[1].index_select(0, idx),
-                                 self.c[1].index_select(0, idx), tv)
-                else:
-                    self._critic(self._tobs.index_select(0, idx), None, None, tv)
-                _native.check(lib.vn_collect_bootstrap(_p(self._boot_idx), _p(tv), M, self.gamma,
-                                                       _p(self.rewards[t]), s()), "vn_collect_bootstrap")
+            # the truncated agents' terminal obs and critic state (before the
+            # episode-start mask below) into the stash; no host read here
+            _native.check(lib.vn_collect_stash(
+                _p(self._boot_idx), _p(self._boot_cnt), _p(sb[t]), _p(sb[t + 1]), t, N, _p(self._tobs),
+                self.env.obs_dim, _p(hsrc[1]) if rec else None, hsrc.element_size() if rec else 0,
+                _p(self.c[1]) if rec else None, self.w.H if rec else 0, _p(self._stash_obs),
+                _p(self._stash_h) if rec else None, _p(self._stash_c) if rec else None, _p(self._stash_flat),
+                self._stash_cap, s()), "vn_collect_stash")
             _native.check(lib.vn_episode_start(_p(self._term), _p(self._trunc), N, _p(self._starts[t + 1]),
                                                _p(self.h) if self.recurrent else None,
                                                _p(self.c) if self.recurrent else None,
@@ -337,6 +352,19 @@ class RolloutCollector:
                                                2 if self.recurrent else 0, self.w.H if self.recurrent else 0, s()),
                           "vn_episode_start")
             self.t_global += 1
+        # the truncation bootstrap of the whole rollout: V(terminal obs) from the
+        # stashed critic states, rewards[t, a] += gamma * V (one host read)
+        M = int(sb[T].item())
+        if M > self._stash_cap:
+            raise RuntimeError(f"bootstrap stash overflow: {M} > {self._stash_cap}")
+        if M:
+            tv = torch.empty(M, dtype=torch.float32, device=self.device)
+            if rec:
+                self._critic(self._stash_obs[:M], self._stash_h[:M], self._stash_c[:M], tv)
+            else:
+                self._critic(self._stash_obs[:M], None, None, tv)
+            _native.check(lib.vn_collect_bootstrap(_p(self._stash_flat), _p(tv), M, self.gamma, _p(self.rewards),
+                                                   s()), "vn_collect_bootstrap")
         # V(last obs) under the current (masked) critic state
         if self.recurrent:
             hsrc = self.h_bf if self.fused else self.h

@@ -248,6 +248,24 @@ int vn_collect_compact(const uint8_t *terminated, const uint8_t *truncated, int3
                        int32_t *boot_count, void *stream);
 
 /*
+ * Append the step's truncated agents (boot_idx / boot_count from
+ * vn_collect_compact, device) to the rollout's bootstrap stash, so the
+ * bootstrap values are computed once per rollout instead of after a host
+ * read of the count every step (collect_rollouts' TimeLimit.truncated loop):
+ * stash row base_in[0] + j takes agent a = boot_idx[j]'s terminal obs
+ * (f32 [obs_dim]), its critic LSTM state (h_critic rows of H elements of
+ * h_bytes = 2 (bf16) or 4 (f32) bytes, c_critic f32 rows; h_critic NULL: no
+ * state) and the flat reward index t*N + a; base_out[0] = base_in[0] +
+ * count (device i32).  Rows at or past cap are dropped: check the final
+ * base <= cap.  Then vn_collect_bootstrap(stash_flat, values, M, gamma,
+ * rewards [T][N]) applies them.
+ */
+int vn_collect_stash(const int32_t *boot_idx, const int32_t *boot_count, const int32_t *base_in, int32_t *base_out,
+                     int32_t t, int32_t N, const float *terminal_obs, int32_t obs_dim, const void *h_critic,
+                     int32_t h_bytes, const float *c_critic, int32_t H, float *stash_obs, void *stash_h,
+                     float *stash_c, int32_t *stash_flat, int32_t cap, void *stream);
+
+/*
  * Truncation bootstrap: rewards[boot_idx[i]] += gamma * terminal_values[i]
  * for i < M (f32, two roundings, as collect_rollouts' numpy update).
  */
