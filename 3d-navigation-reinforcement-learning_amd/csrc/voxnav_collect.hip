@@ -192,7 +192,7 @@ __device__ __forceinline__ float fast_tanh(float x) { return 2.0f * fast_sigm(2.
 #ifndef VN_LF_MIN_WAVES
 #define VN_LF_MIN_WAVES 3   // waves per SIMD the register budget is sized for (12 per CU)
 #endif
-template <bool VEC_X>   // obs_dim % 8 == 0: branch-free staging loads
+template <bool VEC_X, bool MASK>   // obs_dim % 8 == 0: branch-free staging loads; MASK: episode-start mask on c_in
 #ifdef VN_LF_WPE
 #define LF_WPE_ATTR __attribute__((amdgpu_waves_per_eu(VN_LF_WPE, VN_LF_WPE)))
 #else
@@ -200,9 +200,11 @@ template <bool VEC_X>   // obs_dim % 8 == 0: branch-free staging loads
 #endif
 __global__ __launch_bounds__(LF_T, VN_LF_MIN_WAVES) LF_WPE_ATTR void lstm_fused_bf16_kernel(
     const float *__restrict__ x, int obs_dim, int kx, const uint16_t *__restrict__ hin,
-    const uint16_t *__restrict__ w, int Kp, const float *__restrict__ bias, float *__restrict__ c,
-    uint16_t *__restrict__ hout, float *__restrict__ h32, float *__restrict__ h_store, float *__restrict__ c_store,
-    int N, int H, int ncombo) {
+    // c_in and c are the same array on the in/out entry: each lane loads its
+    // 16 states before any store, and a state's store depends on its load
+    const uint16_t *__restrict__ w, int Kp, const float *__restrict__ bias, const float *__restrict__ c_in,
+    const float *__restrict__ start, float *__restrict__ c, uint16_t *__restrict__ hout, float *__restrict__ h32,
+    float *__restrict__ h_store, float *__restrict__ c_store, int N, int H, int ncombo) {
     // one LDS buffer; the next chunk is prefetched into registers during
     // the current chunk's MFMAs
     __shared__ __attribute__((aligned(16))) uint16_t lds[(LF_ROWS + 4 * LF_UNITS) * LF_LDK];
@@ -370,7 +372,8 @@ __global__ __launch_bounds__(LF_T, VN_LF_MIN_WAVES) LF_WPE_ATTR void lstm_fused_
 #pragma unroll
     for (int reg = 0; reg < 16; ++reg) {
         const int n = min(n_base + wr + (reg & 3) + 8 * (reg >> 2) + 4 * (lane >> 5), N - 1);
-        cin[reg] = c[((size_t)b * N + n) * H + u];
+        const float v = c_in[((size_t)b * N + n) * H + u];
+        cin[reg] = (MASK && start[n] != 0.0f) ? 0.0f : v;   // the episode-start mask, applied on read
     }
     const float *bb = bias + (size_t)b * 4 * H;
     const float bi = bb[u], bf = bb[H + u], bg = bb[2 * H + u], bo = bb[3 * H + u];
@@ -754,10 +757,12 @@ int vn_lstm_cell_bf16(const uint16_t *gx, int64_t gx_row_stride, const uint16_t 
                                       H, stream);
 }
 
-int vn_lstm_fused_bf16(const float *x, int32_t obs_dim, const uint16_t *h_in, const uint16_t *w_cat, int32_t Kp,
-                       const float *bias, float *c, uint16_t *h_out, float *h32, float *h_store, float *c_store,
-                       int32_t n_lstm, int32_t N, int32_t H, void *stream) {
-    if (!x || !h_in || !w_cat || !bias || !c || !h_out) return fail(VN_ERR_INVALID, "NULL argument");
+namespace {
+int lstm_fused_launch(const float *x, int32_t obs_dim, const uint16_t *h_in, const uint16_t *w_cat, int32_t Kp,
+                      const float *bias, const float *c_in, const float *start, float *c, uint16_t *h_out,
+                      float *h32, float *h_store, float *c_store, int32_t n_lstm, int32_t N, int32_t H,
+                      void *stream) {
+    if (!x || !h_in || !w_cat || !bias || !c_in || !c || !h_out) return fail(VN_ERR_INVALID, "NULL argument");
     if (h_in == h_out) return fail(VN_ERR_INVALID, "h_in and h_out must differ (other blocks read h_in)");
     const int kx = (obs_dim + 7) & ~7;
     if (n_lstm < 1 || N < 1 || obs_dim < 1 || H < 64 || (H % LF_UNITS) || (Kp % LF_KC) || Kp < kx + H)
@@ -766,14 +771,36 @@ int vn_lstm_fused_bf16(const float *x, int32_t obs_dim, const uint16_t *h_in, co
     // one block per (row tile, combo = LSTM x 64-unit block)
     const int ncombo = n_lstm * (H / LF_UNITS);
     const dim3 grid((unsigned)((N + LF_ROWS - 1) / LF_ROWS) * (unsigned)ncombo);
-    if ((obs_dim & 7) == 0)
-        hipLaunchKernelGGL(lstm_fused_bf16_kernel<true>, grid, dim3(LF_T), 0, (hipStream_t)stream, x, (int)obs_dim,
-                           kx, h_in, w_cat, (int)Kp, bias, c, h_out, h32, h_store, c_store, (int)N, (int)H, ncombo);
-    else
-        hipLaunchKernelGGL(lstm_fused_bf16_kernel<false>, grid, dim3(LF_T), 0, (hipStream_t)stream, x, (int)obs_dim,
-                           kx, h_in, w_cat, (int)Kp, bias, c, h_out, h32, h_store, c_store, (int)N, (int)H, ncombo);
+#define VN_LF_LAUNCH(VX, MK)                                                                                \
+    hipLaunchKernelGGL((lstm_fused_bf16_kernel<VX, MK>), grid, dim3(LF_T), 0, (hipStream_t)stream, x,           \
+                       (int)obs_dim, kx, h_in, w_cat, (int)Kp, bias, c_in, start, c, h_out, h32, h_store, c_store, \
+                       (int)N, (int)H, ncombo)
+    if ((obs_dim & 7) == 0) {
+        if (start) VN_LF_LAUNCH(true, true);
+        else VN_LF_LAUNCH(true, false);
+    } else {
+        if (start) VN_LF_LAUNCH(false, true);
+        else VN_LF_LAUNCH(false, false);
+    }
+#undef VN_LF_LAUNCH
     VN_HIP(hipGetLastError());
     return VN_OK;
+}
+}  // namespace
+
+int vn_lstm_fused_bf16(const float *x, int32_t obs_dim, const uint16_t *h_in, const uint16_t *w_cat, int32_t Kp,
+                       const float *bias, float *c, uint16_t *h_out, float *h32, float *h_store, float *c_store,
+                       int32_t n_lstm, int32_t N, int32_t H, void *stream) {
+    return lstm_fused_launch(x, obs_dim, h_in, w_cat, Kp, bias, c, nullptr, c, h_out, h32, h_store, c_store, n_lstm,
+                             N, H, stream);
+}
+
+int vn_lstm_fused_bf16_masked(const float *x, int32_t obs_dim, const uint16_t *h_in, const uint16_t *w_cat,
+                              int32_t Kp, const float *bias, const float *c_in, const float *start, float *c_out,
+                              uint16_t *h_out, float *h_store, int32_t n_lstm, int32_t N, int32_t H, void *stream) {
+    if (c_in == c_out) return fail(VN_ERR_INVALID, "c_in and c_out must differ");
+    return lstm_fused_launch(x, obs_dim, h_in, w_cat, Kp, bias, c_in, start, c_out, h_out, nullptr, h_store, nullptr,
+                             n_lstm, N, H, stream);
 }
 
 

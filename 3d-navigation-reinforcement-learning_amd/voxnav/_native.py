@@ -75,6 +75,8 @@ _SIGS = {
                                       C.c_int64, C.c_int32, P, P, P, P]),
     "vn_lstm_fused_bf16": (C.c_int, [P, C.c_int32, P, P, C.c_int32, P, P, P, P, P, P, C.c_int32, C.c_int32,
                                      C.c_int32, P]),
+    "vn_lstm_fused_bf16_masked": (C.c_int, [P, C.c_int32, P, P, C.c_int32, P, P, P, P, P, P, C.c_int32, C.c_int32,
+                                            C.c_int32, P]),
     "vn_collect_compact": (C.c_int, [P, P, C.c_int32, P, P, P]),
     "vn_collect_bootstrap": (C.c_int, [P, P, C.c_int32, C.c_double, P, P]),
     "vn_collect_stash": (C.c_int, [P, P, P, P, C.c_int32, C.c_int32, P, C.c_int32, P, C.c_int32, P, C.c_int32, P, P,
@@ -91,8 +93,10 @@ _SIGS = {
 EXPORTED_SYMBOLS = tuple(_SIGS)
 
 
-def _bind(lib):
+def _bind(lib, strict: bool = True):
     for name, (res, args) in _SIGS.items():
+        if not strict and not hasattr(lib, name):
+            continue                      # an older A/B build without this entry point
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
@@ -104,7 +108,7 @@ def _bind(lib):
 def load_variant(path):
     """Load another build of the library (A/B benchmarking); separate handle."""
     import torch  # noqa: F401
-    return _bind(C.CDLL(str(path)))
+    return _bind(C.CDLL(str(path)), strict=False)
 
 
 def load(build_if_missing: bool = True):

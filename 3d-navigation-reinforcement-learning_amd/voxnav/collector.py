@@ -248,19 +248,33 @@ class RolloutCollector:
                                                   _p(w.bias[b0:b0 + nl]), _p(c), _p(h_out), None, _p(hs), _p(cs), nl,
                                                   M, w.H, self._stream()), "vn_lstm_fused_bf16")
 
+    def _fused_rollout(self, obs, t):
+        """The fused step inside collect(): c read from the buffer's lstm_c[t]
+        (the episode-start mask applied on read; step 0 reads the current,
+        already masked state) and written only to lstm_c[t+1]."""
+        w = self.w
+        c_in, start = (self.c, None) if t == 0 else (self._cs[t], self._starts[t])
+        _native.check(self.lib.vn_lstm_fused_bf16_masked(_p(obs), obs.shape[1], _p(self.h_bf), _p(w.w_cat), w.Kp,
+                                                         _p(w.bias), _p(c_in), _p(start), _p(self._cs[t + 1]),
+                                                         _p(self.h_bf2), _p(self._hs[t + 1]), 2, self.N, w.H,
+                                                         self._stream()), "vn_lstm_fused_bf16_masked")
+
     def hidden_state(self):
         """(h, c) f32 [2, N, H] of the (actor, critic) LSTMs after the last step
         (h from its bf16 copy on the fused bf16 path)."""
         h = self.h_bf.float() if self.fused else self.h
         return h, self.c
 
-    def _forward(self, obs: torch.Tensor, t: int):
+    def _forward(self, obs: torch.Tensor, t: int, in_rollout: bool = False):
         """Policy step on obs [N, 80] into actions/values/log_probs[t]."""
         w, N = self.w, self.N
         if self.recurrent and self.fused:
-            hs = self._hs[t + 1] if self.store else None
-            cs = self._cs[t + 1] if self.store else None
-            self._fused(obs, self.h_bf, self.c, self.h_bf2, hs, cs, 2, N, 0)
+            if in_rollout and self.store:
+                self._fused_rollout(obs, t)
+            else:
+                hs = self._hs[t + 1] if self.store else None
+                cs = self._cs[t + 1] if self.store else None
+                self._fused(obs, self.h_bf, self.c, self.h_bf2, hs, cs, 2, N, 0)
             self.h_bf, self.h_bf2 = self.h_bf2, self.h_bf
             lat_pi = _mlp(w.pi, self.h_bf[0])
             lat_vf = _mlp(w.vf, self.h_bf[1])
@@ -328,9 +342,11 @@ class RolloutCollector:
         self._stash_base.zero_()
         sb = self._stash_base
         rec = self.recurrent
-        hsrc = (self.h_bf if self.fused else self.h) if rec else None
+        # fused bf16 step with the buffer: the cell state lives in lstm_c only
+        # (vn_lstm_fused_bf16_masked); self.c is brought up to date after T
+        csbuf = rec and self.fused and self.store
         for t in range(T):
-            self._forward(self._obs[t], t)
+            self._forward(self._obs[t], t, in_rollout=True)
             self.env.step_into(self.actions[t], self._obs[t + 1], self.rewards[t], self._term, self._trunc,
                                self._tobs, reward64=self._r64)
             if mon is not None:
@@ -338,11 +354,14 @@ class RolloutCollector:
             _native.check(lib.vn_collect_compact(_p(self._term), _p(self._trunc), N, _p(self._boot_idx),
                                                  _p(self._boot_cnt), s()), "vn_collect_compact")
             # the truncated agents' terminal obs and critic state (before the
-            # episode-start mask below) into the stash; no host read here
+            # episode-start mask below) into the stash; no host read here.  The
+            # fused path's h_bf is a ping-pong pair: read it after this step's swap
+            hsrc = (self.h_bf if self.fused else self.h) if rec else None
             _native.check(lib.vn_collect_stash(
                 _p(self._boot_idx), _p(self._boot_cnt), _p(sb[t]), _p(sb[t + 1]), t, N, _p(self._tobs),
                 self.env.obs_dim, _p(hsrc[1]) if rec else None, hsrc.element_size() if rec else 0,
-                _p(self.c[1]) if rec else None, self.w.H if rec else 0, _p(self._stash_obs),
+                _p(self._cs[t + 1][1] if csbuf else self.c[1]) if rec else None, self.w.H if rec else 0,
+                _p(self._stash_obs),
                 _p(self._stash_h) if rec else None, _p(self._stash_c) if rec else None, _p(self._stash_flat),
                 self._stash_cap, s()), "vn_collect_stash")
             _native.check(lib.vn_episode_start(_p(self._term), _p(self._trunc), N, _p(self._starts[t + 1]),
@@ -352,6 +371,8 @@ class RolloutCollector:
                                                2 if self.recurrent else 0, self.w.H if self.recurrent else 0, s()),
                           "vn_episode_start")
             self.t_global += 1
+        if csbuf:   # the current (masked) state: lstm_c[T] with the episode-start mask
+            self.c.copy_(torch.where(self._starts[T][None, :, None] != 0, 0.0, self._cs[T]))
         # the truncation bootstrap of the whole rollout: V(terminal obs) from the
         # stashed critic states, rewards[t, a] += gamma * V (one host read)
         M = int(sb[T].item())

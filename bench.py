@@ -15,9 +15,10 @@ One "step" = one batched env step of all agents on the GPU.  The headline
 resets a fresh env, runs exactly ``--warmup`` untimed steps, then times
 exactly ``--steps`` steps (launches of ``--fuse`` F steps into a [F, N, 80]
 rollout-chunk buffer; the last launch of each phase takes the remainder).
-F = 64 by default: a 64-step rollout chunk per launch (the reference's
-rollouts are n_steps = 2048 per env, train/Grid_Train.py:84); the same
-window at F = 16 is reported beside it (``same_window_other_fuse``).
+F = 128 by default: a 128-step rollout chunk per launch (the collector's
+n_steps; the reference's rollouts are n_steps = 2048 per env,
+train/Grid_Train.py:84); the same window at F = 16 is reported beside it
+(``same_window_other_fuse``).
 ``roofline`` is computed from the same timed launches (HIP events on the
 launch stream) and ``traffic`` from the PMC record of the same window
 (profiles/pmc_traffic.json, keyed by room/L/N/F/warmup/steps).  When the
@@ -65,7 +66,7 @@ def parse(argv=None):
     ap.add_argument("--agents", type=int, default=65536, help="agents per GPU")
     ap.add_argument("--room", default="32x32x8", help="WxDxH of the walled-box room")
     ap.add_argument("--L", type=int, default=10, help="local_map_length")
-    ap.add_argument("--fuse", type=int, default=64,
+    ap.add_argument("--fuse", type=int, default=128,
                     help="env steps per kernel launch (headline): one launch fills a [F, N, 80] rollout chunk")
     ap.add_argument("--fuse-check", type=int, default=16,
                     help="also time the same window at this many steps per launch (0 = skip)")
@@ -450,7 +451,7 @@ def roofline_block(bstep, N, F, steps, timed, kern_ms, traffic_rec, kernel_label
     return roof
 
 
-def traffic_for(W, D, H, L, N, F, warmup, steps):
+def traffic_for(W, D, H, L, N, F, warmup, steps, prefix=""):
     prof = REPO / "profiles" / "pmc_traffic.json"
     if not prof.exists():
         return None
@@ -458,7 +459,7 @@ def traffic_for(W, D, H, L, N, F, warmup, steps):
         pm = json.loads(prof.read_text())
     except ValueError:
         return None
-    return pm.get(f"{W}x{D}x{H}_L{L}_N{N}_F{F}_W{warmup}_K{steps}")
+    return pm.get(f"{prefix}{W}x{D}x{H}_L{L}_N{N}_F{F}_W{warmup}_K{steps}")
 
 
 # ---------------------------------------------------------------- main
@@ -595,6 +596,12 @@ def main():
                   "kernel": senv.kernel_label(F),
                   "roofline": {"bound": "hbm", "achieved": round(sach, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                                "frac": round(sach / HBM_PEAK_GBS, 5), "algorithmic_bytes_per_env_step": sb}}
+        strf = traffic_for(W, D, H, 4, N, F, 32, st_steps, prefix="simple_")
+        simple["roofline"]["traffic"] = strf["hbm_bytes_per_launch"] if strf else None
+        if strf:
+            simple["roofline"]["traffic_bytes_per_env_step"] = round(
+                strf["read_bytes_per_env_step"] + strf["write_bytes_per_env_step"], 1)
+            simple["roofline"]["traffic_source"] = strf["source"]
         senv.close()
         del senv
 

@@ -218,6 +218,23 @@ int vn_lstm_fused_bf16(const float *x, int32_t obs_dim, const uint16_t *h_in, co
                        int32_t n_lstm, int32_t N, int32_t H, void *stream);
 
 /*
+ * vn_lstm_fused_bf16 inside a rollout (RolloutCollector.collect): the cell
+ * state is read from the rollout buffer's previous slot and written only to
+ * the next one, so no separate state array is rewritten every step.
+ *   c_in   f32 [n_lstm][N][H]: the state entering the step BEFORE the
+ *          episode-start mask (the buffer's lstm_c[t]); rows n with
+ *          start[n] != 0 are read as zero (RecurrentActorCriticPolicy.
+ *          _process_sequence's (1 - episode_start) mask); start f32 [N] or
+ *          NULL (no mask)
+ *   c_out  f32 [n_lstm][N][H], != c_in: the new state (lstm_c[t+1])
+ *   h_store f32 or NULL: the new h (lstm_h[t+1])
+ * Other arguments as vn_lstm_fused_bf16.
+ */
+int vn_lstm_fused_bf16_masked(const float *x, int32_t obs_dim, const uint16_t *h_in, const uint16_t *w_cat,
+                              int32_t Kp, const float *bias, const float *c_in, const float *start, float *c_out,
+                              uint16_t *h_out, float *h_store, int32_t n_lstm, int32_t N, int32_t H, void *stream);
+
+/*
  * Action and value heads + Categorical draw (ActorCriticPolicy action_net /
  * value_net and distribution.get_actions / log_prob).
  *   latent_pi [N][P] (NULL: value only), latent_vf [N][P] (NULL: no value)

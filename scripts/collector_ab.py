@@ -1,0 +1,51 @@
+#!/usr/bin/env python3
+"""Same-process A/B of the bf16 PPO-LSTM collector (BASELINE C4: 65,536
+agents, P3_training, T=128): the rollout's fused LSTM step through
+vn_lstm_fused_bf16_masked (c read from lstm_c[t] with the episode-start mask,
+written only to lstm_c[t+1]) vs the in/out entry vn_lstm_fused_bf16 (c read
+and rewritten, plus the lstm_c[t+1] copy).  Timing only: the B variant skips
+the masked entry's bookkeeping, so its buffers are not a valid rollout."""
+import sys
+import time
+from pathlib import Path
+
+REPO = Path(__file__).resolve().parent.parent
+sys.path.insert(0, str(REPO / "3d-navigation-reinforcement-learning_amd"))
+sys.path.insert(0, str(REPO))
+import torch  # noqa: E402
+
+
+def main():
+    from voxnav.collector import RolloutCollector
+    from voxnav.env import BatchedGridEnv
+    from voxnav.policy import RecurrentActorCriticPolicy
+    from voxnav.rooms import load_archive_set
+    dev = "cuda:0"
+    N, T = 65536, 128
+    torch.manual_seed(42)
+    pol = RecurrentActorCriticPolicy().to(dev)
+    env = BatchedGridEnv(num_agents=N, rooms=load_archive_set("P3_training"), local_map_length=10, autoreset=True,
+                         device=dev)
+    col = RolloutCollector(env, pol, n_steps=T, sample_seed=42, reset_seed=42, policy_dtype="bf16")
+    masked = col._fused_rollout
+
+    def inout(obs, t):
+        col._fused(obs, col.h_bf, col.c, col.h_bf2, col._hs[t + 1], col._cs[t + 1], 2, N, 0)
+
+    for rep in range(3):
+        for name, fn in (("masked", masked), ("inout", inout)):
+            col._fused_rollout = fn
+            col.collect()
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            for _ in range(2):
+                col.collect()
+            torch.cuda.synchronize()
+            el = time.perf_counter() - t0
+            print(f"rep {rep} {name}: {N * T * 2 / el / 1e6:.1f} M env-steps/s ({el / (2 * T) * 1e3:.3f} ms/step)",
+                  flush=True)
+    env.close()
+
+
+if __name__ == "__main__":
+    main()

@@ -31,6 +31,12 @@ def main():
     def fused():
         assert lib.vn_lstm_fused_bf16(p(x), od, p(hin), p(w), Kp, p(bias), p(c), p(hout), None, p(hs), p(cs), B, N, H,
                                       None) == 0
+    start = (torch.rand(N, device=dev) < 0.02).float()   # ~2 % of the agents start an episode
+    c_out = torch.empty_like(c)
+
+    def masked():   # the collector's rollout entry: c_in -> c_out, mask on read, no c_store
+        assert lib.vn_lstm_fused_bf16_masked(p(x), od, p(hin), p(w), Kp, p(bias), p(c), p(start), p(c_out), p(hout),
+                                             p(hs), B, N, H, None) == 0
     wih = w[:, :, :od].reshape(B * 4 * H, od).contiguous()
     whh = [w[b, :, kx:kx + H].contiguous() for b in range(B)]
     gx = torch.empty((N, B * 4 * H), dtype=torch.bfloat16, device=dev)
@@ -43,7 +49,10 @@ def main():
             torch.mm(hin[b], whh[b].t(), out=gh[b])
         assert lib.vn_lstm_cell_bf16(p(gx), 8 * H, p(gh), p(bias), p(bias), p(h32), p(c), p(hout), p(hs), p(cs), B,
                                      N, H, None) == 0
-    for name, fn in (("fused", fused), ("unfused", unfused)):
+    variants = [("fused", fused), ("unfused", unfused)]
+    if hasattr(lib, "vn_lstm_fused_bf16_masked"):
+        variants.insert(1, ("fused_masked", masked))
+    for name, fn in variants:
         for _ in range(3):
             fn()
         torch.cuda.synchronize()

@@ -262,3 +262,63 @@ def test_fused_mfma_lstm_exact_mapping(voxnav):
     assert lib.vn_lstm_cell_bf16(p(gx), 8 * H, p(gh), p(tb), p(torch.zeros_like(tb)), p(h2), p(c2), None, None, None,
                                  B, N, H, None) == 0
     np.testing.assert_allclose(c2.cpu().numpy(), c1, atol=3e-2, rtol=3e-2)
+    # the rollout entry (vn_lstm_fused_bf16_masked): c read from c_in with the
+    # episode-start mask applied on read, written only to c_out -- bitwise the
+    # same step as vn_lstm_fused_bf16 on the masked state
+    start = (rng.random(N) < 0.3).astype(np.float32)
+    ts = t(start)
+    cm = t(np.where(start[None, :, None] != 0, 0.0, c0).astype(np.float32))
+    h_a = torch.zeros((B, N, H), dtype=torch.bfloat16, device=dev)
+    hs_a = torch.zeros((B, N, H), device=dev)
+    assert lib.vn_lstm_fused_bf16(p(tx), od, p(th), p(tw), Kp, p(tb), p(cm), p(h_a), None, p(hs_a), None, B, N, H,
+                                  None) == 0
+    c_in = t(c0)
+    c_out = torch.full((B, N, H), float("nan"), device=dev)
+    h_b = torch.zeros((B, N, H), dtype=torch.bfloat16, device=dev)
+    hs_b = torch.zeros((B, N, H), device=dev)
+    assert lib.vn_lstm_fused_bf16_masked(p(tx), od, p(th), p(tw), Kp, p(tb), p(c_in), p(ts), p(c_out), p(h_b),
+                                         p(hs_b), B, N, H, None) == 0
+    torch.cuda.synchronize()
+    assert torch.equal(c_out, cm) and torch.equal(h_b, h_a) and torch.equal(hs_b, hs_a)
+    assert torch.equal(c_in, t(c0))                      # the input state is not written
+    assert lib.vn_lstm_fused_bf16_masked(p(tx), od, p(th), p(tw), Kp, p(tb), p(c_in), None, p(c_in), p(h_b),
+                                         None, B, N, H, None) != 0     # c_in == c_out refused
+
+
+def test_fused_bf16_truncation_bootstrap_uses_post_step_state(voxnav):
+    """The fused bf16 collector's truncation bootstrap: rewards[t, a] - r_env
+    == gamma * V(terminal obs; critic state after step t), recomputed here
+    from the rollout buffer's stored states lstm_h / lstm_c[t+1] through the
+    same kernels.  (The fused step's h is a ping-pong pair, so the stash must
+    read the buffer the step just wrote, at every t.)"""
+    from oracle.oracle import OracleEnv
+    from voxnav.collector import RolloutCollector
+    from voxnav.env import BatchedGridEnv
+    prod, orooms = _rooms()
+    N, T, L = 64, 48, 4
+    env = BatchedGridEnv(num_agents=N, rooms=prod, local_map_length=L, device="cuda:0")
+    col = RolloutCollector(env, _policy("lstm").to("cuda:0"), n_steps=T, sample_seed=1234, reset_seed=42,
+                           policy_dtype="bf16")
+    assert col.fused and col.store
+    oenv = OracleEnv(orooms, n_agents=N, local_map_length=L)
+    seeds = 42 + np.arange(N)
+    n_boot, parity = 0, set()
+    for r in range(2):
+        buf = col.collect()
+        torch.cuda.synchronize()
+        acts = buf.actions.cpu().numpy()
+        rr = oenv.run_random(seeds, 0, T, t0=r * T, seed_stride=N, initial_reset=(r == 0), actions=acts,
+                             terminal_obs=True)
+        te, tr = rr["terminated"].astype(bool), rr["truncated"].astype(bool)
+        ts, ag = np.nonzero(tr & ~te)
+        it, ia = torch.as_tensor(ts + 1, device="cuda:0"), torch.as_tensor(ag, device="cuda:0")
+        h = col._hs[it, 1, ia].to(torch.bfloat16)
+        c = col._cs[it, 1, ia].clone()
+        tobs = torch.as_tensor(rr["terminal_obs"][ts, ag], device="cuda:0")
+        v = torch.empty(len(ts), device="cuda:0")
+        col._critic(tobs, h, c, v)
+        got = buf.rewards.cpu().numpy()[ts, ag].astype(np.float64) - rr["reward"].astype(np.float32)[ts, ag]
+        np.testing.assert_allclose(got, 0.99 * v.cpu().numpy().astype(np.float64), atol=2e-5, rtol=1e-5)
+        n_boot += len(ts)
+        parity |= set((ts % 2).tolist())
+    assert n_boot > 0 and parity == {0, 1}, "truncations at both even and odd steps"

@@ -38,10 +38,10 @@ def voxnav():
     return voxnav
 
 
-def make_env(n):
+def make_env(n, **kw):
     from voxnav.env import BatchedGridEnv
     return BatchedGridEnv(num_agents=n, rooms=product_room_set(SRC), local_map_length=L, autoreset=True,
-                          device="cuda:0")
+                          device="cuda:0", **kw)
 
 
 def check_beliefs(env, orc_env, sample, step):
@@ -53,8 +53,11 @@ def check_beliefs(env, orc_env, sample, step):
         np.testing.assert_array_equal(b[j, :W, :D, :H], ref, err_msg=f"belief of agent {sample[j]} at step {step}")
 
 
-def run_random_episode(env, N, sample, F=16):
-    """Bench-shaped launches; compare the sampled agents launch by launch."""
+def run_random_episode(env, N, sample, F=16, gid_base=0, seed_stride=None):
+    """Bench-shaped launches; compare the sampled agents launch by launch.
+    ``sample`` are local agent indices; the shard's global ids start at
+    ``gid_base`` and its seeds advance by ``seed_stride`` (the global count)."""
+    seed_stride = N if seed_stride is None else seed_stride
     from voxnav.env import Rollout
     dev = env.device
     out = Rollout(torch.empty((F, N, 80), dtype=torch.float32, device=dev),
@@ -64,7 +67,8 @@ def run_random_episode(env, N, sample, F=16):
     assert env.kernel_label(F) == "env_kernel<8, false, true, false, 2>"
     idx = torch.as_tensor(sample, device=dev)
     orc_env = oracle_env(SRC, L, n_agents=len(sample))
-    seeds = 42 + np.asarray(sample, dtype=np.int64)
+    gids = gid_base + np.asarray(sample, dtype=np.int64)
+    seeds = 42 + gids
     env.reset(seed=42)
     t = 0
     truncations = 0
@@ -72,8 +76,8 @@ def run_random_episode(env, N, sample, F=16):
         k = min(F, K_TOTAL - t)
         env.step_random(k, policy_seed=42, t0=t,
                         out=Rollout(out.obs[:k], out.reward[:k], out.terminated[:k], out.truncated[:k], None))
-        orc = orc_env.run_random(seeds, policy_seed=42, K=k, t0=t, seed_stride=N, initial_reset=(t == 0),
-                                 gids=sample, threads=8)
+        orc = orc_env.run_random(seeds, policy_seed=42, K=k, t0=t, seed_stride=seed_stride,
+                                 initial_reset=(t == 0), gids=gids, threads=8)
         obs = out.obs[:k].index_select(1, idx).cpu().numpy()
         if obs.tobytes() != orc["obs"].tobytes():
             bad = np.argwhere((obs.view(np.uint32) != orc["obs"].view(np.uint32)).any(-1))
@@ -109,6 +113,21 @@ def test_full_batch_sampled_blocks_full_episode(voxnav):
     sample = blocks * 64 + (blocks * 37 + 11) % 64
     env = make_env(N)
     tr = run_random_episode(env, N, sample)
+    assert tr == len(sample)
+    env.close()
+
+
+def test_c5_last_shard_full_episode_at_bench_launch_size(voxnav):
+    """BASELINE C5 (524,288 agents over 8 GPUs) is 8 independent shards of
+    65,536 agents with global ids.  The last shard (rank 7:
+    global ids 458,752..524,287, seeds advancing by 524,288 per episode) on
+    this GPU, in the bench's 64-step launches, one sampled agent from every
+    64-agent block through the whole episode and the auto-reset."""
+    N, WORLD, RANK = 65536, 8, 7
+    blocks = np.arange(N // 64, dtype=np.int64)
+    sample = blocks * 64 + (blocks * 29 + 5) % 64
+    env = make_env(N, agent_id_base=RANK * N, seed_stride=WORLD * N)
+    tr = run_random_episode(env, N, sample, F=64, gid_base=RANK * N, seed_stride=WORLD * N)
     assert tr == len(sample)
     env.close()
 
