@@ -92,10 +92,14 @@ __device__ __forceinline__ uint32_t philox_word0(uint64_t key, uint64_t gid, uin
 // T = float, or uint16_t for bf16 gate pre-activations (the bf16 policy
 // path, which also writes h in bf16 for the next GEMMs into h_bf).
 // ----------------------------------------------------------------------------
-template <typename T>
+// MASK (the rollout entry vn_lstm_cell_masked): the state is read from c_in
+// (!= c) and gh was computed from the UNMASKED h; agents with start[n] != 0
+// take h = c = 0, i.e. no gh term (h_masked @ W_hh^T = 0 exactly) and c_in 0.
+template <typename T, bool MASK>
 __global__ __launch_bounds__(256) void lstm_cell_kernel(const T *__restrict__ gx, int64_t gx_row,
                                                         const T *__restrict__ gh, const float *__restrict__ b_ih,
                                                         const float *__restrict__ b_hh, float *__restrict__ h,
+                                                        const float *__restrict__ c_in, const float *__restrict__ start,
                                                         float *__restrict__ c, uint16_t *__restrict__ h_bf,
                                                         float *__restrict__ h_store, float *__restrict__ c_store,
                                                         int B, int N, int H) {
@@ -109,7 +113,8 @@ __global__ __launch_bounds__(256) void lstm_cell_kernel(const T *__restrict__ gx
     const int j = (int)(r - n * H4) * 4;
     const int G = 4 * H;
     const T *px = gx + n * gx_row + (int64_t)b * G + j;
-    const T *ph = gh ? gh + ((int64_t)b * N + n) * G + j : nullptr;
+    const bool zero = MASK && start[n] != 0.0f;
+    const T *ph = (gh && !zero) ? gh + ((int64_t)b * N + n) * G + j : nullptr;
     const float *pbi = b_ih + (int64_t)b * G + j;
     const float *pbh = b_hh + (int64_t)b * G + j;
     float4 pre[4];
@@ -128,7 +133,7 @@ __global__ __launch_bounds__(256) void lstm_cell_kernel(const T *__restrict__ gx
         pre[k] = s;
     }
     const int64_t so = ((int64_t)b * N + n) * H + j;
-    float4 cv = *reinterpret_cast<const float4 *>(c + so);
+    float4 cv = zero ? make_float4(0.f, 0.f, 0.f, 0.f) : *reinterpret_cast<const float4 *>((MASK ? c_in : c) + so);
     float4 hv;
 #define VN_CELL(comp)                                                                 \
     {                                                                                 \
@@ -683,14 +688,20 @@ namespace {
 template <typename T>
 int lstm_cell_launch(const T *gx, int64_t gx_row_stride, const T *gh, const float *b_ih, const float *b_hh, float *h,
                      float *c, uint16_t *h_bf, float *h_store, float *c_store, int32_t n_lstm, int32_t N, int32_t H,
-                     void *stream) {
+                     void *stream, const float *c_in = nullptr, const float *start = nullptr) {
     if (!gx || !b_ih || !b_hh || !h || !c) return fail(VN_ERR_INVALID, "NULL argument");
     if (n_lstm < 1 || N < 1 || H < 4 || (H & 3)) return fail(VN_ERR_INVALID, "bad sizes n_lstm=%d N=%d H=%d", n_lstm, N, H);
     if (gx_row_stride < (int64_t)n_lstm * 4 * H || (gx_row_stride & 3))
         return fail(VN_ERR_INVALID, "gx_row_stride %lld too small / unaligned", (long long)gx_row_stride);
     const int64_t threads = (int64_t)n_lstm * N * (H / 4);
-    hipLaunchKernelGGL(lstm_cell_kernel<T>, dim3(blocks_for(threads)), dim3(256), 0, (hipStream_t)stream, gx,
-                       gx_row_stride, gh, b_ih, b_hh, h, c, h_bf, h_store, c_store, (int)n_lstm, (int)N, (int)H);
+    if (start)
+        hipLaunchKernelGGL((lstm_cell_kernel<T, true>), dim3(blocks_for(threads)), dim3(256), 0, (hipStream_t)stream,
+                           gx, gx_row_stride, gh, b_ih, b_hh, h, c_in, start, c, h_bf, h_store, c_store, (int)n_lstm,
+                           (int)N, (int)H);
+    else
+        hipLaunchKernelGGL((lstm_cell_kernel<T, false>), dim3(blocks_for(threads)), dim3(256), 0, (hipStream_t)stream,
+                           gx, gx_row_stride, gh, b_ih, b_hh, h, nullptr, nullptr, c, h_bf, h_store, c_store, (int)n_lstm,
+                           (int)N, (int)H);
     VN_HIP(hipGetLastError());
     return VN_OK;
 }
@@ -748,6 +759,15 @@ int vn_lstm_cell(const float *gx, int64_t gx_row_stride, const float *gh, const 
                  void *stream) {
     return lstm_cell_launch<float>(gx, gx_row_stride, gh, b_ih, b_hh, h, c, nullptr, h_store, c_store, n_lstm, N, H,
                                    stream);
+}
+
+int vn_lstm_cell_masked(const float *gx, int64_t gx_row_stride, const float *gh, const float *b_ih,
+                        const float *b_hh, const float *c_in, const float *start, float *h_out, float *c_out,
+                        int32_t n_lstm, int32_t N, int32_t H, void *stream) {
+    if (!c_in || !start || !gh) return fail(VN_ERR_INVALID, "NULL argument");
+    if (c_in == c_out) return fail(VN_ERR_INVALID, "c_in and c_out must differ");
+    return lstm_cell_launch<float>(gx, gx_row_stride, gh, b_ih, b_hh, h_out, c_out, nullptr, nullptr, nullptr, n_lstm,
+                                   N, H, stream, c_in, start);
 }
 
 int vn_lstm_cell_bf16(const uint16_t *gx, int64_t gx_row_stride, const uint16_t *gh, const float *b_ih,

@@ -70,6 +70,7 @@ _SIGS = {
     "vn_lstm_cell": (C.c_int, [P, C.c_int64, P, P, P, P, P, P, P, C.c_int32, C.c_int32, C.c_int32, P]),
     "vn_policy_head": (C.c_int, [P, P, C.c_int32, C.c_int32, P, P, C.c_int32, P, P, C.c_uint64, C.c_uint64,
                                  C.c_int64, C.c_int32, P, P, P, P]),
+    "vn_lstm_cell_masked": (C.c_int, [P, C.c_int64, P, P, P, P, P, P, P, C.c_int32, C.c_int32, C.c_int32, P]),
     "vn_lstm_cell_bf16": (C.c_int, [P, C.c_int64, P, P, P, P, P, P, P, P, C.c_int32, C.c_int32, C.c_int32, P]),
     "vn_policy_head_bf16": (C.c_int, [P, P, C.c_int32, C.c_int32, P, P, C.c_int32, P, P, C.c_uint64, C.c_uint64,
                                       C.c_int64, C.c_int32, P, P, P, P]),

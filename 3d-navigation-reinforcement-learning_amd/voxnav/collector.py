@@ -192,6 +192,7 @@ class RolloutCollector:
             self.fused = self.bf16 and self.w.fused
             self.h_bf2 = z(2, N, H, dt=torch.bfloat16) if self.fused else None  # fused step's output (ping-pong)
             self.store = bool(store_lstm_states)
+            self._no_start = z(N)                                              # step 0's mask (none)
             self._hs = z(T + 1, 2, N, H) if self.store else None
             self._cs = z(T + 1, 2, N, H) if self.store else None
         # truncation bootstrap stash (vn_collect_stash): the truncated agents'
@@ -281,7 +282,23 @@ class RolloutCollector:
             self._head(lat_pi, lat_vf, N, self.t_global, self.actions[t], self.values[t], self.log_probs[t])
             return
         x = obs if not self.bf16 else obs.to(self.cdt)
-        if self.recurrent:
+        if self.recurrent and in_rollout and self.store and not self.bf16:
+            # f32 inside collect(): (h, c) live in the buffer only; the products
+            # use the unmasked lstm_h[t] and the cell kernel applies the
+            # episode-start mask (vn_lstm_cell_masked); step 0 reads the
+            # current, already masked state
+            H = w.H
+            hin, c_in, start = (self.h, self.c, self._no_start) if t == 0 else \
+                (self._hs[t], self._cs[t], self._starts[t])
+            torch.mm(x, w.w_ih_cat.t(), out=self._gx)
+            torch.mm(hin[0], w.w_hh[0].t(), out=self._gh[0])
+            torch.mm(hin[1], w.w_hh[1].t(), out=self._gh[1])
+            h_out = self._hs[t + 1]
+            _native.check(self.lib.vn_lstm_cell_masked(_p(self._gx), 8 * H, _p(self._gh), _p(w.b_ih), _p(w.b_hh),
+                                                       _p(c_in), _p(start), _p(h_out), _p(self._cs[t + 1]), 2, N, H,
+                                                       self._stream()), "vn_lstm_cell_masked")
+            x_pi, x_vf = h_out[0], h_out[1]
+        elif self.recurrent:
             H = w.H
             hin = self.h_bf if self.bf16 else self.h
             torch.mm(x, w.w_ih_cat.t(), out=self._gx)
@@ -342,9 +359,12 @@ class RolloutCollector:
         self._stash_base.zero_()
         sb = self._stash_base
         rec = self.recurrent
-        # fused bf16 step with the buffer: the cell state lives in lstm_c only
-        # (vn_lstm_fused_bf16_masked); self.c is brought up to date after T
-        csbuf = rec and self.fused and self.store
+        # with the buffer, the fused bf16 step keeps the cell state in lstm_c
+        # only (vn_lstm_fused_bf16_masked) and the f32 step both h and c in
+        # lstm_h / lstm_c (vn_lstm_cell_masked); self.c (and the f32 self.h)
+        # are brought up to date after T
+        csbuf = rec and self.store and (self.fused or not self.bf16)
+        hbuf = csbuf and not self.fused
         for t in range(T):
             self._forward(self._obs[t], t, in_rollout=True)
             self.env.step_into(self.actions[t], self._obs[t + 1], self.rewards[t], self._term, self._trunc,
@@ -356,7 +376,7 @@ class RolloutCollector:
             # the truncated agents' terminal obs and critic state (before the
             # episode-start mask below) into the stash; no host read here.  The
             # fused path's h_bf is a ping-pong pair: read it after this step's swap
-            hsrc = (self.h_bf if self.fused else self.h) if rec else None
+            hsrc = (self._hs[t + 1] if hbuf else self.h_bf if self.fused else self.h) if rec else None
             _native.check(lib.vn_collect_stash(
                 _p(self._boot_idx), _p(self._boot_cnt), _p(sb[t]), _p(sb[t + 1]), t, N, _p(self._tobs),
                 self.env.obs_dim, _p(hsrc[1]) if rec else None, hsrc.element_size() if rec else 0,
@@ -371,8 +391,11 @@ class RolloutCollector:
                                                2 if self.recurrent else 0, self.w.H if self.recurrent else 0, s()),
                           "vn_episode_start")
             self.t_global += 1
-        if csbuf:   # the current (masked) state: lstm_c[T] with the episode-start mask
-            self.c.copy_(torch.where(self._starts[T][None, :, None] != 0, 0.0, self._cs[T]))
+        if csbuf:   # the current (masked) state: lstm_c[T] (lstm_h[T]) with the episode-start mask
+            done = self._starts[T][None, :, None] != 0
+            self.c.copy_(torch.where(done, 0.0, self._cs[T]))
+            if hbuf:
+                self.h.copy_(torch.where(done, 0.0, self._hs[T]))
         # the truncation bootstrap of the whole rollout: V(terminal obs) from the
         # stashed critic states, rewards[t, a] += gamma * V (one host read)
         M = int(sb[T].item())

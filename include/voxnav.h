@@ -193,6 +193,19 @@ int vn_lstm_cell(const float *gx, int64_t gx_row_stride, const float *gh, const 
                  float *h, float *c, float *h_store, float *c_store, int32_t n_lstm, int32_t N, int32_t H,
                  void *stream);
 
+/*
+ * vn_lstm_cell inside a rollout (RolloutCollector.collect, f32 policy): the
+ * state is read from the buffer's lstm_c[t] (c_in, before the episode-start
+ * mask) and the new (h, c) written only to lstm_h[t+1] / lstm_c[t+1]
+ * (h_out, c_out); gh was computed from the unmasked lstm_h[t], so agents
+ * with start[n] != 0 take neither gh nor c_in (their masked state is zero:
+ * RecurrentActorCriticPolicy._process_sequence).  c_in != c_out; gh, start
+ * non-NULL.  Other arguments as vn_lstm_cell.
+ */
+int vn_lstm_cell_masked(const float *gx, int64_t gx_row_stride, const float *gh, const float *b_ih,
+                        const float *b_hh, const float *c_in, const float *start, float *h_out, float *c_out,
+                        int32_t n_lstm, int32_t N, int32_t H, void *stream);
+
 /* vn_lstm_cell with bf16 gate pre-activations (uint16_t storage) from bf16
  * GEMMs; the cell math and the (h, c) state stay f32, and h is also written
  * in bf16 to h_bf16 [n_lstm][N][H] (the next GEMMs' input), or NULL. */

@@ -4,7 +4,9 @@ agents, P3_training, T=128): the rollout's fused LSTM step through
 vn_lstm_fused_bf16_masked (c read from lstm_c[t] with the episode-start mask,
 written only to lstm_c[t+1]) vs the in/out entry vn_lstm_fused_bf16 (c read
 and rewritten, plus the lstm_c[t+1] copy).  Timing only: the B variant skips
-the masked entry's bookkeeping, so its buffers are not a valid rollout."""
+the masked entry's bookkeeping, so its buffers are not a valid rollout.
+``python scripts/collector_ab.py f32``: the same for the f32 policy
+(vn_lstm_cell_masked vs vn_lstm_cell with the (h, c) arrays)."""
 import sys
 import time
 from pathlib import Path
@@ -26,15 +28,25 @@ def main():
     pol = RecurrentActorCriticPolicy().to(dev)
     env = BatchedGridEnv(num_agents=N, rooms=load_archive_set("P3_training"), local_map_length=10, autoreset=True,
                          device=dev)
-    col = RolloutCollector(env, pol, n_steps=T, sample_seed=42, reset_seed=42, policy_dtype="bf16")
-    masked = col._fused_rollout
+    dtype = sys.argv[1] if len(sys.argv) > 1 else "bf16"
+    col = RolloutCollector(env, pol, n_steps=T, sample_seed=42, reset_seed=42, policy_dtype=dtype)
+    if dtype == "bf16":
+        attr, masked = "_fused_rollout", col._fused_rollout
 
-    def inout(obs, t):
-        col._fused(obs, col.h_bf, col.c, col.h_bf2, col._hs[t + 1], col._cs[t + 1], 2, N, 0)
+        def inout(obs, t):
+            col._fused(obs, col.h_bf, col.c, col.h_bf2, col._hs[t + 1], col._cs[t + 1], 2, N, 0)
+    else:
+        attr, fwd = "_forward", col._forward
+
+        def masked(obs, t, in_rollout=False):
+            fwd(obs, t, in_rollout)
+
+        def inout(obs, t, in_rollout=False):
+            fwd(obs, t, False)
 
     for rep in range(3):
         for name, fn in (("masked", masked), ("inout", inout)):
-            col._fused_rollout = fn
+            setattr(col, attr, fn)
             col.collect()
             torch.cuda.synchronize()
             t0 = time.perf_counter()
@@ -42,7 +54,7 @@ def main():
                 col.collect()
             torch.cuda.synchronize()
             el = time.perf_counter() - t0
-            print(f"rep {rep} {name}: {N * T * 2 / el / 1e6:.1f} M env-steps/s ({el / (2 * T) * 1e3:.3f} ms/step)",
+            print(f"rep {rep} {dtype} {name}: {N * T * 2 / el / 1e6:.1f} M env-steps/s ({el / (2 * T) * 1e3:.3f} ms/step)",
                   flush=True)
     env.close()
 

@@ -180,6 +180,22 @@ def test_kernels_match_torch_fp32(voxnav):
     col.c.copy_(c)
     col._forward(obs, 1)
     assert torch.equal(col.actions[1].long(), lg.argmax(1))
+    # the rollout entry (vn_lstm_cell_masked): a step from the buffer's
+    # unmasked lstm_h / lstm_c[t] with episode_starts[t] is bitwise the step
+    # from the masked state through vn_lstm_cell
+    col.deterministic = False
+    start = (torch.rand(N, device="cuda:0", generator=g) < 0.3).float()
+    keep = (start == 0)[None, :, None]
+    col._hs[1].copy_(h)
+    col._cs[1].copy_(c)
+    col._starts[1].copy_(start)
+    col._forward(obs, 1, in_rollout=True)
+    hm, cm = col._hs[2].clone(), col._cs[2].clone()
+    assert torch.equal(col._hs[1], h) and torch.equal(col._cs[1], c)     # inputs not written
+    col.h.copy_(torch.where(keep, h, 0.0))
+    col.c.copy_(torch.where(keep, c, 0.0))
+    col._forward(obs, 2)
+    assert torch.equal(hm, col.h) and torch.equal(cm, col.c)
 
 
 def test_compaction_and_episode_start(voxnav):
