@@ -129,6 +129,20 @@ class _Weights:
             raise NotImplementedError("pi and vf latents must have the same width")
 
 
+def _mm_rocblas(a, b, out):
+    """``torch.mm`` through rocBLAS instead of hipBLASLt: the f32 input
+    projection (65,536 x 80 @ 80 x 2048, output-bound) runs 202 vs 240 us
+    there (scripts/blas_backend_bench.py); every other shape is as fast or
+    faster on hipBLASLt, so the preference is switched around this call only."""
+    bk = torch.backends.cuda
+    prev = bk.preferred_blas_library()
+    bk.preferred_blas_library("hipblas")
+    try:
+        torch.mm(a, b, out=out)
+    finally:
+        bk.preferred_blas_library(prev)
+
+
 def _mlp(layers, x):
     for w, b in layers:
         x = torch.addmm(b, x, w.t())
@@ -290,7 +304,7 @@ class RolloutCollector:
             H = w.H
             hin, c_in, start = (self.h, self.c, self._no_start) if t == 0 else \
                 (self._hs[t], self._cs[t], self._starts[t])
-            torch.mm(x, w.w_ih_cat.t(), out=self._gx)
+            _mm_rocblas(x, w.w_ih_cat.t(), self._gx)
             torch.mm(hin[0], w.w_hh[0].t(), out=self._gh[0])
             torch.mm(hin[1], w.w_hh[1].t(), out=self._gh[1])
             h_out = self._hs[t + 1]
