@@ -205,8 +205,9 @@ template <bool VEC_X, bool MASK>   // obs_dim % 8 == 0: branch-free staging load
 #endif
 __global__ __launch_bounds__(LF_T, VN_LF_MIN_WAVES) LF_WPE_ATTR void lstm_fused_bf16_kernel(
     const float *__restrict__ x, int obs_dim, int kx, const uint16_t *__restrict__ hin,
-    // c_in and c are the same array on the in/out entry: each lane loads its
-    // 16 states before any store, and a state's store depends on its load
+    // MASK: the state is read from c_in (never the array c); !MASK (the
+    // in/out entry): c_in is unused (null) and the state is read from c itself,
+    // so no two restrict pointers alias
     const uint16_t *__restrict__ w, int Kp, const float *__restrict__ bias, const float *__restrict__ c_in,
     const float *__restrict__ start, float *__restrict__ c, uint16_t *__restrict__ hout, float *__restrict__ h32,
     float *__restrict__ h_store, float *__restrict__ c_store, int N, int H, int ncombo) {
@@ -377,7 +378,7 @@ __global__ __launch_bounds__(LF_T, VN_LF_MIN_WAVES) LF_WPE_ATTR void lstm_fused_
 #pragma unroll
     for (int reg = 0; reg < 16; ++reg) {
         const int n = min(n_base + wr + (reg & 3) + 8 * (reg >> 2) + 4 * (lane >> 5), N - 1);
-        const float v = c_in[((size_t)b * N + n) * H + u];
+        const float v = (MASK ? c_in : c)[((size_t)b * N + n) * H + u];
         cin[reg] = (MASK && start[n] != 0.0f) ? 0.0f : v;   // the episode-start mask, applied on read
     }
     const float *bb = bias + (size_t)b * 4 * H;
@@ -782,7 +783,7 @@ int lstm_fused_launch(const float *x, int32_t obs_dim, const uint16_t *h_in, con
                       const float *bias, const float *c_in, const float *start, float *c, uint16_t *h_out,
                       float *h32, float *h_store, float *c_store, int32_t n_lstm, int32_t N, int32_t H,
                       void *stream) {
-    if (!x || !h_in || !w_cat || !bias || !c_in || !c || !h_out) return fail(VN_ERR_INVALID, "NULL argument");
+    if (!x || !h_in || !w_cat || !bias || !c || !h_out || (start && !c_in)) return fail(VN_ERR_INVALID, "NULL argument");
     if (h_in == h_out) return fail(VN_ERR_INVALID, "h_in and h_out must differ (other blocks read h_in)");
     const int kx = (obs_dim + 7) & ~7;
     if (n_lstm < 1 || N < 1 || obs_dim < 1 || H < 64 || (H % LF_UNITS) || (Kp % LF_KC) || Kp < kx + H)
@@ -811,13 +812,14 @@ int lstm_fused_launch(const float *x, int32_t obs_dim, const uint16_t *h_in, con
 int vn_lstm_fused_bf16(const float *x, int32_t obs_dim, const uint16_t *h_in, const uint16_t *w_cat, int32_t Kp,
                        const float *bias, float *c, uint16_t *h_out, float *h32, float *h_store, float *c_store,
                        int32_t n_lstm, int32_t N, int32_t H, void *stream) {
-    return lstm_fused_launch(x, obs_dim, h_in, w_cat, Kp, bias, c, nullptr, c, h_out, h32, h_store, c_store, n_lstm,
-                             N, H, stream);
+    return lstm_fused_launch(x, obs_dim, h_in, w_cat, Kp, bias, nullptr, nullptr, c, h_out, h32, h_store, c_store,
+                             n_lstm, N, H, stream);
 }
 
 int vn_lstm_fused_bf16_masked(const float *x, int32_t obs_dim, const uint16_t *h_in, const uint16_t *w_cat,
                               int32_t Kp, const float *bias, const float *c_in, const float *start, float *c_out,
                               uint16_t *h_out, float *h_store, int32_t n_lstm, int32_t N, int32_t H, void *stream) {
+    if (!start) return fail(VN_ERR_INVALID, "NULL argument (start)");
     if (c_in == c_out) return fail(VN_ERR_INVALID, "c_in and c_out must differ");
     return lstm_fused_launch(x, obs_dim, h_in, w_cat, Kp, bias, c_in, start, c_out, h_out, nullptr, h_store, nullptr,
                              n_lstm, N, H, stream);

@@ -174,7 +174,6 @@ struct Blas {
     decltype(&rocblas_create_handle) create = nullptr;
     decltype(&rocblas_set_stream) set_stream = nullptr;
     decltype(&rocblas_sgemm_strided_batched) sgemm_sb = nullptr;
-    rocblas_handle handle[64] = {};   // per device
     bool ok = false;
 };
 
@@ -195,20 +194,22 @@ Blas &blas() {
     return b;
 }
 
-std::mutex g_blas_mu;
-
-// the calling thread's device's handle, bound to `stream`
+// the calling thread's handle for its current device, bound to `stream`.
+// One handle per (thread, device): a handle carries its stream, so a handle
+// shared between threads driving different streams would let one thread's
+// GEMMs run on the other's stream.  (A thread's handles live until process
+// exit; the learner runs from one thread per device.)
 int blas_handle(hipStream_t stream, rocblas_handle &out) {
     Blas &b = blas();
     if (!b.ok) return fail(VN_ERR_HIP, "rocBLAS (librocblas.so.5) could not be loaded");
     int dev = 0;
     VN_HIP(hipGetDevice(&dev));
     if (dev < 0 || dev >= 64) return fail(VN_ERR_INVALID, "device %d out of range", dev);
-    std::lock_guard<std::mutex> lk(g_blas_mu);
-    if (!b.handle[dev] && b.create(&b.handle[dev]) != rocblas_status_success)
+    thread_local rocblas_handle handles[64] = {};
+    if (!handles[dev] && b.create(&handles[dev]) != rocblas_status_success)
         return fail(VN_ERR_HIP, "rocblas_create_handle failed");
-    if (b.set_stream(b.handle[dev], stream) != rocblas_status_success) return fail(VN_ERR_HIP, "rocblas_set_stream failed");
-    out = b.handle[dev];
+    if (b.set_stream(handles[dev], stream) != rocblas_status_success) return fail(VN_ERR_HIP, "rocblas_set_stream failed");
+    out = handles[dev];
     return VN_OK;
 }
 

@@ -7,6 +7,7 @@ include/voxnav.h.  Public API:
 
   rooms.*             room-file parser / room sets / synthetic boxes
   BatchedGridEnv      N agents per GPU, torch tensors in/out, SB3 auto-reset
+  VoxnavVecEnv        SB3's VecEnv contract (SubprocVecEnv + Monitor) over BatchedGridEnv
   GridAgent           the reference's single-env gymnasium API (CubicEnv)
   SimpleGridAgent     the same for the goal-seeking simpleEnv variant
   RolloutCollector    on-device PPO rollout collection (policy in the loop)
@@ -19,7 +20,7 @@ include/voxnav.h.  Public API:
 from . import rooms  # noqa: F401
 from ._native import VoxnavError, load as load_library  # noqa: F401
 
-__all__ = ["rooms", "BatchedGridEnv", "GridAgent", "SimpleGridAgent", "RolloutCollector", "compute_gae",
+__all__ = ["rooms", "BatchedGridEnv", "VoxnavVecEnv", "GridAgent", "SimpleGridAgent", "RolloutCollector", "compute_gae",
            "PPOLearner", "evaluate_policy", "save_checkpoint", "load_checkpoint", "VoxnavError", "load_library"]
 
 
@@ -28,6 +29,9 @@ def __getattr__(name):
     if name == "BatchedGridEnv":
         from .env import BatchedGridEnv
         return BatchedGridEnv
+    if name == "VoxnavVecEnv":
+        from .vec_env import VoxnavVecEnv
+        return VoxnavVecEnv
     if name == "GridAgent":
         from .gym_api import GridAgent
         return GridAgent

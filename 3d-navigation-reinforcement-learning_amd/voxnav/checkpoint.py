@@ -155,12 +155,22 @@ def load_checkpoint(path: Union[str, Path], device="cpu") -> Tuple[torch.nn.Modu
     with zipfile.ZipFile(path) as z:
         raw = z.read("data")
         sd = torch.load(io.BytesIO(z.read("policy.pth")), map_location="cpu", weights_only=True)
+        ver = z.read("_stable_baselines3_version").decode(errors="replace").strip() \
+            if "_stable_baselines3_version" in z.namelist() else ""
     try:
         data = json.loads(raw)
     except ValueError:
         data = None
-    if not isinstance(data, dict) or data.get("format") != FORMAT_VERSION:
-        return policy_from_state_dict(sd).to(device), {"sb3": True}
+    fmt = data.get("format") if isinstance(data, dict) else None
+    ours = fmt is not None or ver.startswith("voxnav")
+    if ours and fmt != FORMAT_VERSION:
+        raise ValueError(f"{path}: voxnav checkpoint format {fmt or ver!r}, this build reads {FORMAT_VERSION!r}")
+    if not ours:
+        # an SB3 / sb3_contrib zip: JSON data with ``:serialized:`` (cloudpickled) fields and an SB3 version
+        if not (isinstance(data, dict) and any(isinstance(v, dict) and ":serialized:" in v for v in data.values())) \
+                and not ver:
+            raise ValueError(f"{path}: neither a voxnav nor an SB3 checkpoint")
+        return policy_from_state_dict(sd).to(device), {"sb3": True, "sb3_version": ver or None}
     kw = dict(data["policy_kwargs"])
     kw.pop("n_lstm_layers", None)
     cls = RecurrentActorCriticPolicy if data.get("policy_class") == "MlpLstmPolicy" else ActorCriticPolicy

@@ -211,11 +211,15 @@ class RolloutCollector:
             self._cs = z(T + 1, 2, N, H) if self.store else None
         # truncation bootstrap stash (vn_collect_stash): the truncated agents'
         # terminal obs and critic state, appended on the device each step and
-        # bootstrapped once per rollout.  An episode truncates when its step
-        # count reaches the room's free-cell count, so an agent truncates at
-        # most (T - 1) // min_free + 1 times per rollout.
+        # bootstrapped every `_flush_every` steps (one host read each; once per
+        # rollout unless the rooms are small).  An episode truncates when its
+        # step count reaches the room's free-cell count, so an agent truncates
+        # at most (F - 1) // min_free + 1 times in F steps; F = min(T, 4 min_free)
+        # keeps the stash at <= 4 rows per agent (obs + critic h, c: 4 (80 + 2H) B
+        # a row) whatever n_steps is.
         fmin = max(1, int(np.min(env.total_free_cells)))
-        self._stash_cap = N * ((T - 1) // fmin + 1)
+        self._flush_every = min(T, 4 * fmin)
+        self._stash_cap = N * ((self._flush_every - 1) // fmin + 1)
         cap = self._stash_cap
         self._stash_base = z(T + 1, dt=torch.int32)
         self._stash_obs = z(cap, env.obs_dim)
@@ -268,7 +272,7 @@ class RolloutCollector:
         (the episode-start mask applied on read; step 0 reads the current,
         already masked state) and written only to lstm_c[t+1]."""
         w = self.w
-        c_in, start = (self.c, None) if t == 0 else (self._cs[t], self._starts[t])
+        c_in, start = (self.c, self._no_start) if t == 0 else (self._cs[t], self._starts[t])
         _native.check(self.lib.vn_lstm_fused_bf16_masked(_p(obs), obs.shape[1], _p(self.h_bf), _p(w.w_cat), w.Kp,
                                                          _p(w.bias), _p(c_in), _p(start), _p(self._cs[t + 1]),
                                                          _p(self.h_bf2), _p(self._hs[t + 1]), 2, self.N, w.H,
@@ -405,24 +409,16 @@ class RolloutCollector:
                                                2 if self.recurrent else 0, self.w.H if self.recurrent else 0, s()),
                           "vn_episode_start")
             self.t_global += 1
+            if (t + 1) % self._flush_every == 0 and t + 1 < T:
+                self._bootstrap(sb[t + 1])       # bounded stash: flush, restart at row 0
+                sb[t + 1].zero_()
         if csbuf:   # the current (masked) state: lstm_c[T] (lstm_h[T]) with the episode-start mask
             done = self._starts[T][None, :, None] != 0
             self.c.copy_(torch.where(done, 0.0, self._cs[T]))
             if hbuf:
                 self.h.copy_(torch.where(done, 0.0, self._hs[T]))
-        # the truncation bootstrap of the whole rollout: V(terminal obs) from the
-        # stashed critic states, rewards[t, a] += gamma * V (one host read)
-        M = int(sb[T].item())
-        if M > self._stash_cap:
-            raise RuntimeError(f"bootstrap stash overflow: {M} > {self._stash_cap}")
-        if M:
-            tv = torch.empty(M, dtype=torch.float32, device=self.device)
-            if rec:
-                self._critic(self._stash_obs[:M], self._stash_h[:M], self._stash_c[:M], tv)
-            else:
-                self._critic(self._stash_obs[:M], None, None, tv)
-            _native.check(lib.vn_collect_bootstrap(_p(self._stash_flat), _p(tv), M, self.gamma, _p(self.rewards),
-                                                   s()), "vn_collect_bootstrap")
+        # the truncation bootstrap of the rest of the rollout
+        self._bootstrap(sb[T])
         # V(last obs) under the current (masked) critic state
         if self.recurrent:
             hsrc = self.h_bf if self.fused else self.h
@@ -443,6 +439,21 @@ class RolloutCollector:
                              episode_starts=self._starts[:T], values=self.values, log_probs=self.log_probs,
                              advantages=adv, returns=ret, lstm_h=hs, lstm_c=cs, last_values=self._last_values,
                              dones=self._starts[T])
+
+    def _bootstrap(self, count: torch.Tensor):
+        """V(terminal obs) from the stashed critic states, rewards[t, a] +=
+        gamma * V for the stash's first ``count`` rows (one host read)."""
+        M = int(count.item())
+        if M > self._stash_cap:     # cannot happen: at most (F-1)//min_free+1 truncations per agent in F steps
+            raise RuntimeError(f"bootstrap stash overflow: {M} > {self._stash_cap}")
+        if M:
+            tv = torch.empty(M, dtype=torch.float32, device=self.device)
+            if self.recurrent:
+                self._critic(self._stash_obs[:M], self._stash_h[:M], self._stash_c[:M], tv)
+            else:
+                self._critic(self._stash_obs[:M], None, None, tv)
+            _native.check(self.lib.vn_collect_bootstrap(_p(self._stash_flat), _p(tv), M, self.gamma,
+                                                        _p(self.rewards), self._stream()), "vn_collect_bootstrap")
 
     def _carry_over(self):
         # the previous rollout's last obs / episode starts / lstm states become

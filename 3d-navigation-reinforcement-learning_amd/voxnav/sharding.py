@@ -47,26 +47,36 @@ def shard_for(n_local: int, rank: Optional[int] = None, world: Optional[int] = N
     return Shard(int(rank), int(world), int(n_local))
 
 
-def allgather_rollout(buffers: Dict[str, torch.Tensor], agent_dim: int = 1,
-                      group=None) -> Dict[str, torch.Tensor]:
+def allgather_rollout(buffers: Dict[str, torch.Tensor], agent_dim: int = 1, group=None,
+                      flat: bool = False) -> Dict[str, torch.Tensor]:
     """All-gather per-shard trajectory buffers along the agent dimension.
 
-    Each tensor is [T, n_local, ...] (agent_dim=1); the result is
-    [T, n_global, ...] ordered by rank, i.e. by global agent id.  One
-    collective per buffer, issued back to back (large messages: the ring is
-    per-link bound on xGMI, so fewer bigger transfers are preferable).
+    Each tensor is [T, n_local, ...] (agent dim ``agent_dim``), contiguous.
+    One ``all_gather_into_tensor`` per buffer straight from the buffer into
+    a [world * T, n_local, ...] output (ranks concatenated: no copy before
+    the collective), returned as a zero-copy strided view with the rank as
+    a new dimension in front of the agent dimension: [T, world, n_local,
+    ...], so ``out[:, r, i]`` is global agent ``r * n_local + i`` and the
+    view enumerates agents in global-id order (its C-order bytes are those
+    of a [T, n_global, ...] buffer).  ``flat=True`` materialises that
+    [T, n_global, ...] tensor (one copy) for callers that need it.  Large
+    messages, back to back: the xGMI ring is per-link bound, so few big
+    transfers.
     """
-    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size(group) == 1:
-        return dict(buffers)
-    world = dist.get_world_size(group)
+    world = dist.get_world_size(group) if (dist.is_available() and dist.is_initialized()) else 1
     out = {}
     for name, t in buffers.items():
-        t = t.contiguous()
-        moved = t.movedim(agent_dim, 0).contiguous()
-        gathered = torch.empty((world * moved.shape[0],) + tuple(moved.shape[1:]), dtype=moved.dtype,
-                               device=moved.device)
-        dist.all_gather_into_tensor(gathered, moved, group=group)
-        out[name] = gathered.movedim(0, agent_dim).contiguous()
+        if not t.is_contiguous():
+            raise ValueError(f"{name}: allgather_rollout gathers contiguous buffers in place")
+        if world == 1:
+            g = t.unsqueeze(0)
+        else:
+            g = torch.empty((world,) + tuple(t.shape), dtype=t.dtype, device=t.device)
+            dist.all_gather_into_tensor(g.view((world * t.shape[0],) + tuple(t.shape[1:])), t, group=group)
+        v = g.movedim(0, agent_dim)                     # [..., world, n_local, ...]
+        if flat:
+            v = v.reshape(tuple(t.shape[:agent_dim]) + (world * t.shape[agent_dim],) + tuple(t.shape[agent_dim + 1:]))
+        out[name] = v
     return out
 
 

@@ -210,6 +210,9 @@ def cpu_baseline(room_whd, L, seconds):
     cal = REPO / "profiles" / "py_baseline_calibration.json"
     if cal.exists():
         c = json.loads(cal.read_text())
+        ratio = float(c["restatement_over_reference"])
+        rec["reference_equivalent_value"] = round(v / ratio, 1)
+        rec["reference_equivalent_single_core_value"] = round(v1 / ratio, 1)
         rec["reference_calibration"] = {
             "restatement_over_reference": c["restatement_over_reference"],
             "reference_single_core_build_container": c["reference_envs_CubicEnv_steps_per_s"],
@@ -344,17 +347,19 @@ def allgather_leg(torch, dist, dev, rank, world, buf, reps=3):
         if _ < reps - 1:
             del got
     # this rank's slice of the gathered buffers is its own data
-    n = buf.rewards.shape[1]
-    assert torch.equal(got["rewards"][:, rank * n:(rank + 1) * n], buf.rewards)
-    assert torch.equal(got["obs"][:, rank * n:(rank + 1) * n], buf.obs)
+    # [T, world, n_local, ...] views (no copy before or after the collective):
+    # this rank's slice is its own data
+    assert torch.equal(got["rewards"][:, rank], buf.rewards)
+    assert torch.equal(got["obs"][:, rank], buf.obs)
     if buf.lstm_h is not None:
-        assert torch.equal(got["lstm_h0"][:, :, rank * n:(rank + 1) * n], buf.lstm_h[:1])
+        assert torch.equal(got["lstm_h0"][:, :, rank], buf.lstm_h[:1])
     del got
     el = min(times)
     total = local_bytes * world
     return {"bytes_per_rank": local_bytes, "gathered_bytes": total, "seconds": round(el, 5),
             "algbw_GBps": round(total / el / 1e9, 2), "busbw_GBps": round(total * (world - 1) / world / el / 1e9, 2),
-            "collective": "all_gather_into_tensor per buffer (RCCL over xGMI)", "reps": reps}
+            "collective": "all_gather_into_tensor per buffer straight from the rollout buffer (RCCL over xGMI); "
+                          "results as [T, world, n_local] views, no copies in the timed region", "reps": reps}
 
 
 def learner_leg(args, torch, dist, dev, world, pol, buf, kind):
@@ -546,6 +551,10 @@ def main():
     roof = roofline_block(bstep, N, F, args.steps, timed, kern_ms,
                           traffic_for(W, D, H, args.L, N, F, args.warmup, args.steps), label)
     value = N * world * args.steps / elapsed
+    # every agent starts at t=0 and a random-policy episode truncates at the
+    # room's free-cell count: an auto-reset is inside the
+    # window iff it reaches that step
+    resets_in_window = args.warmup + args.steps >= box_room(W, D, H).total_free_cells
 
     episode = None
     if args.episode_window and args.steps < EPISODE_WINDOW:
@@ -621,7 +630,10 @@ def main():
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "int8",
             "data": "synthetic (walled-box room in the reference room-file grammar; Philox uniform random policy)",
             "config": {"workload": f"C3 env step: {N} agents/GPU, {W}x{D}x{H} room, L={args.L}, "
-                                   f"random policy, SB3 auto-reset", "agents_per_gpu": N,
+                                   f"random policy" + (", SB3 auto-reset in the window" if resets_in_window
+                                                       else " (episode steps inside one episode: the "
+                                                            "window holds no auto-reset)"),
+                       "agents_per_gpu": N,
                        "global_agents": N * world, "room": f"{W}x{D}x{H}", "local_map_length": args.L,
                        "steps_per_launch": F,
                        "window": f"fresh env, {args.warmup} untimed steps, then exactly {args.steps} timed steps "

@@ -12,8 +12,8 @@ actions; the float policy quantities are compared with the float64 oracle
                                         boundary (f32 vs f64 rounding)
 With policy_dtype="bf16" (bf16 GEMM operands, f32 accumulation and cell
 state) the float bounds are 6e-2 + 6e-2|f64| (advantages 0.6 + 6e-2|f64|)
-and up to 6 % of the draws may flip within 0.08 of a CDF boundary.
-and the GAE kernel bit-exact against the f32 oracle on the GPU's own
+and up to 6 % of the draws may flip within 0.08 of a CDF boundary.  The
+GAE kernel is bit-exact against the f32 oracle on the GPU's own
 rewards/values.  The kernels alone are compared with the plain-PyTorch f32
 policy (voxnav.policy.forward_torch) at 2e-5.
 """
@@ -71,19 +71,33 @@ def _set_rooms(name):
     return product_room_set(f"set:{name}"), [parse_room_text(t, n) for n, t in set_members(name)]
 
 
+# BASELINE C5: 524,288 agents as 8 shards of 65,536; the last shard (rank 7)
+# has global ids 458,752.. and its seeds advance by 524,288 per episode
+C5_SHARD = (7 * 65536, 8 * 65536)
+
 COLLECT_CASES = [
-    # (policy, T, rollouts, dtype, rooms, L, N)
-    ("lstm", 48, 2, "f32", "boxes", 4, 64), ("mlp", 80, 1, "f32", "boxes", 4, 64),
-    ("lstm", 48, 2, "bf16", "boxes", 4, 64), ("mlp", 48, 1, "bf16", "boxes", 4, 64),
+    # (policy, T, rollouts, dtype, rooms, L, N, (agent_id_base, seed_stride) or None)
+    # T=96 / 80 > 4 x 18 (the smallest box's free cells): the bootstrap stash
+    # is flushed once inside the rollout (collector._flush_every = 72)
+    ("lstm", 96, 2, "f32", "boxes", 4, 64, None), ("mlp", 80, 1, "f32", "boxes", 4, 64, None),
+    ("lstm", 48, 2, "bf16", "boxes", 4, 64, None), ("mlp", 48, 1, "bf16", "boxes", 4, 64, None),
     # BASELINE configs at the reference's settings, a few hundred agents:
     # C4 = PPO-LSTM on P3_training (L=10, n_steps 128), C3 = PPO-MLP on P2_training
-    ("lstm", 128, 2, "f32", "P3_training", 10, 192), ("mlp", 128, 3, "f32", "P2_training", 10, 256),
+    ("lstm", 128, 2, "f32", "P3_training", 10, 192, None), ("mlp", 128, 3, "f32", "P2_training", 10, 256, None),
+    # C4 through the bf16 policy path the bench also reports (its stated bounds)
+    ("lstm", 128, 2, "bf16", "P3_training", 10, 192, None),
+    # C5: the last shard's collector -- Philox draws keyed by global id, seeds
+    # on the 524,288 stride (the bench's N>1 path)
+    ("lstm", 128, 2, "f32", "P3_training", 10, 192, C5_SHARD),
 ]
 
 
-@pytest.mark.parametrize("kind,T,rollouts,dtype,rooms,L,N", COLLECT_CASES,
-                         ids=[f"{c[0]}-{c[3]}-{c[4]}-T{c[1]}" for c in COLLECT_CASES])
-def test_collector_matches_oracle(voxnav, kind, T, rollouts, dtype, rooms, L, N):
+def _case_id(c):
+    return f"{c[0]}-{c[3]}-{c[4]}-T{c[1]}" + ("-C5shard" if c[7] else "")
+
+
+@pytest.mark.parametrize("kind,T,rollouts,dtype,rooms,L,N,shard", COLLECT_CASES, ids=[_case_id(c) for c in COLLECT_CASES])
+def test_collector_matches_oracle(voxnav, kind, T, rollouts, dtype, rooms, L, N, shard):
     from oracle import collector_oracle as co
     from oracle.oracle import OracleEnv, gae as gae32
     from voxnav.collector import RolloutCollector
@@ -91,7 +105,9 @@ def test_collector_matches_oracle(voxnav, kind, T, rollouts, dtype, rooms, L, N)
     from voxnav.policy import numpy_weights
     prod, orooms = _rooms() if rooms == "boxes" else _set_rooms(rooms)
     pol = _policy(kind)
-    env = BatchedGridEnv(num_agents=N, rooms=prod, local_map_length=L, device="cuda:0")
+    gid_base, stride = shard if shard else (0, N)
+    env = BatchedGridEnv(num_agents=N, rooms=prod, local_map_length=L, device="cuda:0", agent_id_base=gid_base,
+                         seed_stride=stride)
     col = RolloutCollector(env, pol.to("cuda:0"), n_steps=T, sample_seed=1234, reset_seed=42, policy_dtype=dtype)
     # f32: the reference's dtype, tight bounds; bf16 GEMM operands (8-bit
     # mantissa): looser bounds and some draws flip near a CDF boundary
@@ -99,7 +115,7 @@ def test_collector_matches_oracle(voxnav, kind, T, rollouts, dtype, rooms, L, N)
         dict(v=(6e-2, 6e-2), r=(6e-2, 6e-2), adv=(0.6, 6e-2), flip=0.08, nflip=int(0.06 * T * N))
     orc = co.PolicyOracle(numpy_weights(pol))
     oenv = OracleEnv(orooms, n_agents=N, local_map_length=L)
-    seeds = 42 + np.arange(N)
+    seeds = 42 + gid_base + np.arange(N)
     # reset observations
     ref = OracleEnv(orooms, n_agents=N, local_map_length=L)
     obs0 = np.stack([ref.reset(i, int(seeds[i])) for i in range(N)])
@@ -111,12 +127,13 @@ def test_collector_matches_oracle(voxnav, kind, T, rollouts, dtype, rooms, L, N)
         buf = col.collect()
         torch.cuda.synchronize()
         acts = buf.actions.cpu().numpy()
-        rr = oenv.run_random(seeds, 0, T, t0=r * T, seed_stride=N, initial_reset=(r == 0), actions=acts,
-                             terminal_obs=True)
+        rr = oenv.run_random(seeds, 0, T, t0=r * T, seed_stride=stride, initial_reset=(r == 0), actions=acts,
+                             terminal_obs=True, gid_base=gid_base)
         gobs = buf.obs.cpu().numpy()
         assert gobs[1:].tobytes() == rr["obs"][:-1].tobytes(), "env obs"
         assert col._obs[T].cpu().numpy().tobytes() == rr["obs"][-1].tobytes()
-        out = co.collect(orc, rr, gobs[0], starts0, acts, gamma=0.99, h0=h, c0=c, sample_seed=1234, t0=r * T)
+        out = co.collect(orc, rr, gobs[0], starts0, acts, gamma=0.99, h0=h, c0=c, sample_seed=1234, t0=r * T,
+                         gid_base=gid_base)
         h, c, starts0 = out["h"], out["c"], out["dones"]
         te, tr = rr["terminated"].astype(bool), rr["truncated"].astype(bool)
         total_boot += int((tr & ~te).sum())

@@ -4,12 +4,15 @@ and the SB3 auto-reset (plane clear at full u32 row width, wall-image
 re-copy), against the CPU oracle (oracle/voxnav_oracle.c, pinned to the
 reference's golden trajectories by tests/test_oracle_golden.py).
 
-* the bench's call: ``step_random(out=...)`` in F=16 launches, f32 reward,
-  no action record -> ``env_kernel<8, false, true, false, 2>``;
+* the bench's call: ``step_random(out=...)`` in F=16 and F=128 (the bench
+  default) launches, f32 reward, no action record ->
+  ``env_kernel<8, false, true, false, 2>``;
 * the collector's call: ``step_into`` with explicit actions, f32 reward,
   one step per launch -> ``env_kernel<8, true, true, false, 2>``;
 * the full BASELINE batch (65,536 agents) with one sampled agent from every
-  64-agent block, through a whole episode.
+  64-agent block, through a whole episode (also as C5's last shard);
+* BASELINE C2 at its size (4,096 agents, 16x16x8, L=10) through its
+  1,176-step truncation and auto-reset.
 
 Bar: obs bytes, f32 reward (the oracle's f64 reward rounded), terminated /
 truncated flags bit-exact at every step; exported belief maps equal the
@@ -53,7 +56,8 @@ def check_beliefs(env, orc_env, sample, step):
         np.testing.assert_array_equal(b[j, :W, :D, :H], ref, err_msg=f"belief of agent {sample[j]} at step {step}")
 
 
-def run_random_episode(env, N, sample, F=16, gid_base=0, seed_stride=None):
+def run_random_episode(env, N, sample, F=16, gid_base=0, seed_stride=None, src=SRC, k_total=K_TOTAL,
+                       belief_at=BELIEF_AT, L=L):
     """Bench-shaped launches; compare the sampled agents launch by launch.
     ``sample`` are local agent indices; the shard's global ids start at
     ``gid_base`` and its seeds advance by ``seed_stride`` (the global count)."""
@@ -66,14 +70,14 @@ def run_random_episode(env, N, sample, F=16, gid_base=0, seed_stride=None):
                   torch.empty((F, N), dtype=torch.uint8, device=dev), None)
     assert env.kernel_label(F) == "env_kernel<8, false, true, false, 2>"
     idx = torch.as_tensor(sample, device=dev)
-    orc_env = oracle_env(SRC, L, n_agents=len(sample))
+    orc_env = oracle_env(src, L, n_agents=len(sample))
     gids = gid_base + np.asarray(sample, dtype=np.int64)
     seeds = 42 + gids
     env.reset(seed=42)
     t = 0
     truncations = 0
-    while t < K_TOTAL:
-        k = min(F, K_TOTAL - t)
+    while t < k_total:
+        k = min(F, k_total - t)
         env.step_random(k, policy_seed=42, t0=t,
                         out=Rollout(out.obs[:k], out.reward[:k], out.terminated[:k], out.truncated[:k], None))
         orc = orc_env.run_random(seeds, policy_seed=42, K=k, t0=t, seed_stride=seed_stride,
@@ -89,7 +93,7 @@ def run_random_episode(env, N, sample, F=16, gid_base=0, seed_stride=None):
         np.testing.assert_array_equal(tr, orc["truncated"])
         truncations += int(tr.sum())
         t += k
-        if t in BELIEF_AT:
+        if t in belief_at:
             check_beliefs(env, orc_env, sample, t)
     return truncations
 
@@ -117,18 +121,40 @@ def test_full_batch_sampled_blocks_full_episode(voxnav):
     env.close()
 
 
-def test_c5_last_shard_full_episode_at_bench_launch_size(voxnav):
-    """BASELINE C5 (524,288 agents over 8 GPUs) is 8 independent shards of
-    65,536 agents with global ids.  The last shard (rank 7:
-    global ids 458,752..524,287, seeds advancing by 524,288 per episode) on
-    this GPU, in the bench's 64-step launches, one sampled agent from every
-    64-agent block through the whole episode and the auto-reset."""
+def test_c5_last_shard_env_full_episode_at_bench_launch_size(voxnav):
+    """The env half of BASELINE C5's last shard (rank 7 of 8: global ids
+    458,752..524,287, seeds advancing by 524,288 per episode) under the
+    random policy on the headline box, in the bench's 128-step launches,
+    one sampled agent from every 64-agent block through the whole episode
+    and the auto-reset.  (The PPO-LSTM collector of the same shard on
+    P3_training: tests/test_collector_gpu.py, case lstm-f32-P3_training-C5shard.)"""
     N, WORLD, RANK = 65536, 8, 7
     blocks = np.arange(N // 64, dtype=np.int64)
     sample = blocks * 64 + (blocks * 29 + 5) % 64
     env = make_env(N, agent_id_base=RANK * N, seed_stride=WORLD * N)
-    tr = run_random_episode(env, N, sample, F=64, gid_base=RANK * N, seed_stride=WORLD * N)
+    tr = run_random_episode(env, N, sample, F=128, gid_base=RANK * N, seed_stride=WORLD * N)
     assert tr == len(sample)
+    env.close()
+
+
+C2_SRC, C2_EPISODE = "box:16x16x8", 1176   # BASELINE C2: 4,096 agents, one 16x16x8 room (1,176 free cells)
+
+
+def test_c2_config_through_truncation_and_autoreset(voxnav):
+    """BASELINE config C2 at its size: 4,096 agents, 16x16x8 box, L=10,
+    random policy, in the bench's 128-step launches for 1,280 steps -- every
+    agent's 1,176-step episode truncates and auto-resets inside the window.
+    256 sampled agents (every 16th, offset varied) step-by-step bit-exact,
+    belief maps of the sample at steps 640 and 1,280 (the truncation at
+    1,176 falls inside the tenth launch, 1,152 + 24)."""
+    from voxnav.env import BatchedGridEnv
+    N = 4096
+    env = BatchedGridEnv(num_agents=N, rooms=product_room_set(C2_SRC), local_map_length=10, autoreset=True,
+                         device="cuda:0")
+    blocks = np.arange(N // 16, dtype=np.int64)
+    sample = blocks * 16 + (blocks * 7 + 3) % 16
+    tr = run_random_episode(env, N, sample, F=128, src=C2_SRC, k_total=1280, belief_at=(640, 1280))
+    assert tr == len(sample)          # each sampled agent truncated exactly once, at step 1,176
     env.close()
 
 

@@ -190,9 +190,40 @@ def test_load_reference_sb3_zip_infers_architecture(tmp_path, kind):
            else ActorCriticPolicy(net_arch=arch))
     p = _sb3_style_zip(tmp_path / "rppo_hp1_s1234_view10.zip", pol)
     got, data = load_checkpoint(p)
-    assert data == {"sb3": True} and type(got) is type(pol)
+    assert data == {"sb3": True, "sb3_version": "2.3.2"} and type(got) is type(pol)
     sd, sd2 = pol.state_dict(), got.state_dict()
     assert sd.keys() == sd2.keys() and all(torch.equal(sd[k], sd2[k]) for k in sd)
+
+
+def test_unknown_voxnav_checkpoint_format_is_refused(tmp_path):
+    """A voxnav zip of another format version fails loudly instead of
+    loading through the SB3 shape-inference route (which would drop
+    num_timesteps, hyperparameters and policy_kwargs)."""
+    import json
+    import zipfile
+    from voxnav.checkpoint import load_checkpoint, save_checkpoint
+    from voxnav.policy import ActorCriticPolicy
+    torch.manual_seed(3)
+    pol = ActorCriticPolicy(net_arch=dict(pi=[16], vf=[16]))
+    p = tmp_path / "a.zip"
+    save_checkpoint(p, pol, num_timesteps=7)
+    q = tmp_path / "b.zip"
+    with zipfile.ZipFile(p) as zi, zipfile.ZipFile(q, "w") as zo:
+        for n in zi.namelist():
+            b = zi.read(n)
+            if n == "data":
+                d = json.loads(b)
+                d["format"] = "voxnav-sb3-layout-999"
+                b = json.dumps(d).encode()
+            zo.writestr(n, b)
+    with pytest.raises(ValueError, match="format"):
+        load_checkpoint(q)
+    r = tmp_path / "c.zip"                                   # neither voxnav nor SB3
+    with zipfile.ZipFile(p) as zi, zipfile.ZipFile(r, "w") as zo:
+        zo.writestr("data", json.dumps({"x": 1}))
+        zo.writestr("policy.pth", zi.read("policy.pth"))
+    with pytest.raises(ValueError, match="neither"):
+        load_checkpoint(r)
 
 
 def test_policy_state_load_is_strict():

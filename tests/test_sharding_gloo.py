@@ -46,14 +46,19 @@ def _worker(rank, world, port, q):
         bufs = {"obs": torch.from_numpy(r["obs"]), "reward": torch.from_numpy(r["reward"]),
                 "terminated": torch.from_numpy(r["terminated"]), "truncated": torch.from_numpy(r["truncated"])}
         g = allgather_rollout(bufs)
+        g_flat = allgather_rollout({"r": bufs["reward"]}, flat=True)["r"]
         slowest = max_over_ranks(float(rank + 1))
         if rank == 0:
             full = oracle_env(SRC, L, n_agents=N_LOCAL * world).run_random(
                 42 + np.arange(N_LOCAL * world), policy_seed=3, K=K, seed_stride=N_LOCAL * world)
-            ok = (g["obs"].numpy().tobytes() == full["obs"].tobytes()
-                  and np.array_equal(g["reward"].numpy(), full["reward"])
-                  and np.array_equal(g["terminated"].numpy(), full["terminated"])
-                  and np.array_equal(g["truncated"].numpy(), full["truncated"])
+            # [K, world, n_local, ...] views in global-id order
+            flat = lambda t: t.reshape(K, N_LOCAL * world, *t.shape[3:]).numpy()  # noqa: E731
+            ok = (tuple(g["obs"].shape) == (K, world, N_LOCAL, 80)
+                  and g["obs"].numpy().tobytes() == full["obs"].tobytes()
+                  and np.array_equal(flat(g["reward"]), full["reward"])
+                  and np.array_equal(flat(g["terminated"]), full["terminated"])
+                  and np.array_equal(flat(g["truncated"]), full["truncated"])
+                  and np.array_equal(g_flat.numpy(), full["reward"])
                   and slowest == float(world))
             q.put(("ok" if ok else "mismatch", int(full["truncated"].sum())))
         dist.barrier()

@@ -169,6 +169,76 @@ def _rollout_vs_oracle(src, L, N, K):
         np.testing.assert_array_equal(b, oenv.belief(i))
 
 
+def _bench_shaped_run(N, sample, K, F=128, src="box:32x32x8", L=4, policy_seed=42):
+    """The bench's simpleEnv call: ``step_random(out=...)`` in F-step launches
+    into a reused [F, N, 6L+7] chunk, f32 reward, no action record; the
+    sampled agents compared with the oracle launch by launch (the per-agent
+    reset draw-ahead is carried across launches)."""
+    from voxnav.env import Rollout
+    env = make_env(src, L, n=N, autoreset=True)
+    assert env.kernel_label(F) == "simple_pipe_kernel<4>"
+    dev = env.device
+    D = env.obs_dim
+    out = Rollout(torch.empty((F, N, D), dtype=torch.float32, device=dev),
+                  torch.empty((F, N), dtype=torch.float32, device=dev),
+                  torch.empty((F, N), dtype=torch.uint8, device=dev),
+                  torch.empty((F, N), dtype=torch.uint8, device=dev), None)
+    idx = torch.as_tensor(sample, device=dev)
+    gids = np.asarray(sample, dtype=np.int64)
+    oenv = oracle_env(src, L, n_agents=len(sample), variant=1)
+    env.reset(seed=42)
+    t, ends = 0, {"terminated": 0, "truncated": 0}
+    while t < K:
+        k = min(F, K - t)
+        env.step_random(k, policy_seed=policy_seed, t0=t,
+                        out=Rollout(out.obs[:k], out.reward[:k], out.terminated[:k], out.truncated[:k], None))
+        orc = oenv.run_random(42 + gids, policy_seed=policy_seed, K=k, t0=t, seed_stride=N, initial_reset=(t == 0),
+                              gids=gids, threads=8)
+        got = out.obs[:k].index_select(1, idx).cpu().numpy()
+        bad = np.argwhere((got.view(np.uint32) != orc["obs"].view(np.uint32)).any(-1))
+        assert bad.size == 0, f"obs mismatch at (step, sampled agent) {(bad[:5] + [t, 0]).tolist()}"
+        np.testing.assert_array_equal(out.reward[:k].index_select(1, idx).cpu().numpy(),
+                                      orc["reward"].astype(np.float32), err_msg=f"reward, steps {t}..{t + k}")
+        for f in ends:
+            g = getattr(out, f)[:k].index_select(1, idx).cpu().numpy()
+            np.testing.assert_array_equal(g, orc[f], err_msg=f"{f}, steps {t}..{t + k}")
+            ends[f] += int(g.sum())
+        t += k
+    st = env.export_state().index_select(0, idx).cpu().numpy()
+    bel = env.belief()
+    for j in range(0, len(sample), max(1, len(sample) // 32)):
+        o = oenv.state(j)
+        assert [o[f] for f in ("x", "y", "z", "facing", "last_action", "step_count", "visited_count", "bump_count",
+                               "done")] == [int(v) for v in st[j, :9]], f"state of agent {sample[j]}"
+        W, D_, H = oenv.rooms[o["room"]].whd
+        b = bel[int(sample[j]), :W, :D_, :H].cpu().numpy().astype(np.int64)
+        np.testing.assert_array_equal(b, oenv.belief(j), err_msg=f"belief of agent {sample[j]}")
+    env.close()
+    return ends
+
+
+def test_simple_bench_instantiation_all_agents(voxnav):
+    """The benched simpleEnv instantiation (simple_pipe_kernel<4>: 32x32x8,
+    L=4, 128-step launches, f32 reward) with 256 agents checked in full over
+    2,560 steps: goal terminations (a goal-seeking episode ends every ~2k
+    steps per agent under the random policy) and resets from the draw-ahead
+    inside and across launches."""
+    N = 256
+    ends = _bench_shaped_run(N, np.arange(N, dtype=np.int64), 2560)
+    assert ends["terminated"] > 0
+
+
+def test_simple_bench_instantiation_full_batch_sampled(voxnav):
+    """The bench's full batch (65,536 agents) in the same launches: one
+    sampled agent from every 64-agent block of the kernel (position varied),
+    2,560 steps."""
+    N = 65536
+    blocks = np.arange(N // 64, dtype=np.int64)
+    sample = blocks * 64 + (blocks * 41 + 9) % 64
+    ends = _bench_shaped_run(N, sample, 2560)
+    assert ends["terminated"] > 0
+
+
 def test_simple_step_actions_terminal_obs(voxnav):
     src, L, N, K = "box:8x8x4", 4, 200, 160
     env = make_env(src, L, n=N, autoreset=True)
