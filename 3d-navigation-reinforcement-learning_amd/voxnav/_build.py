@@ -18,7 +18,8 @@ CSRC = PROJECT / "csrc"
 INCLUDE = REPO / "include"
 LIBDIR = PKG / "_lib"
 LIB = LIBDIR / "libvoxnav.so"
-SOURCES = [CSRC / "voxnav_env.hip", CSRC / "voxnav_collect.hip", CSRC / "voxnav_learn.hip"]
+SOURCES = [CSRC / "voxnav_env.hip", CSRC / "voxnav_collect.hip", CSRC / "voxnav_learn.hip",
+           CSRC / "voxnav_policy_f32.hip"]
 HEADERS = [INCLUDE / "voxnav.h", CSRC / "vn_common.h"]
 ARCH = os.environ.get("VOXNAV_ARCH", "gfx950")
 

@@ -121,6 +121,23 @@ class _Weights:
         ext = policy.mlp_extractor
         self.pi = [(g(m.weight), g(m.bias)) for m in ext.linears("pi")]
         self.vf = [(g(m.weight), g(m.bias)) for m in ext.linears("vf")]
+        # f32 policy path on the f32 matrix cores (csrc/voxnav_policy_f32.hip):
+        # the LSTM step as one kernel (vn_lstm_fused_f32) and the MLP layers as
+        # Linear+Tanh kernels (vn_linear_f32, both branches per launch); needs
+        # H % 64 == 0, layer widths % 128 and inputs % 16, pi and vf the same widths
+        widths = [w.shape[0] for w, _ in self.pi]
+        self.f32mlp = (dtype == torch.float32 and widths == [w.shape[0] for w, _ in self.vf]
+                       and all(w.shape[0] % 128 == 0 and w.shape[1] % 16 == 0 for w, _ in self.pi + self.vf))
+        self.fused32 = self.recurrent and self.f32mlp and self.H % 64 == 0
+        if self.f32mlp:
+            self.pi_packed = [pack_linear_f32(w) for w, _ in self.pi]
+            self.vf_packed = [pack_linear_f32(w) for w, _ in self.vf]
+        if self.fused32:
+            od = la.weight_ih_l0.shape[1]
+            self.Kp32 = (od + 15) // 16 * 16 + self.H
+            self.lstm_packed = pack_lstm_f32([f(la.weight_ih_l0), f(lc.weight_ih_l0)],
+                                             [f(la.weight_hh_l0), f(lc.weight_hh_l0)])
+            self.bias32 = (self.b_ih + self.b_hh).contiguous()
         self.wa, self.ba = f(policy.action_net.weight), f(policy.action_net.bias)
         self.wv, self.bv = f(policy.value_net.weight).reshape(-1), f(policy.value_net.bias)
         self.A = self.wa.shape[0]
@@ -129,18 +146,27 @@ class _Weights:
             raise NotImplementedError("pi and vf latents must have the same width")
 
 
-def _mm_rocblas(a, b, out):
-    """``torch.mm`` through rocBLAS instead of hipBLASLt: the f32 input
-    projection (65,536 x 80 @ 80 x 2048, output-bound) runs 202 vs 240 us
-    there (scripts/blas_backend_bench.py); every other shape is as fast or
-    faster on hipBLASLt, so the preference is switched around this call only."""
-    bk = torch.backends.cuda
-    prev = bk.preferred_blas_library()
-    bk.preferred_blas_library("hipblas")
-    try:
-        torch.mm(a, b, out=out)
-    finally:
-        bk.preferred_blas_library(prev)
+def pack_lstm_f32(w_ih, w_hh) -> torch.Tensor:
+    """[W_ih | 0 | W_hh] of each LSTM in vn_lstm_fused_f32's layout
+    [n_lstm][H/64][Kp][4][64] (include/voxnav.h): element [b][ub][k][g][uu] =
+    Wcat_b[g*H + 64*ub + uu][k], W_ih in columns [0, obs_dim), W_hh in
+    [kx, kx + H), kx = obs_dim rounded up to 16."""
+    nl = len(w_ih)
+    G, od = w_ih[0].shape
+    H = w_hh[0].shape[1]
+    kx = (od + 15) // 16 * 16
+    Kp = kx + H
+    wc = torch.zeros((nl, G, Kp), dtype=torch.float32, device=w_ih[0].device)
+    for b in range(nl):
+        wc[b, :, :od] = w_ih[b]
+        wc[b, :, kx:kx + H] = w_hh[b]
+    return wc.view(nl, 4, H // 64, 64, Kp).permute(0, 2, 4, 1, 3).contiguous()
+
+
+def pack_linear_f32(w: torch.Tensor) -> torch.Tensor:
+    """W [Nout, K] in vn_linear_f32's layout [Nout/128][K][128]."""
+    n, k = w.shape
+    return w.detach().to(torch.float32).reshape(n // 128, 128, k).permute(0, 2, 1).contiguous()
 
 
 def _mlp(layers, x):
@@ -196,12 +222,15 @@ class RolloutCollector:
         self._boot_cnt = z(1, dt=torch.int32)
         self._last_values = z(N)
         self.recurrent = self.w.recurrent
+        # the f32 MLP kernels' per-layer outputs, [branch][rows][width]; sized
+        # for the larger of N and the bootstrap stash (the critic runs on it)
         if self.recurrent:
             H = self.w.H
             self.h = z(2, N, H)
             self.c = z(2, N, H)
-            self._gx = z(N, 2 * 4 * H, dt=self.cdt)
-            self._gh = z(2, N, 4 * H, dt=self.cdt)
+            if not self.w.fused32:     # gate pre-activations of the library-GEMM path
+                self._gx = z(N, 2 * 4 * H, dt=self.cdt)
+                self._gh = z(2, N, 4 * H, dt=self.cdt)
             self.h_bf = z(2, N, H, dt=torch.bfloat16) if self.bf16 else None   # GEMM copy of h
             self.fused = self.bf16 and self.w.fused
             self.h_bf2 = z(2, N, H, dt=torch.bfloat16) if self.fused else None  # fused step's output (ping-pong)
@@ -229,6 +258,11 @@ class RolloutCollector:
             self._stash_c = z(cap, self.w.H)
         # SB3 Monitor on every worker (train/Grid_Train.py:125): it sums the env's
         # f64 rewards, so the env step also writes them (voxnav.monitor)
+        if self.w.f32mlp:
+            rows = max(N, self._stash_cap)
+            self._lat32 = [z(2, rows, wt.shape[0]) for wt, _ in self.w.vf]
+        if self.recurrent and self.w.fused32:
+            self._h_alt = z(2, N, self.w.H)           # ping-pong partner of self.h outside collect()
         self.monitor = EpisodeMonitor(self.lib, N, T, dev) if monitor else None
         self._r64 = z(N, dt=torch.float64) if monitor else None
         # learn() start: reset every env, episode_starts = ones, zero states
@@ -278,6 +312,30 @@ class RolloutCollector:
                                                          _p(self.h_bf2), _p(self._hs[t + 1]), 2, self.N, w.H,
                                                          self._stream()), "vn_lstm_fused_bf16_masked")
 
+    def _lstm32(self, obs, h_in, c_in, start, c_out, h_out, nl, M, b0):
+        w = self.w
+        _native.check(self.lib.vn_lstm_fused_f32(_p(obs), obs.shape[1], _p(h_in), _p(w.lstm_packed[b0:b0 + nl]),
+                                                 w.Kp32, _p(w.bias32[b0:b0 + nl]), _p(c_in), _p(start), _p(c_out),
+                                                 _p(h_out), nl, M, w.H, self._stream()), "vn_lstm_fused_f32")
+
+    def _mlp32(self, x_pi, x_vf, M):
+        """Both MLP branches (or the value branch alone when x_pi is None),
+        layer by layer through vn_linear_f32 into the collector's latent
+        buffers; returns (lat_pi, lat_vf)."""
+        w = self.w
+        br = [(x_pi, w.pi_packed, w.pi, 0)] if x_pi is not None else []
+        br.append((x_vf, w.vf_packed, w.vf, 1))
+        xs = [b[0] for b in br]
+        for li, (wt, _) in enumerate(w.vf):
+            nout, k = wt.shape
+            ys = [self._lat32[li][b[3]][:M] for b in br]
+            arr = lambda ts: (C.c_void_p * 2)(*[t.data_ptr() for t in ts])  # noqa: E731
+            _native.check(self.lib.vn_linear_f32(len(br), arr(xs), xs[0].stride(0), arr([b[1][li] for b in br]),
+                                                 arr([b[2][li][1] for b in br]), arr(ys), M, k, nout, 1,
+                                                 self._stream()), "vn_linear_f32")
+            xs = ys
+        return (xs[0] if x_pi is not None else None), xs[-1]
+
     def hidden_state(self):
         """(h, c) f32 [2, N, H] of the (actor, critic) LSTMs after the last step
         (h from its bf16 copy on the fused bf16 path)."""
@@ -299,6 +357,25 @@ class RolloutCollector:
             lat_vf = _mlp(w.vf, self.h_bf[1])
             self._head(lat_pi, lat_vf, N, self.t_global, self.actions[t], self.values[t], self.log_probs[t])
             return
+        if self.recurrent and self.w.fused32:
+            # f32 on the matrix cores: the LSTM step (gates in registers) and the
+            # Linear+Tanh layers; inside collect() (h, c) live in the buffer only
+            # and the kernel applies the episode-start mask on read; step 0
+            # reads the current, already masked state
+            if in_rollout and self.store:
+                hin, c_in, start = (self.h, self.c, None) if t == 0 else (self._hs[t], self._cs[t], self._starts[t])
+                h_out, c_out = self._hs[t + 1], self._cs[t + 1]
+                self._lstm32(obs, hin, c_in, start, c_out, h_out, 2, N, 0)
+            else:
+                h_out = self._h_alt
+                self._lstm32(obs, self.h, self.c, None, self.c, h_out, 2, N, 0)
+                if self.store:
+                    self._hs[t + 1].copy_(h_out)
+                    self._cs[t + 1].copy_(self.c)
+                self.h, self._h_alt = h_out, self.h
+            lat_pi, lat_vf = self._mlp32(h_out[0], h_out[1], N)
+            self._head(lat_pi, lat_vf, N, self.t_global, self.actions[t], self.values[t], self.log_probs[t])
+            return
         x = obs if not self.bf16 else obs.to(self.cdt)
         if self.recurrent and in_rollout and self.store and not self.bf16:
             # f32 inside collect(): (h, c) live in the buffer only; the products
@@ -308,7 +385,7 @@ class RolloutCollector:
             H = w.H
             hin, c_in, start = (self.h, self.c, self._no_start) if t == 0 else \
                 (self._hs[t], self._cs[t], self._starts[t])
-            _mm_rocblas(x, w.w_ih_cat.t(), self._gx)
+            torch.mm(x, w.w_ih_cat.t(), out=self._gx)
             torch.mm(hin[0], w.w_hh[0].t(), out=self._gh[0])
             torch.mm(hin[1], w.w_hh[1].t(), out=self._gh[1])
             h_out = self._hs[t + 1]
@@ -328,8 +405,11 @@ class RolloutCollector:
             x_pi, x_vf = (self.h_bf[0], self.h_bf[1]) if self.bf16 else (self.h[0], self.h[1])
         else:
             x_pi = x_vf = x
-        lat_pi = _mlp(w.pi, x_pi)
-        lat_vf = _mlp(w.vf, x_vf)
+        if w.f32mlp:
+            lat_pi, lat_vf = self._mlp32(x_pi, x_vf, N)
+        else:
+            lat_pi = _mlp(w.pi, x_pi)
+            lat_vf = _mlp(w.vf, x_vf)
         self._head(lat_pi, lat_vf, N, self.t_global, self.actions[t], self.values[t], self.log_probs[t])
 
     def _critic(self, obs: torch.Tensor, h: Optional[torch.Tensor], c: Optional[torch.Tensor], out: torch.Tensor):
@@ -340,6 +420,14 @@ class RolloutCollector:
             h_out = torch.empty((M, w.H), dtype=torch.bfloat16, device=self.device)
             self._fused(obs.contiguous(), h.contiguous(), c, h_out, None, None, 1, M, 1)
             self._head(None, _mlp(w.vf, h_out), M, 0, None, out, None)
+            return
+        if self.recurrent and w.fused32:
+            h_out = torch.empty((M, w.H), dtype=torch.float32, device=self.device)
+            self._lstm32(obs.contiguous(), h.contiguous(), c, None, c, h_out, 1, M, 1)
+            self._head(None, self._mlp32(None, h_out, M)[1], M, 0, None, out, None)
+            return
+        if not self.recurrent and w.f32mlp:
+            self._head(None, self._mlp32(None, obs.contiguous(), M)[1], M, 0, None, out, None)
             return
         x = obs if not self.bf16 else obs.to(self.cdt)
         if self.recurrent:

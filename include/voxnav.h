@@ -248,6 +248,47 @@ int vn_lstm_fused_bf16_masked(const float *x, int32_t obs_dim, const uint16_t *h
                               uint16_t *h_out, float *h_store, int32_t n_lstm, int32_t N, int32_t H, void *stream);
 
 /*
+ * The whole LSTM step of the f32 (reference-dtype) policy path on the f32
+ * matrix cores (v_mfma_f32_32x32x2_f32, exact f32 FMA chains): the gate GEMM
+ * [x | h] @ [W_ih | W_hh]^T for n_lstm LSTMs with the cell update as its
+ * epilogue, so the 4H gate pre-activations never reach memory
+ * (RecurrentActorCriticPolicy._process_sequence for actor and critic,
+ * sb3_contrib; replaces the two library GEMMs +
+ * vn_lstm_cell_masked of one collector step).
+ *   x        f32 [N][obs_dim], 16-byte aligned when obs_dim % 4 == 0
+ *   h_in     f32 [n_lstm][N][H], != h_out; with start, rows n with
+ *            start[n] != 0 are read as zero (the (1 - episode_start) mask)
+ *   w_packed f32 [n_lstm][H/64][Kp][4][64]: element [b][ub][k][g][uu] =
+ *            Wcat_b[g*H + 64*ub + uu][k], Wcat_b = [W_ih | 0 | W_hh] with
+ *            W_ih in columns [0, obs_dim), W_hh in [kx, kx + H), kx =
+ *            obs_dim rounded up to 16, Kp = kx + H
+ *   bias     f32 [n_lstm][4H] = b_ih + b_hh
+ *   c_in     f32 [n_lstm][N][H] (masked like h_in when start != NULL); may be
+ *            c_out (in-place state)
+ *   c_out, h_out  f32 [n_lstm][N][H]: the new state
+ *   start    f32 [N] or NULL
+ * H must be a multiple of 64.
+ */
+int vn_lstm_fused_f32(const float *x, int32_t obs_dim, const float *h_in, const float *w_packed, int32_t Kp,
+                      const float *bias, const float *c_in, const float *start, float *c_out, float *h_out,
+                      int32_t n_lstm, int32_t N, int32_t H, void *stream);
+
+/*
+ * One Linear layer (+ Tanh when tanh_act) of the policy's pi / vf MLPs
+ * (MlpExtractor, net_arch [256, 256, 128] with Tanh, train/Grid_Train.py:68-80)
+ * for n_branch (1 or 2) branches in one launch, on the f32 matrix cores with
+ * the bias and Tanh in the epilogue:  y[i] = tanh(x[i] @ W_i^T + b_i).
+ *   x[i]        f32 [M][K] rows with row stride ldx (>= K, % 4), 16-byte aligned
+ *   w_packed[i] f32 [Nout/128][K][128]: element [cb][k][j] = W_i[128*cb + j][k]
+ *   bias[i]     f32 [Nout];  y[i]  f32 [M][Nout]
+ * K a multiple of 16, Nout a multiple of 128.  x, w_packed, bias and y are
+ * host arrays of n_branch device pointers.
+ */
+int vn_linear_f32(int32_t n_branch, const float *const *x, int64_t ldx, const float *const *w_packed,
+                  const float *const *bias, float *const *y, int32_t M, int32_t K, int32_t Nout, int32_t tanh_act,
+                  void *stream);
+
+/*
  * Action and value heads + Categorical draw (ActorCriticPolicy action_net /
  * value_net and distribution.get_actions / log_prob).
  *   latent_pi [N][P] (NULL: value only), latent_vf [N][P] (NULL: no value)

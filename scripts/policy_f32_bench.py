@@ -1,0 +1,122 @@
+#!/usr/bin/env python3
+"""Time the f32 policy step pieces at the C4 shape (65,536 agents, LSTM 256,
+pi/vf [256, 256, 128]) on the f32 matrix cores vs the library-GEMM path,
+HIP events on the current stream:
+
+  lstm    vn_lstm_fused_f32 (both LSTMs, masked rollout entry) vs
+          x @ W_ih^T + 2 x h @ W_hh^T (torch.mm) + vn_lstm_cell_masked
+  mlp     3 x vn_linear_f32 (both branches per launch, bias + Tanh fused) vs
+          6 x (torch.addmm + tanh_)
+
+Prints one JSON line; TFLOP/s against the 157.3 TF/s f32 matrix peak."""
+import ctypes as C
+import json
+import sys
+from pathlib import Path
+
+REPO = Path(__file__).resolve().parent.parent
+sys.path.insert(0, str(REPO / "3d-navigation-reinforcement-learning_amd"))
+import torch  # noqa: E402
+
+from voxnav import _native  # noqa: E402
+from voxnav.collector import pack_linear_f32, pack_lstm_f32  # noqa: E402
+
+PEAK = 157.3
+
+
+def timed(fn, reps=20):
+    for _ in range(3):
+        fn()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        fn()
+    e1.record()
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) / reps * 1e3   # us
+
+
+def main():
+    lib = _native.load()
+    dev = "cuda:0"
+    B, N, H, od = 2, int(sys.argv[1]) if len(sys.argv) > 1 else 65536, 256, 80
+    g = torch.Generator(device=dev).manual_seed(0)
+    r = lambda *s, sc=1.0: (torch.rand(s, device=dev, generator=g) - 0.5) * sc  # noqa: E731
+    x = r(N, od)
+    w_ih = [r(4 * H, od, sc=0.2) for _ in range(B)]
+    w_hh = [r(4 * H, H, sc=0.2) for _ in range(B)]
+    bias = r(B, 4 * H)
+    hin, cin = r(B, N, H), r(B, N, H)
+    hout, cout = torch.empty_like(hin), torch.empty_like(cin)
+    start = (torch.rand(N, device=dev, generator=g) < 0.02).float()
+    wp = pack_lstm_f32(w_ih, w_hh)
+    Kp = (od + 15) // 16 * 16 + H
+    p = lambda t: C.c_void_p(t.data_ptr())  # noqa: E731
+    st = lambda: C.c_void_p(torch.cuda.current_stream().cuda_stream)  # noqa: E731
+
+    def fused():
+        assert lib.vn_lstm_fused_f32(p(x), od, p(hin), p(wp), Kp, p(bias), p(cin), p(start), p(cout), p(hout), B, N,
+                                     H, st()) == 0
+    wcat = torch.cat(w_ih, 0)
+    gx = torch.empty((N, B * 4 * H), device=dev)
+    gh = torch.empty((B, N, 4 * H), device=dev)
+    zb = torch.zeros_like(bias)
+
+    def library():
+        torch.mm(x, wcat.t(), out=gx)
+        for b in range(B):
+            torch.mm(hin[b], w_hh[b].t(), out=gh[b])
+        assert lib.vn_lstm_cell_masked(p(gx), 8 * H, p(gh), p(bias), p(zb), p(cin), p(start), p(hout), p(cout), B,
+                                       N, H, st()) == 0
+    lstm_flop = 2 * B * N * (od + H) * 4 * H
+    out = {"N": N}
+    for name, fn in (("lstm_fused_f32", fused), ("lstm_library", library)):
+        us = timed(fn)
+        out[name] = {"us": round(us, 1), "tflops": round(lstm_flop / us / 1e6, 1),
+                     "frac": round(lstm_flop / us / 1e6 / PEAK, 3)}
+
+    widths = [256, 256, 128]
+    ws, bs, wps = [], [], []
+    k = H
+    for w in widths:
+        ws.append([r(w, k, sc=0.2) for _ in range(B)])
+        bs.append([r(w) for _ in range(B)])
+        wps.append([pack_linear_f32(t) for t in ws[-1]])
+        k = w
+    lat = [[torch.empty((N, w), device=dev) for _ in range(B)] for w in widths]
+    arr = lambda ts: (C.c_void_p * 2)(*[t.data_ptr() for t in ts])  # noqa: E731
+
+    def mlp_kernels():
+        xs = [hout[0], hout[1]]
+        kk = H
+        for li, w in enumerate(widths):
+            assert lib.vn_linear_f32(2, arr(xs), kk, arr(wps[li]), arr(bs[li]), arr(lat[li]), N, kk, w, 1, st()) == 0
+            xs, kk = lat[li], w
+
+    def mlp_library():
+        for b in range(B):
+            y = hout[b]
+            for li in range(len(widths)):
+                y = torch.addmm(bs[li][b], y, ws[li][b].t())
+                y.tanh_()
+    mlp_flop = 0
+    k = H
+    for w in widths:
+        mlp_flop += 2 * B * N * k * w
+        k = w
+    for name, fn in (("mlp_linear_f32", mlp_kernels), ("mlp_library", mlp_library)):
+        us = timed(fn)
+        out[name] = {"us": round(us, 1), "tflops": round(mlp_flop / us / 1e6, 1),
+                     "frac": round(mlp_flop / us / 1e6 / PEAK, 3)}
+    # numerics: fused vs library on the same inputs
+    fused()
+    h1, c1 = hout.clone(), cout.clone()
+    library()
+    torch.cuda.synchronize()
+    out["lstm_max_abs_diff"] = {"h": float((h1 - hout).abs().max()), "c": float((c1 - cout).abs().max())}
+    print(json.dumps(out), flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -355,3 +355,83 @@ def test_fused_bf16_truncation_bootstrap_uses_post_step_state(voxnav):
         n_boot += len(ts)
         parity |= set((ts % 2).tolist())
     assert n_boot > 0 and parity == {0, 1}, "truncations at both even and odd steps"
+
+
+@pytest.mark.parametrize("N,od,masked,inplace", [(300, 80, False, False), (257, 80, True, False),
+                                                 (130, 31, True, False), (128, 80, False, True)])
+def test_fused_f32_lstm_exact_mapping(voxnav, N, od, masked, inplace):
+    """vn_lstm_fused_f32 (v_mfma_f32_32x32x2_f32) against a float64
+    restatement on small-integer / 8 data, so the f32 gate sums are exact and
+    any row / unit / gate / k mix-up in the operand, packing or accumulator
+    maps shows; row tails (N % 128), obs_dim % 4 != 0 (scalar x loads), the
+    episode-start mask (h rows and c of starting agents read as zero) and the
+    in-place state (c_in == c_out)."""
+    import ctypes as C
+    from voxnav.collector import pack_lstm_f32
+    lib = voxnav.load_library()
+    rng = np.random.default_rng(23 + N)
+    B, H = 2, 128
+    x = (rng.integers(-4, 5, size=(N, od)) / 8.0).astype(np.float32)
+    h_in = (rng.integers(-4, 5, size=(B, N, H)) / 8.0).astype(np.float32)
+    w_ih = (rng.integers(-3, 4, size=(B, 4 * H, od)) / 8.0).astype(np.float32)
+    w_hh = (rng.integers(-3, 4, size=(B, 4 * H, H)) / 8.0).astype(np.float32)
+    bias = (rng.integers(-8, 9, size=(B, 4 * H)) / 8.0).astype(np.float32)
+    c0 = rng.standard_normal((B, N, H)).astype(np.float32)
+    start = (rng.random(N) < 0.3).astype(np.float32)
+    dev = "cuda:0"
+    t = lambda a: torch.as_tensor(a, device=dev).contiguous()  # noqa: E731
+    wp = pack_lstm_f32([t(w_ih[b]) for b in range(B)], [t(w_hh[b]) for b in range(B)])
+    Kp = (od + 15) // 16 * 16 + H
+    tc_in = t(c0)
+    tc_out = tc_in if inplace else torch.full((B, N, H), float("nan"), device=dev)
+    th_out = torch.full((B, N, H), float("nan"), device=dev)
+    p = lambda a: None if a is None else C.c_void_p(a.data_ptr())  # noqa: E731
+    tx, th = t(x), t(h_in)
+    assert lib.vn_lstm_fused_f32(p(tx), od, p(th), p(wp), Kp, p(t(bias)), p(tc_in), p(t(start)) if masked else None,
+                                 p(tc_out), p(th_out), B, N, H, None) == 0
+    torch.cuda.synchronize()
+    keep = (start == 0)[None, :, None] if masked else np.ones((1, N, 1), bool)
+    hm = np.where(keep, h_in, 0.0)
+    cm = np.where(keep, c0, 0.0)
+    pre = (np.einsum("nk,bgk->bng", x.astype(np.float64), w_ih.astype(np.float64))
+           + np.einsum("bnk,bgk->bng", hm.astype(np.float64), w_hh.astype(np.float64)) + bias[:, None, :])
+    sg = lambda v: 1.0 / (1.0 + np.exp(-v))  # noqa: E731
+    i, f, g, o = (pre[..., k * H:(k + 1) * H] for k in range(4))
+    c1 = sg(f) * cm + sg(i) * np.tanh(g)
+    h1 = sg(o) * np.tanh(c1)
+    np.testing.assert_allclose(tc_out.cpu().numpy(), c1, atol=2e-6, rtol=2e-6)
+    np.testing.assert_allclose(th_out.cpu().numpy(), h1, atol=2e-6, rtol=2e-6)
+    if not inplace:
+        assert torch.equal(tc_in, t(c0)) and torch.equal(th, t(h_in))     # inputs not written
+    assert lib.vn_lstm_fused_f32(p(tx), od, p(th), p(wp), Kp, p(t(bias)), p(tc_in), None, p(tc_out), p(th), B, N, H,
+                                 None) != 0                                  # h_in == h_out refused
+
+
+@pytest.mark.parametrize("M,K,nout,nb", [(65, 256, 256, 2), (300, 80, 128, 1), (1024, 256, 384, 2)])
+def test_linear_f32_exact_mapping(voxnav, M, K, nout, nb):
+    """vn_linear_f32 (bias + Tanh epilogue, one or two branches per launch)
+    against float64 on exact data; the identity-activation form is bitwise
+    the exact sum."""
+    import ctypes as C
+    from voxnav.collector import pack_linear_f32
+    lib = voxnav.load_library()
+    rng = np.random.default_rng(M + K)
+    dev = "cuda:0"
+    xs = [(rng.integers(-4, 5, size=(M, K)) / 8.0).astype(np.float32) for _ in range(nb)]
+    ws = [(rng.integers(-3, 4, size=(nout, K)) / 16.0).astype(np.float32) for _ in range(nb)]
+    bs = [(rng.integers(-8, 9, size=nout) / 8.0).astype(np.float32) for _ in range(nb)]
+    tx = [torch.as_tensor(a, device=dev) for a in xs]
+    tw = [pack_linear_f32(torch.as_tensor(w, device=dev)) for w in ws]
+    tb = [torch.as_tensor(b, device=dev) for b in bs]
+    arr = lambda ts: (C.c_void_p * 2)(*[t.data_ptr() for t in ts])  # noqa: E731
+    for act in (1, 0):
+        ty = [torch.full((M, nout), float("nan"), device=dev) for _ in range(nb)]
+        assert lib.vn_linear_f32(nb, arr(tx), K, arr(tw), arr(tb), arr(ty), M, K, nout, act, None) == 0
+        torch.cuda.synchronize()
+        for i in range(nb):
+            ref = xs[i].astype(np.float64) @ ws[i].astype(np.float64).T + bs[i]
+            got = ty[i].cpu().numpy()
+            if act:
+                np.testing.assert_allclose(got, np.tanh(ref), atol=2e-7, rtol=2e-6)
+            else:
+                np.testing.assert_array_equal(got, ref.astype(np.float32))
