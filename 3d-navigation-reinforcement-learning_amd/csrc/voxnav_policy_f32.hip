@@ -42,7 +42,26 @@ namespace {
 
 typedef __attribute__((ext_vector_type(16))) float f32x16_t;
 
+#ifndef VN_PF_FAST
+#define VN_PF_FAST 1   // gate / Tanh nonlinearities on the hardware exp and rcp (|err| <= ~4e-7)
+#endif
+#ifndef VN_PF_DIAG
+#define VN_PF_DIAG 0   // timing diagnostics (results invalid): 1 no K loop, 2 no nonlinearities
+#endif
+#if VN_PF_FAST
+__device__ __forceinline__ float sigm_f32(float x) { return __frcp_rn(1.0f + __expf(-x)); }
+__device__ __forceinline__ float tanh_f32(float x) { return 1.0f - 2.0f * __frcp_rn(1.0f + __expf(2.0f * x)); }
+#else
 __device__ __forceinline__ float sigm_f32(float x) { return 1.0f / (1.0f + expf(-x)); }
+__device__ __forceinline__ float tanh_f32(float x) { return tanhf(x); }
+#endif
+#if VN_PF_DIAG == 2
+#define PF_SIGM(v) (v)
+#define PF_TANH(v) (v)
+#else
+#define PF_SIGM(v) sigm_f32(v)
+#define PF_TANH(v) tanh_f32(v)
+#endif
 
 constexpr int PF_KC = 16;          // K per LDS chunk (8 MFMA k-steps)
 constexpr int PF_AP = 128 + 4;     // A chunk pitch in floats (128 rows + pad)
@@ -70,24 +89,21 @@ __device__ __forceinline__ f32x16_t zero16() {
 //   c_in   f32 [n_lstm][N][H] (may equal c_out); c_out, h_out f32 [n_lstm][N][H]
 // ---------------------------------------------------------------------------
 constexpr int LS_ROWS = 128, LS_UNITS = 64, LS_COLS = 4 * LS_UNITS;
+constexpr int LS_RT = LS_ROWS / 64;             // 32-row MFMA tiles per wave = A float4 staged per thread
+constexpr int LS_AP = LS_ROWS + 4;              // A chunk pitch
 
-template <bool VEC_X, bool MASK>
-__global__ __launch_bounds__(256, 2) void lstm_fused_f32_kernel(const float *__restrict__ x, int obs_dim, int kx,
-                                                                const float *__restrict__ hin,
-                                                                const float *__restrict__ wp, int Kp,
-                                                                const float *__restrict__ bias, const float *c_in,
-                                                                const float *__restrict__ start, float *c_out,
-                                                                float *h_out, int N, int H, int ncombo) {
-    __shared__ float As[2][PF_KC][PF_AP];
-    __shared__ __attribute__((aligned(16))) float Bs[2][PF_KC][LS_COLS];
-    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-    const int ublocks = H / LS_UNITS;
-    const int ntiles = (N + LS_ROWS - 1) / LS_ROWS;
-    // 1-D grid over (row tile, combo = LSTM x 64-unit block).  Blocks go to the
-    // 8 XCDs round-robin by id; when the tile count allows, the combos of one
-    // row tile get ids of one residue mod 8 (same XCD, close in time), so the
-    // tile's x / h rows are fetched into that XCD's L2 once.
-    const int id = (int)blockIdx.x;
+// A work item: one (row tile, LSTM, 64-unit block).  Items are dealt to the
+// persistent blocks with stride gridDim.x (a multiple of 8), so a block's
+// items stay on its XCD; when the tile count allows, the items of one round on
+// one XCD are all the unit blocks of a few row tiles (their x / h rows are
+// fetched into that XCD's L2 once).
+struct LsItem {
+    int n_base, b, u_base;
+    const float *wblk, *hb;
+};
+
+__device__ __forceinline__ LsItem ls_decode(int id, int ntiles, int ncombo, int ublocks, int N, int H, int Kp,
+                                            const float *wp, const float *hin) {
     int tile, combo;
     if ((ntiles & 7) == 0) {
         const int xcd = id & 7, local = id >> 3;
@@ -97,36 +113,67 @@ __global__ __launch_bounds__(256, 2) void lstm_fused_f32_kernel(const float *__r
         tile = id / ncombo;
         combo = id - tile * ncombo;
     }
-    const int b = combo / ublocks, ub = combo - b * ublocks;
-    const int n_base = tile * LS_ROWS, u_base = ub * LS_UNITS;
-    const float *wblk = wp + ((size_t)b * ublocks + ub) * (size_t)Kp * LS_COLS;
-    const float *hb = hin + (size_t)b * N * H;
-    const int nchunks = Kp / PF_KC;
+    LsItem d;
+    d.b = combo / ublocks;
+    const int ub = combo - d.b * ublocks;
+    d.n_base = tile * LS_ROWS;
+    d.u_base = ub * LS_UNITS;
+    d.wblk = wp + ((size_t)d.b * ublocks + ub) * (size_t)Kp * LS_COLS;
+    d.hb = hin + (size_t)d.b * N * H;
+    return d;
+}
 
-    // A staging: thread covers (row q>>2, k 4(q&3) .. +3) for q = tid, tid + 256
-    int arow[2];
-    bool azero[2];
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-        const int q = tid + 256 * i;
-        const int n = min(n_base + (q >> 2), N - 1);
-        arow[i] = n;
-        azero[i] = MASK && start[n] != 0.0f;
-    }
+// Persistent: gridDim.x blocks (the co-resident count, 2 per CU) walk the
+// items.  The chunk stream runs on across items: the last chunk of an item
+// stages the next item's first chunk, and the epilogue's state stores drain
+// behind the next item's MFMAs.
+template <bool VEC_X, bool MASK>
+__global__ __launch_bounds__(256, 2) void lstm_fused_f32_kernel(const float *__restrict__ x, int obs_dim, int kx,
+                                                                const float *__restrict__ hin,
+                                                                const float *__restrict__ wp, int Kp,
+                                                                const float *__restrict__ bias, const float *c_in,
+                                                                const float *__restrict__ start, float *c_out,
+                                                                float *h_out, int N, int H, int ncombo, int n_items) {
+    __shared__ float As[2][PF_KC][LS_AP];
+    __shared__ __attribute__((aligned(16))) float Bs[2][PF_KC][LS_COLS];
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const int ublocks = H / LS_UNITS;
+    const int ntiles = (N + LS_ROWS - 1) / LS_ROWS;
+    const int nchunks = Kp / PF_KC;
     const int kq = (tid & 3) * 4;
+    const int wr = (wv & 1) * (LS_ROWS / 2), wu = (wv >> 1) * 32;
+    const int col = lane & 31, kh = lane >> 5;
+
+    int item = (int)blockIdx.x;
+    if (item >= n_items) return;
+    LsItem cur = ls_decode(item, ntiles, ncombo, ublocks, N, H, Kp, wp, hin);
+
+    // staging rows of the item being staged: thread covers (row q>>2, k 4(q&3)
+    // .. +3) for q = tid, tid + 256
+    int arow0, arow1;
+    bool az0 = false, az1 = false;
+#define LS_ROWS_FOR(d)                                                                                       \
+    {                                                                                                        \
+        arow0 = min((d).n_base + (tid >> 2), N - 1);                                                         \
+        arow1 = min((d).n_base + ((tid + 256) >> 2), N - 1);                                                 \
+        if (MASK) {                                                                                          \
+            az0 = start[arow0] != 0.0f;                                                                      \
+            az1 = start[arow1] != 0.0f;                                                                      \
+        }                                                                                                    \
+    }
     // staging registers, named (an indexed array lives in scratch); the loads
     // are unconditional from a selected address and the zeroing happens when
     // the registers are written to LDS, so nothing waits between issuing the
     // next chunk's loads and this chunk's MFMAs
     float4 ra0, ra1, rb0, rb1, rb2, rb3;
-#define LS_A_LOAD(dst, i)                                                                                    \
+#define LS_A_LOAD(dst, arow, hb_)                                                                            \
     {                                                                                                        \
         if (VEC_X) {                                                                                         \
-            const float *p_ = isx_ ? x + (size_t)arow[i] * obs_dim + min(k_, obs_dim - 4)                    \
-                                   : hb + (size_t)arow[i] * H + (k_ - kx);                                   \
+            const float *p_ = isx_ ? x + (size_t)(arow) * obs_dim + min(k_, obs_dim - 4)                     \
+                                   : (hb_) + (size_t)(arow) * H + (k_ - kx);                                 \
             dst = *reinterpret_cast<const float4 *>(p_);                                                     \
         } else {                                                                                             \
-            const float *p_ = isx_ ? x + (size_t)arow[i] * obs_dim : hb + (size_t)arow[i] * H - kx;          \
+            const float *p_ = isx_ ? x + (size_t)(arow) * obs_dim : (hb_) + (size_t)(arow) * H - kx;         \
             const int lim_ = isx_ ? obs_dim - 1 : 0x7fffffff;                                                \
             dst.x = p_[min(k_ + 0, lim_)];                                                                   \
             dst.y = p_[min(k_ + 1, lim_)];                                                                   \
@@ -134,18 +181,19 @@ __global__ __launch_bounds__(256, 2) void lstm_fused_f32_kernel(const float *__r
             dst.w = p_[min(k_ + 3, lim_)];                                                                   \
         }                                                                                                    \
     }
-#define LS_LOAD(ch)                                                                                          \
+    // chunk ch of the item d into the staging registers
+#define LS_LOAD(d, ch)                                                                                       \
     {                                                                                                        \
         const int k_ = (ch) * PF_KC + kq;                                                                    \
         const bool isx_ = (ch) * PF_KC < kx; /* block-uniform: a chunk is all x or all h (kx % 16 == 0) */   \
-        LS_A_LOAD(ra0, 0) LS_A_LOAD(ra1, 1)                                                                  \
-        const float4 *pb_ = reinterpret_cast<const float4 *>(wblk + (size_t)(ch) * PF_KC * LS_COLS) + tid;   \
+        LS_A_LOAD(ra0, arow0, (d).hb) LS_A_LOAD(ra1, arow1, (d).hb)                                          \
+        const float4 *pb_ = reinterpret_cast<const float4 *>((d).wblk + (size_t)(ch) * PF_KC * LS_COLS) + tid; \
         rb0 = pb_[0];                                                                                        \
         rb1 = pb_[256];                                                                                      \
         rb2 = pb_[512];                                                                                      \
         rb3 = pb_[768];                                                                                      \
     }
-#define LS_A_PUT(v, i)                                                                                       \
+#define LS_A_PUT(v, i, az)                                                                                   \
     {                                                                                                        \
         const int r_ = (tid + 256 * (i)) >> 2;                                                               \
         float4 v_ = v;                                                                                       \
@@ -154,7 +202,7 @@ __global__ __launch_bounds__(256, 2) void lstm_fused_f32_kernel(const float *__r
             if (k_ + 1 >= obs_dim) v_.y = 0.0f;                                                              \
             if (k_ + 2 >= obs_dim) v_.z = 0.0f;                                                              \
             if (k_ + 3 >= obs_dim) v_.w = 0.0f;                                                              \
-        } else if (MASK && azero[i]) {                                                                       \
+        } else if (MASK && (az)) {                                                                           \
             v_ = make_float4(0.f, 0.f, 0.f, 0.f);                                                            \
         }                                                                                                    \
         As[buf_][kq + 0][r_] = v_.x;                                                                         \
@@ -162,12 +210,13 @@ __global__ __launch_bounds__(256, 2) void lstm_fused_f32_kernel(const float *__r
         As[buf_][kq + 2][r_] = v_.z;                                                                         \
         As[buf_][kq + 3][r_] = v_.w;                                                                         \
     }
-#define LS_STORE(ch)                                                                                         \
+    // the staging registers (chunk ch) into LDS buffer bf
+#define LS_STORE(bf, ch)                                                                                     \
     {                                                                                                        \
-        const int buf_ = (ch) & 1;                                                                           \
+        const int buf_ = (bf);                                                                               \
         const int k_ = (ch) * PF_KC + kq;                                                                    \
         const bool isx_ = (ch) * PF_KC < kx;                                                                 \
-        LS_A_PUT(ra0, 0) LS_A_PUT(ra1, 1)                                                                    \
+        LS_A_PUT(ra0, 0, az0) LS_A_PUT(ra1, 1, az1)                                                          \
         float4 *pl_ = reinterpret_cast<float4 *>(&Bs[buf_][0][0]) + tid;                                     \
         pl_[0] = rb0;                                                                                        \
         pl_[256] = rb1;                                                                                      \
@@ -175,73 +224,123 @@ __global__ __launch_bounds__(256, 2) void lstm_fused_f32_kernel(const float *__r
         pl_[768] = rb3;                                                                                      \
     }
 
-    f32x16_t acc[2][4];
-#pragma unroll
-    for (int t = 0; t < 2; ++t)
-#pragma unroll
-        for (int g = 0; g < 4; ++g) acc[t][g] = zero16();
-    const int wr = (wv & 1) * 64, wu = (wv >> 1) * 32;
-    const int col = lane & 31, kh = lane >> 5;
+    f32x16_t acc[LS_RT][4];
+#define LS_RD(bf, s_, A0, A1, B0, B1, B2, B3)                                                                \
+    {                                                                                                        \
+        const int kk_ = 2 * (s_) + kh;                                                                       \
+        A0 = As[bf][kk_][wr + col];                                                                          \
+        A1 = As[bf][kk_][wr + 32 + col];                                                                     \
+        B0 = Bs[bf][kk_][wu + col];                                                                          \
+        B1 = Bs[bf][kk_][LS_UNITS + wu + col];                                                               \
+        B2 = Bs[bf][kk_][2 * LS_UNITS + wu + col];                                                           \
+        B3 = Bs[bf][kk_][3 * LS_UNITS + wu + col];                                                           \
+    }
+#define LS_MM(A0, A1, B0, B1, B2, B3)                                                                        \
+    {                                                                                                        \
+        acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(A0, B0, acc[0][0], 0, 0, 0);                        \
+        acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(A0, B1, acc[0][1], 0, 0, 0);                        \
+        acc[0][2] = __builtin_amdgcn_mfma_f32_32x32x2f32(A0, B2, acc[0][2], 0, 0, 0);                        \
+        acc[0][3] = __builtin_amdgcn_mfma_f32_32x32x2f32(A0, B3, acc[0][3], 0, 0, 0);                        \
+        acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(A1, B0, acc[1][0], 0, 0, 0);                        \
+        acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(A1, B1, acc[1][1], 0, 0, 0);                        \
+        acc[1][2] = __builtin_amdgcn_mfma_f32_32x32x2f32(A1, B2, acc[1][2], 0, 0, 0);                        \
+        acc[1][3] = __builtin_amdgcn_mfma_f32_32x32x2f32(A1, B3, acc[1][3], 0, 0, 0);                        \
+    }
+    // the MFMAs of one chunk in LDS buffer bf: two operand sets, k-step s+1's
+    // reads issued before k-step s's MFMAs (3 LDS reads -- one ds_read2 of A,
+    // two of B -- per k-step, enforced on the scheduler)
+#define LS_COMPUTE(bf)                                                                                       \
+    {                                                                                                        \
+        float pa0, pa1, pb0, pb1, pb2, pb3, qa0, qa1, qb0, qb1, qb2, qb3;                                    \
+        LS_RD(bf, 0, pa0, pa1, pb0, pb1, pb2, pb3)                                                           \
+        _Pragma("unroll") for (int s = 0; s < PF_KC / 2; s += 2) {                                           \
+            LS_RD(bf, s + 1, qa0, qa1, qb0, qb1, qb2, qb3)                                                   \
+            LS_MM(pa0, pa1, pb0, pb1, pb2, pb3)                                                              \
+            if (s + 2 < PF_KC / 2) LS_RD(bf, s + 2, pa0, pa1, pb0, pb1, pb2, pb3)                            \
+            LS_MM(qa0, qa1, qb0, qb1, qb2, qb3)                                                              \
+        }                                                                                                    \
+        __builtin_amdgcn_sched_group_barrier(0x100, 3, 0);                                                   \
+        _Pragma("unroll") for (int s = 0; s < PF_KC / 2; ++s) {                                              \
+            if (s + 1 < PF_KC / 2) __builtin_amdgcn_sched_group_barrier(0x100, 3, 0);                        \
+            __builtin_amdgcn_sched_group_barrier(0x008, 8, 0);                                               \
+        }                                                                                                    \
+    }
 
-    LS_LOAD(0)
-    LS_STORE(0)
+    LS_ROWS_FOR(cur)
+    LS_LOAD(cur, 0)
+    LS_STORE(0, 0)
     __syncthreads();
-    for (int ch = 0; ch < nchunks; ++ch) {
-        // the next chunk's loads, in flight during this chunk's MFMAs (the last
-        // iteration reloads its own chunk into the idle buffer: unconditional,
-        // so the staging stays in registers)
-        const int nx = ch + 1 < nchunks ? ch + 1 : ch;
-        LS_LOAD(nx)
+    int g = 0;        // chunks computed so far: chunk g sits in LDS buffer g & 1
+    for (;;) {
+#pragma unroll
+        for (int t = 0; t < LS_RT; ++t)
+#pragma unroll
+            for (int gg = 0; gg < 4; ++gg) acc[t][gg] = zero16();
+        const int nitem = item + (int)gridDim.x;
+        const bool more = nitem < n_items;
+        const LsItem nxt = more ? ls_decode(nitem, ntiles, ncombo, ublocks, N, H, Kp, wp, hin) : cur;
+        for (int ch = 0; ch < (VN_PF_DIAG == 1 ? 0 : nchunks - 1); ++ch) {
+            LS_LOAD(cur, ch + 1)
+            __builtin_amdgcn_sched_barrier(0);
+            LS_COMPUTE(g & 1)
+            LS_STORE((g + 1) & 1, ch + 1)
+            __syncthreads();
+            ++g;
+        }
+        // the item's last chunk: stage the next item's first chunk (this
+        // item's own first chunk again when there is none: into the idle
+        // buffer, unconditional) and load this item's cell states
+        LS_ROWS_FOR(nxt)
+        LS_LOAD(nxt, 0)
         __builtin_amdgcn_sched_barrier(0);
-        const int buf = ch & 1;
+        if (VN_PF_DIAG != 1) LS_COMPUTE(g & 1)
+        LS_STORE((g + 1) & 1, 0)
+        __syncthreads();
+        ++g;
+
+        // epilogue: lane holds unit u; gate gg of (row, u) in acc[t][gg][reg].
+        // A row tile's 16 states are loaded together before any store (vmcnt
+        // retires in order: a load issued after a store waits for it); the
+        // stores drain behind the next item's MFMAs
+        const int u = cur.u_base + wu + col;
+        const float *bb = bias + (size_t)cur.b * 4 * H;
+        const float bi = bb[u], bf = bb[H + u], bg = bb[2 * H + u], bo = bb[3 * H + u];
 #pragma unroll
-        for (int s = 0; s < PF_KC / 2; ++s) {
-            const int kk = 2 * s + kh;
-            const float a0 = As[buf][kk][wr + col], a1 = As[buf][kk][wr + 32 + col];
+        for (int t = 0; t < LS_RT; ++t) {
+            float cin[16];
 #pragma unroll
-            for (int g = 0; g < 4; ++g) {
-                const float bv = Bs[buf][kk][g * LS_UNITS + wu + col];
-                acc[0][g] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, bv, acc[0][g], 0, 0, 0);
-                acc[1][g] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, bv, acc[1][g], 0, 0, 0);
+            for (int reg = 0; reg < 16; ++reg) {
+                const int n = min(cur.n_base + wr + 32 * t + (reg & 3) + 8 * (reg >> 2) + 4 * kh, N - 1);
+                const float v = c_in[((size_t)cur.b * N + n) * H + u];
+                cin[reg] = (MASK && start[n] != 0.0f) ? 0.0f : v;      // the episode-start mask, on read
+            }
+#pragma unroll
+            for (int reg = 0; reg < 16; ++reg) {
+                const int n = cur.n_base + wr + 32 * t + (reg & 3) + 8 * (reg >> 2) + 4 * kh;
+                if (n < N) {
+                    const size_t so = ((size_t)cur.b * N + n) * H + u;
+                    const float cv = cin[reg];
+                    const float ig = PF_SIGM(acc[t][0][reg] + bi), fg = PF_SIGM(acc[t][1][reg] + bf);
+                    const float gg = PF_TANH(acc[t][2][reg] + bg), og = PF_SIGM(acc[t][3][reg] + bo);
+                    const float fc = fg * cv, ig2 = ig * gg;
+                    const float cn = fc + ig2;
+                    c_out[so] = cn;
+                    h_out[so] = og * PF_TANH(cn);
+                }
             }
         }
-        LS_STORE(nx)
-        __syncthreads();
+        if (!more) break;
+        item = nitem;
+        cur = nxt;
     }
+#undef LS_ROWS_FOR
 #undef LS_A_LOAD
 #undef LS_A_PUT
 #undef LS_LOAD
 #undef LS_STORE
-
-    // epilogue: lane holds unit u; gate g of (row, u) in acc[t][g][reg]
-    const int u = u_base + wu + col;
-    const float *bb = bias + (size_t)b * 4 * H;
-    const float bi = bb[u], bf = bb[H + u], bg = bb[2 * H + u], bo = bb[3 * H + u];
-#pragma unroll
-    for (int t = 0; t < 2; ++t) {
-        // the 16 states of this row tile loaded together before any store
-        // (vmcnt retires in order: a load issued after a store waits for it)
-        float cin[16];
-#pragma unroll
-        for (int reg = 0; reg < 16; ++reg) {
-            const int n = min(n_base + wr + 32 * t + (reg & 3) + 8 * (reg >> 2) + 4 * kh, N - 1);
-            const float v = c_in[((size_t)b * N + n) * H + u];
-            cin[reg] = (MASK && start[n] != 0.0f) ? 0.0f : v;
-        }
-#pragma unroll
-        for (int reg = 0; reg < 16; ++reg) {
-            const int n = n_base + wr + 32 * t + (reg & 3) + 8 * (reg >> 2) + 4 * kh;
-            if (n < N) {
-                const size_t so = ((size_t)b * N + n) * H + u;
-                const float ig = sigm_f32(acc[t][0][reg] + bi), fg = sigm_f32(acc[t][1][reg] + bf);
-                const float gg = tanhf(acc[t][2][reg] + bg), og = sigm_f32(acc[t][3][reg] + bo);
-                const float fc = fg * cin[reg], ig2 = ig * gg;
-                const float cn = fc + ig2;
-                c_out[so] = cn;
-                h_out[so] = og * tanhf(cn);
-            }
-        }
-    }
+#undef LS_RD
+#undef LS_MM
+#undef LS_COMPUTE
 }
 
 // ---------------------------------------------------------------------------
@@ -326,21 +425,53 @@ __global__ __launch_bounds__(256, 4) void linear_f32_kernel(LinearArgs a, int64_
     LN_LOAD(0)
     LN_STORE(0)
     __syncthreads();
-    for (int ch = 0; ch < nchunks; ++ch) {
+    for (int ch = 0; ch < (VN_PF_DIAG == 1 ? 0 : nchunks); ++ch) {
         const int nx = ch + 1 < nchunks ? ch + 1 : ch;
         LN_LOAD(nx)
         __builtin_amdgcn_sched_barrier(0);
         const int buf = ch & 1;
+#define LN_RD(s_, A0, A1, B0, B1)                                                                            \
+    {                                                                                                        \
+        const int kk_ = 2 * (s_) + kh;                                                                       \
+        A0 = As[buf][kk_][wr + col];                                                                         \
+        A1 = As[buf][kk_][wr + 32 + col];                                                                    \
+        B0 = Bs[buf][kk_][wc + col];                                                                         \
+        B1 = Bs[buf][kk_][wc + 32 + col];                                                                    \
+    }
+#define LN_MM(A0, A1, B0, B1)                                                                                \
+    {                                                                                                        \
+        acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(A0, B0, acc[0][0], 0, 0, 0);                        \
+        acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(A0, B1, acc[0][1], 0, 0, 0);                        \
+        acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(A1, B0, acc[1][0], 0, 0, 0);                        \
+        acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(A1, B1, acc[1][1], 0, 0, 0);                        \
+    }
+        float pa0, pa1, pb0, pb1;
+#if VN_PF_PREF
+        float qa0, qa1, qb0, qb1;
+        LN_RD(0, pa0, pa1, pb0, pb1)
+#pragma unroll
+        for (int s = 0; s < PF_KC / 2; s += 2) {
+            LN_RD(s + 1, qa0, qa1, qb0, qb1)
+            LN_MM(pa0, pa1, pb0, pb1)
+            if (s + 2 < PF_KC / 2) LN_RD(s + 2, pa0, pa1, pb0, pb1)
+            LN_MM(qa0, qa1, qb0, qb1)
+        }
+        // 2 LDS reads (ds_read2 of A, of B) per k-step, one k-step ahead of its 4 MFMAs
+        __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
 #pragma unroll
         for (int s = 0; s < PF_KC / 2; ++s) {
-            const int kk = 2 * s + kh;
-            const float a0 = As[buf][kk][wr + col], a1 = As[buf][kk][wr + 32 + col];
-            const float b0 = Bs[buf][kk][wc + col], b1 = Bs[buf][kk][wc + 32 + col];
-            acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b0, acc[0][0], 0, 0, 0);
-            acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b1, acc[0][1], 0, 0, 0);
-            acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b0, acc[1][0], 0, 0, 0);
-            acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b1, acc[1][1], 0, 0, 0);
+            if (s + 1 < PF_KC / 2) __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+            __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);
         }
+#else
+#pragma unroll
+        for (int s = 0; s < PF_KC / 2; ++s) {
+            LN_RD(s, pa0, pa1, pb0, pb1)
+            LN_MM(pa0, pa1, pb0, pb1)
+        }
+#endif
+#undef LN_RD
+#undef LN_MM
         LN_STORE(nx)
         __syncthreads();
     }
@@ -361,7 +492,7 @@ __global__ __launch_bounds__(256, 4) void linear_f32_kernel(LinearArgs a, int64_
                 const int n = n_base + wr + 32 * t + (reg & 3) + 8 * (reg >> 2) + 4 * kh;
                 if (n < M) {
                     const float v = acc[t][c][reg] + bj;
-                    y[(size_t)n * Nout + j] = TANH ? tanhf(v) : v;
+                    y[(size_t)n * Nout + j] = TANH ? PF_TANH(v) : v;
                 }
             }
     }
@@ -384,11 +515,18 @@ int vn_lstm_fused_f32(const float *x, int32_t obs_dim, const float *h_in, const 
          ((obs_dim & 3) == 0 ? reinterpret_cast<uintptr_t>(x) : 0)) & 15)
         return fail(VN_ERR_INVALID, "x / h_in / w_packed must be 16-byte aligned");
     const int ncombo = n_lstm * (H / LS_UNITS);
-    const dim3 grid((unsigned)((N + LS_ROWS - 1) / LS_ROWS) * (unsigned)ncombo);
+    const int n_items = (N + LS_ROWS - 1) / LS_ROWS * ncombo;
+    // persistent grid: the co-resident block count (2 per CU), a multiple of 8
+    // so a block's items stay on one XCD
+    int dev = 0, cus = 0;
+    VN_HIP(hipGetDevice(&dev));
+    VN_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+    const int slots = (2 * cus + 7) / 8 * 8;
+    const dim3 grid((unsigned)(n_items < slots ? n_items : slots));
 #define VN_LS_LAUNCH(VX, MK)                                                                                    \
     hipLaunchKernelGGL((lstm_fused_f32_kernel<VX, MK>), grid, dim3(256), 0, (hipStream_t)stream, x,             \
                        (int)obs_dim, kx, h_in, w_packed, (int)Kp, bias, c_in, start, c_out, h_out, (int)N, (int)H, \
-                       ncombo)
+                       ncombo, n_items)
     if ((obs_dim & 3) == 0) {
         if (start) VN_LS_LAUNCH(true, true);
         else VN_LS_LAUNCH(true, false);

@@ -206,6 +206,7 @@ class RolloutCollector:
             raise ValueError("policy_dtype must be 'f32' (the reference's) or 'bf16'")
         self.bf16 = policy_dtype == "bf16"
         self.cdt = torch.bfloat16 if self.bf16 else torch.float32
+        self._sp = None
         self.sync_weights()
         T, N, dev = self.n_steps, self.N, self.device
         z = lambda *s, dt=torch.float32: torch.zeros(s, dtype=dt, device=dev)  # noqa: E731
@@ -263,6 +264,16 @@ class RolloutCollector:
             self._lat32 = [z(2, rows, wt.shape[0]) for wt, _ in self.w.vf]
         if self.recurrent and self.w.fused32:
             self._h_alt = z(2, N, self.w.H)           # ping-pong partner of self.h outside collect()
+            self._crit_h = z(max(N, self._stash_cap), self.w.H)   # critic-only LSTM output (bootstrap, last values)
+        # per-rollout buffers allocated once (the returned RolloutBuffer views
+        # them until the next collect()): no allocator traffic between rollouts
+        self._adv = z(T, N)
+        self._ret = z(T, N)
+        self._tv = z(max(N, self._stash_cap))
+        self._zero = torch.zeros((), device=dev)
+        if self.recurrent:
+            self._crit_hin = z(N, self.w.H, dt=torch.bfloat16 if self.fused else torch.float32)
+            self._crit_c = z(N, self.w.H)
         self.monitor = EpisodeMonitor(self.lib, N, T, dev) if monitor else None
         self._r64 = z(N, dt=torch.float64) if monitor else None
         # learn() start: reset every env, episode_starts = ones, zero states
@@ -274,6 +285,8 @@ class RolloutCollector:
         self.w = _Weights(self.policy, self.device, self.cdt)
 
     def _stream(self):
+        if self._sp is not None:       # inside collect(): the stream it started on
+            return self._sp
         return C.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
 
     # -------------------------------------------------------------- policy
@@ -422,7 +435,7 @@ class RolloutCollector:
             self._head(None, _mlp(w.vf, h_out), M, 0, None, out, None)
             return
         if self.recurrent and w.fused32:
-            h_out = torch.empty((M, w.H), dtype=torch.float32, device=self.device)
+            h_out = self._crit_h[:M]
             self._lstm32(obs.contiguous(), h.contiguous(), c, None, c, h_out, 1, M, 1)
             self._head(None, self._mlp32(None, h_out, M)[1], M, 0, None, out, None)
             return
@@ -456,6 +469,14 @@ class RolloutCollector:
         """One rollout of n_steps.  The returned buffer views the collector's
         storage: it stays valid until the next ``collect()``."""
         T, N, lib = self.n_steps, self.N, self.lib
+        self._sp = None
+        self._sp = self._stream()
+        try:
+            return self._collect(T, N, lib)
+        finally:
+            self._sp = None
+
+    def _collect(self, T, N, lib):
         s = self._stream
         if self._carry:
             self._carry_over()
@@ -490,31 +511,34 @@ class RolloutCollector:
                 _p(self._stash_obs),
                 _p(self._stash_h) if rec else None, _p(self._stash_c) if rec else None, _p(self._stash_flat),
                 self._stash_cap, s()), "vn_collect_stash")
+            # episode_starts[t+1]; the (h, c) rows of finished agents are zeroed
+            # only where the next step reads the state arrays themselves (the
+            # f32 buffer path reads lstm_h / lstm_c[t+1] and masks on read)
+            zs = rec and not hbuf
             _native.check(lib.vn_episode_start(_p(self._term), _p(self._trunc), N, _p(self._starts[t + 1]),
-                                               _p(self.h) if self.recurrent else None,
-                                               _p(self.c) if self.recurrent else None,
-                                               _p(self.h_bf) if self.recurrent else None,
-                                               2 if self.recurrent else 0, self.w.H if self.recurrent else 0, s()),
-                          "vn_episode_start")
+                                               _p(self.h) if zs else None, _p(self.c) if zs else None,
+                                               _p(self.h_bf) if zs else None, 2 if zs else 0,
+                                               self.w.H if zs else 0, s()), "vn_episode_start")
             self.t_global += 1
             if (t + 1) % self._flush_every == 0 and t + 1 < T:
                 self._bootstrap(sb[t + 1])       # bounded stash: flush, restart at row 0
                 sb[t + 1].zero_()
         if csbuf:   # the current (masked) state: lstm_c[T] (lstm_h[T]) with the episode-start mask
             done = self._starts[T][None, :, None] != 0
-            self.c.copy_(torch.where(done, 0.0, self._cs[T]))
+            torch.where(done, self._zero, self._cs[T], out=self.c)      # no rollout-sized temporaries
             if hbuf:
-                self.h.copy_(torch.where(done, 0.0, self._hs[T]))
+                torch.where(done, self._zero, self._hs[T], out=self.h)
         # the truncation bootstrap of the rest of the rollout
         self._bootstrap(sb[T])
         # V(last obs) under the current (masked) critic state
         if self.recurrent:
             hsrc = self.h_bf if self.fused else self.h
-            self._critic(self._obs[T], hsrc[1].clone(), self.c[1].clone(), self._last_values)
+            self._crit_hin.copy_(hsrc[1])
+            self._crit_c.copy_(self.c[1])
+            self._critic(self._obs[T], self._crit_hin, self._crit_c, self._last_values)
         else:
             self._critic(self._obs[T], None, None, self._last_values)
-        adv = torch.empty((T, N), dtype=torch.float32, device=self.device)
-        ret = torch.empty((T, N), dtype=torch.float32, device=self.device)
+        adv, ret = self._adv, self._ret
         _native.check(lib.vn_gae(_p(self.rewards), _p(self.values), _p(self._starts), _p(self._last_values),
                                  _p(self._starts[T]), T, N, self.gamma, self.gae_lambda, _p(adv), _p(ret), s()),
                       "vn_gae")
@@ -535,7 +559,7 @@ class RolloutCollector:
         if M > self._stash_cap:     # cannot happen: at most (F-1)//min_free+1 truncations per agent in F steps
             raise RuntimeError(f"bootstrap stash overflow: {M} > {self._stash_cap}")
         if M:
-            tv = torch.empty(M, dtype=torch.float32, device=self.device)
+            tv = self._tv[:M]
             if self.recurrent:
                 self._critic(self._stash_obs[:M], self._stash_h[:M], self._stash_c[:M], tv)
             else:

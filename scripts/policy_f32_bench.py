@@ -38,7 +38,7 @@ def timed(fn, reps=20):
 
 
 def main():
-    lib = _native.load()
+    lib = _native.load() if len(sys.argv) < 3 else _native.load_variant(sys.argv[2])
     dev = "cuda:0"
     B, N, H, od = 2, int(sys.argv[1]) if len(sys.argv) > 1 else 65536, 256, 80
     g = torch.Generator(device=dev).manual_seed(0)

@@ -432,6 +432,6 @@ def test_linear_f32_exact_mapping(voxnav, M, K, nout, nb):
             ref = xs[i].astype(np.float64) @ ws[i].astype(np.float64).T + bs[i]
             got = ty[i].cpu().numpy()
             if act:
-                np.testing.assert_allclose(got, np.tanh(ref), atol=2e-7, rtol=2e-6)
+                np.testing.assert_allclose(got, np.tanh(ref), atol=1e-6, rtol=1e-5)   # hardware exp / rcp
             else:
                 np.testing.assert_array_equal(got, ref.astype(np.float32))
