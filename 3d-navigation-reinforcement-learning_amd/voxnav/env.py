@@ -236,6 +236,27 @@ class BatchedGridEnv:
         self._t = int(t0) + K
         return Rollout(obs, rew, te, tr, act)
 
+    def step_random_launcher(self, k_steps: int, policy_seed: int, t0: int, out: Rollout, reward_f64: bool = False):
+        """``step_random(k_steps, policy_seed, t0, out=out)`` prepared: the
+        argument checks and conversions happen here, and the returned
+        zero-argument callable is one C call on the current stream (for timed
+        loops whose host overhead per launch should be the launch itself)."""
+        if not self._was_reset:
+            raise RuntimeError("call reset() before step_random()")
+        K, N = int(k_steps), self.num_agents
+        obs, rew, te, tr, act = out
+        if tuple(obs.shape) != (K, N, self.obs_dim) or tuple(rew.shape) != (K, N) or not obs.is_contiguous():
+            raise ValueError("out: expected contiguous [K, N, obs_dim] obs and [K, N] rewards")
+        args = (self._h, int(policy_seed), int(t0), K, _ptr(act), _ptr(obs), None if reward_f64 else _ptr(rew),
+                _ptr(rew) if reward_f64 else None, _ptr(te), _ptr(tr), None, self._stream())
+        fn = self.lib.vn_step_random
+
+        def launch():
+            rc = fn(*args)
+            if rc:
+                _native.check(rc, "vn_step_random")
+        return launch
+
     def kernel_label(self, k_steps: int = 16, explicit_actions: bool = False, fast: bool = True) -> str:
         """Name of the kernel instantiation a step call of this shape launches
         (``k_steps=0``: reset; ``fast``: the rollout-buffer call)."""
