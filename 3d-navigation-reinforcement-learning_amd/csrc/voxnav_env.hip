@@ -1372,7 +1372,7 @@ __device__ __forceinline__ void group_reset(const Params &p, int8_t *map, uint64
 // min(center visit count, 25) (pen = min(0.5, 0.02 n) is 0.5 from n = 25 on:
 // 25 * 0.02 rounds to 0.5 in f64), 5 moved, 6 was_near_wall, 7 repeated
 // non-back move, 8 back after back, 9 explored, 10 done, 11 truncated.
-__device__ __forceinline__ float reward_of_events(uint32_t ev, double crash_penalty) {
+__device__ __forceinline__ double reward_of_events(uint32_t ev, double crash_penalty) {
     double r = -0.05;
     const double pen = (double)(ev & 31u) * 0.02;
     r -= (0.5 < pen) ? 0.5 : pen;
@@ -1386,7 +1386,7 @@ __device__ __forceinline__ float reward_of_events(uint32_t ev, double crash_pena
     if (ev & 512u) r += 1.0;
     if (ev & 1024u) r += 100.0;
     if (ev & 2048u) r += -5.0;
-    return (float)r;
+    return r;
 }
 
 constexpr int BLOCK = 256;
@@ -1413,8 +1413,9 @@ __device__ unsigned long long g_env_prof[16];
 // separate instantiation: with both sources in one loop the action register
 // may hold a pending load on entry to every step, and the compiler then waits
 // for all outstanding stores of the previous step before the move is known.
-// FAST: reward / terminated / truncated requested, reward64 / actions_out
-// not (the rollout-buffer call): no runtime pointer tests in the step loop.
+// FAST: reward / terminated / truncated requested, actions_out not (the
+// rollout-buffer call, reward64 optional): no runtime pointer tests in the
+// step loop.
 // PC: plane-set mode (see pset_fill).  36 KiB of LDS per 256-thread block
 // (u32 rows), so 16 waves fit a CU; measured full episode: 256 threads
 // 7.32, 128 7.21, 64 7.18 G env-steps/s.
@@ -1596,7 +1597,7 @@ __global__ __launch_bounds__(PCM ? VN_PC_BLOCK : BLOCK, PCM ? VN_PC_MIN_WAVES : 
         if (!(VN_ABLATE & 128u)) {
             const size_t o = kk * (size_t)p.N + (size_t)ai;
             if (FAST || p.reward) *(active ? p.reward + o : p.scratch + lane) = pr;
-            if (!FAST && p.reward64) *(active ? p.reward64 + o : reinterpret_cast<double *>(p.scratch + 128) + lane) = pr64;
+            if (p.reward64) *(active ? p.reward64 + o : reinterpret_cast<double *>(p.scratch + 128) + lane) = pr64;
             if (FAST || p.term) *(active ? p.term + o : reinterpret_cast<uint8_t *>(p.scratch + 64) + lane) = pte;
             if (FAST || p.trunc) *(active ? p.trunc + o : reinterpret_cast<uint8_t *>(p.scratch + 96) + lane) = ptr8;
         }
@@ -1868,7 +1869,7 @@ __global__ __launch_bounds__(PCM ? VN_PC_BLOCK : BLOCK, PCM ? VN_PC_MIN_WAVES : 
 
             if (q == 0 && !(VN_ABLATE & 128u)) {
                 if (FAST || p.reward) p.reward[row] = (float)r;
-                if (!FAST && p.reward64) p.reward64[row] = r;
+                if (p.reward64) p.reward64[row] = r;
                 if (FAST || p.term) p.term[row] = g.done ? 1 : 0;
                 if (FAST || p.trunc) p.trunc[row] = truncated ? 1 : 0;
             }
@@ -1921,9 +1922,10 @@ __global__ __launch_bounds__(PCM ? VN_PC_BLOCK : BLOCK, PCM ? VN_PC_MIN_WAVES : 
         const int s0 = (int)(tb & 3u);
         if (active && q >= s0 && q < s0 + jn && !(VN_ABLATE & 128u)) {
             const uint32_t ev = (uint32_t)(ev4 >> (16 * q)) & 0xffffu;
-            const float r = reward_of_events(ev, p.crash_penalty);
+            const double r = reward_of_events(ev, p.crash_penalty);
             const size_t o = (size_t)(kb + q - s0) * (size_t)p.N + (size_t)i;
-            p.reward[o] = r;
+            p.reward[o] = (float)r;
+            if (p.reward64) p.reward64[o] = r;       // the Monitor's exact f64 reward (once per 4-step block)
             p.term[o] = (uint8_t)((ev >> 10) & 1u);
             p.trunc[o] = (uint8_t)(ev >> 11);
         }
@@ -3661,7 +3663,9 @@ int launch_ph(int N, hipStream_t s, const Params &p) {
     const int bs = PCM ? VN_PC_BLOCK : BLOCK;
     const dim3 block((unsigned)bs);
     const dim3 grid((unsigned)(((size_t)N * GROUP + bs - 1) / bs));
-    const bool fast = p.reward && p.term && p.trunc && !p.reward64 && !p.actions_out;
+    // FAST: the rollout-buffer call (f32 reward, flags; the f64 reward for the
+    // Monitor optional, stored once per 4-step block); no action record
+    const bool fast = p.reward && p.term && p.trunc && !p.actions_out;
     if (RESET_ONLY)
         hipLaunchKernelGGL((env_kernel<PH, false, false, true, PCM>), grid, block, 0, s, p);
     else if (p.actions && fast)

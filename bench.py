@@ -78,6 +78,9 @@ def parse(argv=None):
                     help="CPU baseline sample per leg in seconds (0 = skip)")
     ap.add_argument("--simple", type=int, default=1,
                     help="also time the simpleEnv variant (envs/simpleEnv.py) on the same agents/room, L=4")
+    ap.add_argument("--room-sets", default="P2_training,P3_training",
+                    help="env-only legs on these reference room sets (random policy, same launches), or none")
+    ap.add_argument("--room-set-steps", type=int, default=1024, help="timed steps of each room-set leg")
     ap.add_argument("--collector", default="lstm,mlp",
                     help="policy-in-the-loop rollout collector legs: any of lstm (PPO-LSTM, P3_training, "
                          "BASELINE config C4) and mlp (PPO-MLP, P2_training, config C3), or none")
@@ -463,6 +466,9 @@ def roofline_block(bstep, N, F, steps, timed, kern_ms, traffic_rec, kernel_label
 
 
 def traffic_for(W, D, H, L, N, F, warmup, steps, prefix=""):
+    """The PMC traffic record of one window (profiles/pmc_traffic.json, written
+    by scripts/traffic_record.py), keyed by room (WxDxH, or a room-set name in
+    W with D = H = ""), L, N, launch size and window."""
     prof = REPO / "profiles" / "pmc_traffic.json"
     if not prof.exists():
         return None
@@ -470,7 +476,8 @@ def traffic_for(W, D, H, L, N, F, warmup, steps, prefix=""):
         pm = json.loads(prof.read_text())
     except ValueError:
         return None
-    return pm.get(f"{prefix}{W}x{D}x{H}_L{L}_N{N}_F{F}_W{warmup}_K{steps}")
+    room = f"{W}x{D}x{H}" if D != "" else str(W)
+    return pm.get(f"{prefix}{room}_L{L}_N{N}_F{F}_W{warmup}_K{steps}")
 
 
 # ---------------------------------------------------------------- main
@@ -620,6 +627,25 @@ def main():
         senv.close()
         del senv
 
+    # env-only legs on the room sets the reference trains on (train/Grid_Train.py:36-60):
+    # P2_training (BASELINE C3's rooms) and P3_training (C4's), the same random-policy
+    # window as the episode leg (the sets' rooms are 6-12 high: byte-mark kernels)
+    room_sets = {}
+    for rs in [r for r in args.room_sets.split(",") if r and r != "none"]:
+        from voxnav.rooms import load_archive_set
+        env = BatchedGridEnv(num_agents=N, rooms=load_archive_set(rs), local_map_length=args.L, autoreset=True,
+                             device=dev, agent_id_base=rank * N, seed_stride=N * world)
+        env.reset(seed=42)
+        rlab = env.kernel_label(F)
+        r_el, r_km, r_timed, _ = time_window(torch, dist, dev, world, env, N, F, 32, args.room_set_steps)
+        env.close()
+        del env
+        room_sets[rs] = {"value": round(N * world * args.room_set_steps / r_el, 1), "unit": "env-steps/s",
+                         "warmup": 32, "steps": args.room_set_steps, "steps_per_launch": F,
+                         "roofline": roofline_block(bstep, N, F, args.room_set_steps, r_timed, r_km,
+                                                   traffic_for(rs, "", "", args.L, N, F, 32, args.room_set_steps,
+                                                               prefix="set_"), rlab)}
+
     legs = {}
     kinds = [k for k in args.collector.split(",") if k and k != "none"]
     for kind in kinds:
@@ -656,6 +682,8 @@ def main():
             rec["drop_in_single_step"] = single   # vn_step-shaped call: one env step per launch
         if simple is not None:
             rec["simple_env"] = simple            # goal-seeking variant
+        if room_sets:
+            rec["env_room_sets"] = room_sets      # the reference's training room sets (P2 / P3)
         rec.update(legs)                          # policy in the loop
         if world == 1 and args.cpu_seconds > 0:
             rec["cpu_baseline"] = cpu_baseline((W, D, H), args.L, args.cpu_seconds)

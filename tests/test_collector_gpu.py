@@ -123,6 +123,7 @@ def test_collector_matches_oracle(voxnav, kind, T, rollouts, dtype, rooms, L, N,
     starts0 = np.ones(N, np.float32)
     h = c = None
     total_boot = 0
+    run_ret, run_len = np.zeros(N), np.zeros(N, np.int64)     # the Monitor's running sums (f64, step order)
     for r in range(rollouts):
         buf = col.collect()
         torch.cuda.synchronize()
@@ -137,6 +138,18 @@ def test_collector_matches_oracle(voxnav, kind, T, rollouts, dtype, rooms, L, N,
         h, c, starts0 = out["h"], out["c"], out["dones"]
         te, tr = rr["terminated"].astype(bool), rr["truncated"].astype(bool)
         total_boot += int((tr & ~te).sum())
+        # Monitor episodes: the env step's exact f64 rewards (the FAST kernel
+        # stores them with the f32 ones), summed in step order
+        want = []
+        for t in range(T):
+            run_ret += rr["reward"][t]
+            run_len += 1
+            for a in np.nonzero(te[t] | tr[t])[0]:
+                want.append((t, a, run_ret[a], run_len[a]))
+                run_ret[a], run_len[a] = 0.0, 0
+        got = col.monitor.last_episodes
+        assert got["agent"].tolist() == [w[1] for w in want] and got["step"].tolist() == [w[0] for w in want]
+        assert got["return"].cpu().numpy().tobytes() == np.array([w[2] for w in want], np.float64).tobytes()
         np.testing.assert_array_equal(buf.episode_starts.cpu().numpy(), out["episode_starts"])
         np.testing.assert_array_equal(buf.dones.cpu().numpy(), out["dones"])
         _close(buf.values.cpu(), out["values"], *tol["v"], "values")
