@@ -404,11 +404,12 @@ def learner_leg(args, torch, dist, dev, world, pol, buf, kind):
 
 
 # ---------------------------------------------------------------- env window
-def time_window(torch, dist, dev, world, env, N, F, warmup, steps, policy_seed=42):
+def time_window(torch, dist, dev, world, env, N, F, warmup, steps, policy_seed=42, events=True):
     """Reset already done by the caller.  Run exactly ``warmup`` untimed
     steps, then time exactly ``steps`` steps in launches of F (remainder
     last).  Returns (elapsed_s max-over-ranks, kernel_ms_total max-over-ranks,
-    launch sizes, out)."""
+    launch sizes, out).  ``events=False``: no HIP event records in the timed
+    region (kernel_ms is None)."""
     from voxnav.env import Rollout
     out = Rollout(torch.empty((F, N, env.obs_dim), dtype=torch.float32, device=dev),
                   torch.empty((F, N), dtype=torch.float32, device=dev),
@@ -433,14 +434,21 @@ def time_window(torch, dist, dev, world, env, N, F, warmup, steps, policy_seed=4
         dist.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
-    for (a, b), fn in zip(ev, fns):
-        a.record(stream)
-        fn()
-        b.record(stream)
+    if events:
+        for (a, b), fn in zip(ev, fns):
+            a.record(stream)
+            fn()
+            b.record(stream)
+    else:
+        for fn in fns:
+            fn()
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    if not events:
+        elapsed, = _max_over_ranks(torch, dist, dev, world, elapsed)
+        return elapsed, None, timed, out
     kern_ms = sum(a.elapsed_time(b) for a, b in ev)
     elapsed, kern_ms = _max_over_ranks(torch, dist, dev, world, elapsed, kern_ms)
     return elapsed, kern_ms, timed, out
@@ -554,13 +562,21 @@ def main():
         e.reset(seed=42)
         return e
 
-    # headline: a fresh env, exactly W warmup + K timed steps
+    # headline: a fresh env, exactly W warmup + K timed steps, nothing but the
+    # launches between the two synchronizes; the roofline's kernel time from
+    # HIP events on the launch stream over an identical re-run of the window
+    # (fresh env, same seeds: the same work; the event records would add
+    # ~15 us of host time to a one-launch window)
     env = make_env()
     label = env.kernel_label(F)
-    elapsed, kern_ms, timed, out = time_window(torch, dist, dev, world, env, N, F, args.warmup, args.steps)
+    elapsed, _, timed, out = time_window(torch, dist, dev, world, env, N, F, args.warmup, args.steps, events=False)
     assert torch.isfinite(out.obs).all().item()   # the trajectory buffer holds real observations
     env.close()
     del env, out
+    env = make_env()
+    ev_el, kern_ms, _, _ = time_window(torch, dist, dev, world, env, N, F, args.warmup, args.steps)
+    env.close()
+    del env
     roof = roofline_block(bstep, N, F, args.steps, timed, kern_ms,
                           traffic_for(W, D, H, args.L, N, F, args.warmup, args.steps), label)
     value = N * world * args.steps / elapsed
@@ -670,7 +686,9 @@ def main():
                        "steps_per_launch": F,
                        "window": f"fresh env, {args.warmup} untimed steps, then exactly {args.steps} timed steps "
                                  f"in {len(timed)} launches (episode steps {args.warmup + 1}-"
-                                 f"{args.warmup + args.steps}); roofline and traffic from these launches",
+                                 f"{args.warmup + args.steps}); roofline and traffic from the same launches of an "
+                                 f"identical re-run of the window timed with HIP events "
+                                 f"(wall {round(ev_el * 1e3 / args.steps, 5)} ms per step with the events)",
                        "parallelism": f"agent-sharded x{world} (no collective in the step)"},
             "roofline": roof,
         }
