@@ -140,6 +140,7 @@ struct Params {
     int sbits;               // simpleEnv bit-plane layout (rooms up to 64 x 64 x 31)
     int sb_aw;               // bit-plane kernel: agents per 64-lane wave (16, 32 or 64)
     uint32_t sy_off, sz_off, qz_off;
+    int sline;               // simpleEnv line layout (rooms up to 32 x 32 x 8; simple_line_kernel)
     const int8_t *wimg;      // plane-set mode (CubicEnv, PH 8, rooms <= 64 x 64): latent-wall room images
     int pcache;
     float *scratch;          // 4 KiB: targets of inactive lanes' output stores
@@ -1982,6 +1983,20 @@ __device__ __forceinline__ int rel_dir(int a, int facing) {
 // +x -> east(1), -x -> west(3), +y -> north(0), -y -> south(2)
 __device__ __forceinline__ int facing_of(int d) { return (int)((0x8Du >> (2 * d)) & 3u); }
 
+// obs slot of absolute direction j < 4 for facing f: slot k with rel_dir of
+// [fwd, left, right, back][k] == j
+constexpr uint32_t pack_obs_slot() {
+    uint32_t v = 0;
+    const int rel_of_slot[4] = {0, 3, 1, 2};   // forward, left, right, backward (action indices)
+    for (int f = 0; f < 4; ++f)
+        for (int k = 0; k < 4; ++k) v |= (uint32_t)k << (2 * (4 * f + kRelDir[rel_of_slot[k]][f]));
+    return v;
+}
+__device__ __forceinline__ int obs_slot(int j, int facing) {
+    return j >= 4 ? j : (int)((pack_obs_slot() >> (2 * (4 * facing + j))) & 3u);
+}
+
+
 // MT draws of simpleEnv's load_room (:350, :410-426): room, start (drawn if
 // absent or on a wall), goal (drawn if absent or on a wall).  Returns
 // (start | room<<24, goal).
@@ -2385,6 +2400,46 @@ __device__ __forceinline__ void sb_observe(const Params &p, const SPlanes &pl, A
     if (newq) g.move_mask |= 1u;
 }
 
+// sb_observe without divergent branches, for waves in which no lane has Q
+// marks or stands where a ray ends at the room's edge (ray record bit 17):
+// the rays in ABSOLUTE directions (ray axis, sign and S word fixed per ray),
+// each written at the obs slot the agent's facing gives it (obs_slot).  Per
+// ray cell s < L: the S bit if s < min(n, L), else 2 at s == n (wall), else -1
+// (:301-337).  Otherwise the wave takes sb_observe.
+template <int LMAX>
+__device__ __forceinline__ void sp_observe(const Params &p, const SPlanes &pl, Agent &g, const SRows &w, float *row) {
+    const bool slow = (g.move_mask & 1u) || ((w.rec.y >> 17) & 1u);
+    if (__builtin_expect(__ballot(slow) != 0ull, 0)) {
+        sb_observe<LMAX>(p, pl, g, w, row);
+        return;
+    }
+    const int L = p.L;
+#pragma unroll
+    for (int j = 0; j < 6; ++j) {
+        const uint32_t e8 = ray_e8(w.rec, j);
+        const int n = (int)(e8 & 0x7fu);
+        const int m = n < L ? n : L;
+        // t: bit s = the S bit of ray cell s + 1
+        uint32_t t;
+        if (j == 0) t = (uint32_t)(w.wx >> ((g.x + 1) & 63));
+        else if (j == 2) t = (uint32_t)(w.wy >> ((g.y + 1) & 63));
+        else if (j == 4) t = w.wz >> ((g.z + 1) & 31);
+        else if (j == 1) t = __builtin_bitreverse32((uint32_t)((w.wx << ((64 - g.x) & 63)) >> 32));
+        else if (j == 3) t = __builtin_bitreverse32((uint32_t)((w.wy << ((64 - g.y) & 63)) >> 32));
+        else t = __builtin_bitreverse32(w.wz << ((32 - g.z) & 31));
+        float *out = row + obs_slot(j, g.facing) * L;
+#pragma unroll
+        for (int s = 0; s < LMAX; ++s) {
+            if (s >= L) break;
+            const float fb = ((t >> s) & 1u) ? 1.0f : 0.0f;
+            const float pad = s == n ? 2.0f : -1.0f;
+            out[s] = s < m ? fb : pad;
+        }
+        row[6 * L + obs_slot(j, g.facing)] = (float)m * 0.25f;   // round(count * 0.25, 2) is exact
+    }
+    row[6 * L + 6] = (float)g.last_action;
+}
+
 __device__ __forceinline__ void sb_load_rows(const Params &p, const SPlanes &pl, const Agent &g, const Room &R,
                                              SRows &w) {
     w.wx = pl.sx[g.y * p.ph + g.z];
@@ -2437,9 +2492,14 @@ __device__ __forceinline__ void sb_reset_wave(const Params &p, const SPlanes &pl
         w.wx = 1ull << g.x;                                                     // :86
         w.wy = 1ull << g.y;
         w.wz = 1u << g.z;
-        pl.sx[g.y * p.ph + g.z] = w.wx;
-        pl.sy[g.x * p.ph + g.z] = w.wy;
-        pl.sz[g.x * p.pd + g.y] = w.wz;
+        if (p.sline) {                   // line layout: u32 SX[y][z], SY[x][z] (simple_line_kernel)
+            reinterpret_cast<uint32_t *>(pl.sx)[g.y * p.ph + g.z] = (uint32_t)w.wx;
+            reinterpret_cast<uint32_t *>(pl.sy)[g.x * p.ph + g.z] = (uint32_t)w.wy;
+        } else {
+            pl.sx[g.y * p.ph + g.z] = w.wx;
+            pl.sy[g.x * p.ph + g.z] = w.wy;
+            pl.sz[g.x * p.pd + g.y] = w.wz;
+        }
         w.rec = p.rays[R.ray_off + (uint32_t)((g.x * R.D + g.y) * R.H + g.z)];
         sb_observe<LMAX>(p, pl, g, w, row);
     }
@@ -2833,10 +2893,8 @@ __global__ __launch_bounds__(128) void simple_split_kernel(Params p) {
 // lane (same instructions, so the same time as for one lane): the resetting
 // lanes take their draw and the others keep theirs for their next reset.
 // Measured: the chain was half of the kernel's time (resets ablated: 2x).
-template <int LMAX>
-__device__ __forceinline__ void sp_reset_wave(const Params &p, const SPlanes &pl, bool need, bool live, uint32_t seed,
-                                              Agent &g, uint32_t &goal, Room &R, SRows &w, float *row, int lane,
-                                              int block_agent0, uint4 &nd, uint32_t *mt_lds) {
+__device__ __forceinline__ uint2 sp_reset_draw(const Params &p, bool need, bool live, uint32_t seed, int lane, uint4 &nd,
+                                               uint32_t *mt_lds) {
     const bool have = need && nd.w == 1u && nd.z == seed;
     uint2 drawn = have ? make_uint2(nd.x, nd.y) : make_uint2(0u, 0u);
     if (need) nd.w = 0u;                                   // consumed: the next episode has another seed
@@ -2855,6 +2913,14 @@ __device__ __forceinline__ void sp_reset_wave(const Params &p, const SPlanes &pl
         if (need && !have) drawn = d2;
         else if (live) nd = make_uint4(d2.x, d2.y, s2, 1u);
     }
+    return drawn;
+}
+
+template <int LMAX>
+__device__ __forceinline__ void sp_reset_wave(const Params &p, const SPlanes &pl, bool need, bool live, uint32_t seed,
+                                              Agent &g, uint32_t &goal, Room &R, SRows &w, float *row, int lane,
+                                              int block_agent0, uint4 &nd, uint32_t *mt_lds) {
+    const uint2 drawn = sp_reset_draw(p, need, live, seed, lane, nd, mt_lds);
     uint64_t m = __ballot(need);
     const uint32_t n16 = p.agent_bytes >> 4;
     while (m) {
@@ -2895,7 +2961,7 @@ struct SPend {
     bool moved;
 };
 
-template <int LMAX>
+template <int LMAX, bool EXT>
 __global__ __launch_bounds__(128) void simple_pipe_kernel(Params p) {
     extern __shared__ float sm[];
     const int OD = p.obs_dim, L = p.L;
@@ -2932,6 +2998,16 @@ __global__ __launch_bounds__(128) void simple_pipe_kernel(Params p) {
     }
 
     // ---- stepping wave ----
+    // Every global store of the step loop is issued unconditionally (the
+    // evicted S words go through a buffer resource over the block's belief
+    // maps; a lane with nothing to store gives an out-of-range offset, which
+    // the hardware drops).  vmcnt retires in issue order, so a load can be
+    // waited for with the stores issued after it still in flight only when
+    // their count is the same on every path; a store skipped by a branch
+    // made hipcc wait vmcnt(0) -- for the stores too -- in every step.
+    const __amdgpu_buffer_rsrc_t brs = __builtin_amdgcn_make_buffer_rsrc(
+        p.belief + (size_t)a0 * p.agent_bytes, 0, (int)((uint32_t)rows * p.agent_bytes), 0x00020000);
+    const uint32_t lane_off = (uint32_t)lane * p.agent_bytes;
     const int ai = a0 + lane;
     const bool live = ai < p.N;
     const SPlanes pl = splanes(p, live ? ai : a0);
@@ -2973,7 +3049,7 @@ __global__ __launch_bounds__(128) void simple_pipe_kernel(Params p) {
     auto premove = [&](int k) {
         const uint64_t t = p.t0 + (uint64_t)k;
         int a;
-        if (p.actions) {
+        if (EXT) {
             a = p.actions[(size_t)k * p.N + (live ? ai : a0)];
         } else {
             if ((t >> 2) != r4blk) {
@@ -3004,20 +3080,25 @@ __global__ __launch_bounds__(128) void simple_pipe_kernel(Params p) {
         }
     };
     if (live && p.K > 0) premove(0);
+#if VN_SIMPLE_PROF
+    uint64_t prof[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    uint64_t tprev = __builtin_amdgcn_s_memtime();
+#endif
 
     for (int k = 0; k < p.K; ++k) {
         const int b = k & 1;
         float *row = stage + b * 64 * OD + lane * OD;
         bool trunc = false, term = false;
+        int a = 0;
+        bool moved = false, explored = false, seen = true;
         if (live) {
             // ---- commit step k (:109-150) ----
             if (p.actions_out) p.actions_out[(size_t)k * p.N + ai] = pm.a;
             g.step_count += 1;
             trunc = g.step_count >= R.total_free;                      // :111, max_steps = total_free (:409)
             g.facing = pm.facing;
-            const int a = pm.a;
-            const bool moved = pm.moved;
-            bool explored = false, seen = true;
+            a = pm.a;
+            moved = pm.moved;
             if (moved) {                                                 // _mark_visited (:273-298)
                 const int ax = pm.d >> 1;
                 // the target's S bit from the cached word of the move axis (kept in wn)
@@ -3048,15 +3129,23 @@ __global__ __launch_bounds__(128) void simple_pipe_kernel(Params p) {
             cbx = cby = 0ull;
             cbz = 0u;
             g.last_action = a;                                           // :137
+            SB_T(0);
             // ---- the next step's move and its loads, issued before this step's
             // S-mark stores (a wait for these loads then never waits for them) ----
             if (k + 1 < p.K) premove(k + 1);
             if (!(VN_ABLATE & 1024u)) {                 // the evicted words, behind the loads
-                if (evm & 1u) pl.sx[evyx * p.ph + evz_] = evx;
-                if (evm & 2u) pl.sy[evxy * p.ph + evz_] = evy;
-                if (evm & 4u) pl.sz[evxx * p.pd + evyy] = evz;
+                constexpr uint32_t OFF = 0x80000000u;   // out of range: dropped
+                typedef uint32_t u32x2_t __attribute__((ext_vector_type(2)));
+                const u32x2_t vx = {(uint32_t)evx, (uint32_t)(evx >> 32)}, vy = {(uint32_t)evy, (uint32_t)(evy >> 32)};
+                __builtin_amdgcn_raw_buffer_store_b64(
+                    vx, brs, (evm & 1u) ? lane_off + 8u * (uint32_t)(evyx * p.ph + evz_) : OFF, 0, 0);
+                __builtin_amdgcn_raw_buffer_store_b64(
+                    vy, brs, (evm & 2u) ? lane_off + p.sy_off + 8u * (uint32_t)(evxy * p.ph + evz_) : OFF, 0, 0);
+                __builtin_amdgcn_raw_buffer_store_b32(
+                    evz, brs, (evm & 4u) ? lane_off + p.sz_off + 4u * (uint32_t)(evxx * p.pd + evyy) : OFF, 0, 0);
             }
             evm = 0u;
+            SB_T(1);
             if (moved) {
                 // a Q cell (internal_grid 2) is entered without counting, but it
                 // is a sensing position all the same, so S is set
@@ -3081,7 +3170,9 @@ __global__ __launch_bounds__(128) void simple_pipe_kernel(Params p) {
                     }
                 }
             }
-            if (!(VN_ABLATE & 4u)) sb_observe<LMAX>(p, pl, g, w, row);   // :139
+            SB_T(2);
+            if (!(VN_ABLATE & 4u)) sp_observe<LMAX>(p, pl, g, w, row);   // :139
+            SB_T(3);
             // compute_reward (:189-217), f64 in the reference's order
             double r = -0.1;
             if (!moved) {
@@ -3106,6 +3197,7 @@ __global__ __launch_bounds__(128) void simple_pipe_kernel(Params p) {
                 for (int q = 0; q < OD; ++q) to[q] = row[q];
             }
         }
+        SB_T(4);
         // SB3 VecEnv auto-reset
         const bool need = live && p.autoreset && (term || trunc) && !(VN_ABLATE & 512u);
         if (__ballot(need)) {
@@ -3125,12 +3217,418 @@ __global__ __launch_bounds__(128) void simple_pipe_kernel(Params p) {
                 vn_touch((uint32_t)(R.D | (R.H << 8)));
             }
         }
+        SB_T(5);
         lds_handoff();                         // hand buffer b to the store wave
+        SB_T(6);
     }
+#if VN_SIMPLE_PROF
+    if (lane == 0) {
+        uint64_t tot = 0;
+        for (int q = 0; q < 7; ++q) {
+            atomicAdd(&g_simple_prof[q], (unsigned long long)prof[q]);
+            tot += prof[q];
+        }
+        atomicAdd(&g_simple_prof[7], tot);
+        atomicAdd(&g_simple_prof[8], 1ull);
+    }
+#endif
     if (live) {
         if (sdirty & 1u) pl.sx[g.y * p.ph + g.z] = w.wx;
         if (sdirty & 2u) pl.sy[g.x * p.ph + g.z] = w.wy;
         if (sdirty & 4u) pl.sz[g.x * p.pd + g.y] = w.wz;
+        p.hot[ai] = pack(g);
+        p.goal[ai] = goal;
+        p.next_seed[ai] = next_seed;
+        p.predraw[ai] = nd;
+    }
+    (void)L;
+}
+
+
+// ============================================================================
+// simpleEnv, line layout (the default for rooms up to 32 x 32 x 8, e.g. the
+// bench's 32x32x8 box).  Same belief as the bit-plane layout -- S (cells
+// stood on) and Q (edge-quirk marks), every other internal_grid value derived
+// -- but S is kept as LINES: SX[y] = 8 u32 words over z (bit x), SY[x] = 8 u32
+// words over z (bit y), 32 B each; a column's z bits (the up / down rays) are
+// bit x of the SX[y] line, so there is no third copy.  The stepping lane keeps
+// the two lines through its cell in LDS: a move along x replaces the SY line,
+// along y the SX line, along z neither; the line left is stored back if it
+// was marked.
+// Why (rocprofv3, round 3): the simpleEnv step is bound by the CUs' 64-B
+// request rate -- the address unit is busy 87-95 % of the kernel, at 5.7
+// requests per env-step, 1.1 of them the evicted S words of the word layout
+// (each move replaced 2-3 words; without those stores the kernel ran 1.4x).
+// A lane's 32-B line access is 2 x 16 B; lane pairs split it so that both
+// halves of one line go out in ONE instruction (a request per line, not per
+// half): instruction 1 moves the even lane's line, instruction 2 the odd
+// lane's, and the halves are swapped across the pair with one DPP move.
+// Every line load / store is issued every step (an out-of-range buffer offset
+// when a lane has none: no request, and the same vmcnt count on every path).
+// LDS per lane: the X and Y line (12-word stride: 16-B aligned rows).
+// QZ (edge-quirk marks) as in the bit-plane layout.
+// ============================================================================
+constexpr int SL_STRIDE = 12;   // words per LDS line slot
+constexpr uint32_t SL_OFF = 0x80000000u;   // out-of-range buffer offset: dropped
+typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));
+
+struct SLine {
+    u32x4_t h0, h1;   // words 0-3, 4-7
+};
+
+__device__ __forceinline__ uint32_t dpp_swap_pair(uint32_t v) {   // lane i <- lane i ^ 1
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0xB1, 0xF, 0xF, false);
+}
+__device__ __forceinline__ u32x4_t dpp_swap_pair4(u32x4_t v) {
+    u32x4_t r;
+    r.x = dpp_swap_pair(v.x);
+    r.y = dpp_swap_pair(v.y);
+    r.z = dpp_swap_pair(v.z);
+    r.w = dpp_swap_pair(v.w);
+    return r;
+}
+
+// lane-pair line load: each lane gets the line at its byte offset `off`
+// (SL_OFF: none, zeros).  Must run with the whole wave active.
+__device__ __forceinline__ SLine sl_pair_load(__amdgpu_buffer_rsrc_t rs, uint32_t off, bool odd) {
+    const uint32_t off_e = dpp_swap_pair(off), off_o = dpp_swap_pair(off);
+    const uint32_t ae = odd ? off_e : off, ao = odd ? off : off_o;     // the pair's even / odd line
+    const uint32_t half = odd ? 16u : 0u;
+    const u32x4_t r1 = __builtin_amdgcn_raw_buffer_load_b128(rs, ae == SL_OFF ? SL_OFF : ae + half, 0, 0);
+    const u32x4_t r2 = __builtin_amdgcn_raw_buffer_load_b128(rs, ao == SL_OFF ? SL_OFF : ao + half, 0, 0);
+    // even: r1 = own h0, r2 = partner's h0; odd: r1 = partner's h1, r2 = own h1
+    const u32x4_t sw = dpp_swap_pair4(odd ? r1 : r2);
+    SLine l;
+    l.h0 = odd ? sw : r1;
+    l.h1 = odd ? r2 : sw;
+    return l;
+}
+
+// lane-pair line store of each lane's line `l` at `off` (SL_OFF: none)
+__device__ __forceinline__ void sl_pair_store(__amdgpu_buffer_rsrc_t rs, uint32_t off, const SLine &l, bool odd) {
+    const uint32_t off_p = dpp_swap_pair(off);
+    const uint32_t ae = odd ? off_p : off, ao = odd ? off : off_p;
+    const uint32_t half = odd ? 16u : 0u;
+    const u32x4_t sw = dpp_swap_pair4(odd ? l.h0 : l.h1);   // even gets the odd lane's h0, odd the even's h1
+    __builtin_amdgcn_raw_buffer_store_b128(odd ? sw : l.h0, rs, ae == SL_OFF ? SL_OFF : ae + half, 0, 0);
+    __builtin_amdgcn_raw_buffer_store_b128(odd ? l.h1 : sw, rs, ao == SL_OFF ? SL_OFF : ao + half, 0, 0);
+}
+
+__device__ __forceinline__ void sl_lds_put(uint32_t *slot, const SLine &l) {
+    reinterpret_cast<u32x4_t *>(slot)[0] = l.h0;
+    reinterpret_cast<u32x4_t *>(slot)[1] = l.h1;
+}
+__device__ __forceinline__ SLine sl_lds_get(const uint32_t *slot) {
+    SLine l;
+    l.h0 = reinterpret_cast<const u32x4_t *>(slot)[0];
+    l.h1 = reinterpret_cast<const u32x4_t *>(slot)[1];
+    return l;
+}
+// bit z = bit b of word z (the column's S bits from the SX line)
+__device__ __forceinline__ uint32_t sl_column(const SLine &l, int b) {
+    const uint32_t w[8] = {l.h0.x, l.h0.y, l.h0.z, l.h0.w, l.h1.x, l.h1.y, l.h1.z, l.h1.w};
+    uint32_t c = 0;
+#pragma unroll
+    for (int z = 0; z < 8; ++z) c |= ((w[z] >> b) & 1u) << z;
+    return c;
+}
+
+// reset of the lanes with `need` (sp_reset_wave in the line layout): the
+// wave zeroes every resetting agent's SX / SY lines (and QZ if it holds
+// marks), then each marks its start cell in its LDS lines (dirty) and senses
+template <int LMAX>
+__device__ __forceinline__ void sl_reset_wave(const Params &p, const SPlanes &pl, bool need, bool live, uint32_t seed,
+                                              Agent &g, uint32_t &goal, Room &R, SRows &w, float *row, int lane,
+                                              int block_agent0, uint4 &nd, uint32_t *mt_lds, uint32_t *lx,
+                                              uint32_t *ly) {
+    const uint2 drawn = sp_reset_draw(p, need, live, seed, lane, nd, mt_lds);
+    const bool hadq = need && (g.move_mask & 1u);
+    uint64_t m = __ballot(need);
+    const uint64_t mq = __ballot(hadq);
+    while (m) {
+        const int src = __ffsll((unsigned long long)m) - 1;
+        m &= m - 1;
+        // QZ (at the end of the agent's block) is all zero unless the episode marked it
+        const uint32_t n16 = (((mq >> src) & 1ull) ? p.agent_bytes : p.qz_off) >> 4;
+        uint4 *base = reinterpret_cast<uint4 *>(p.belief + (size_t)(block_agent0 + src) * p.agent_bytes);
+        for (uint32_t q = (uint32_t)lane; q < n16; q += 64u) base[q] = make_uint4(0u, 0u, 0u, 0u);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+    if (need) {
+        g.room = (int)(drawn.x >> 24);
+        R = load_room(p, g.room);
+        g.x = drawn.x & 0xff;
+        g.y = (drawn.x >> 8) & 0xff;
+        g.z = (drawn.x >> 16) & 0xff;
+        goal = drawn.y;
+        g.facing = 0;
+        g.last_action = 0;
+        g.done = g.last_bump = g.near_wall = g.was_near_wall = false;
+        g.step_count = 0;
+        g.visited = 1;
+        g.bumps = 0;
+        g.cid = 0;
+        g.move_mask = 0;
+        w.wx = 1ull << g.x;                                                     // :86
+        w.wy = 1ull << g.y;
+        w.wz = 1u << g.z;
+#pragma unroll
+        for (int z = 0; z < 8; ++z) {
+            lx[z] = z == g.z ? (uint32_t)w.wx : 0u;
+            ly[z] = z == g.z ? (uint32_t)w.wy : 0u;
+        }
+        w.rec = p.rays[R.ray_off + (uint32_t)((g.x * R.D + g.y) * R.H + g.z)];
+        sb_observe<LMAX>(p, pl, g, w, row);
+    }
+}
+
+template <int LMAX, bool EXT>
+__global__ __launch_bounds__(128) void simple_line_kernel(Params p) {
+    extern __shared__ float sm[];
+    const int OD = p.obs_dim, L = p.L;
+    float *stage = sm;
+    float *srew = sm + 2 * 64 * OD;
+    uint32_t *sflg = reinterpret_cast<uint32_t *>(srew + 2 * 64);
+    uint32_t *mt_lds = sflg + 2 * 64;
+    uint32_t *lines = mt_lds + 64 * MT_WS + 4;   // [2][64][SL_STRIDE]; 16-B aligned (see the launch)
+    const int lane = threadIdx.x & 63;
+    const int a0 = blockIdx.x * 64;
+    const int rows = min(64, p.N - a0);
+
+    if (threadIdx.x >= 64) {                     // ---- store wave (as simple_pipe_kernel) ----
+        for (int k = 0; k < p.K; ++k) {
+            lds_handoff();                     // step k staged in buffer k & 1
+            const int b = k & 1;
+            const float *st = stage + b * 64 * OD;
+            float *dst = p.obs + ((size_t)k * p.N + a0) * OD;
+            if (VN_ABLATE & 16u) {
+            } else if (!((rows * OD) & 3) && !(reinterpret_cast<uintptr_t>(dst) & 15u)) {
+                const float4 *s4 = reinterpret_cast<const float4 *>(st);
+                float4 *d4 = reinterpret_cast<float4 *>(dst);
+                for (int q = lane; q < (rows * OD) >> 2; q += 64) obs_store(d4 + q, s4[q]);
+            } else {
+                for (int q = lane; q < rows * OD; q += 64) __builtin_nontemporal_store(st[q], dst + q);
+            }
+            if (lane < rows) {
+                const size_t o = (size_t)k * p.N + a0 + lane;
+                const uint32_t f = sflg[b * 64 + lane];
+                if (p.reward) p.reward[o] = srew[b * 64 + lane];
+                if (p.term) p.term[o] = (uint8_t)(f & 1u);
+                if (p.trunc) p.trunc[o] = (uint8_t)(f >> 1);
+            }
+        }
+        return;
+    }
+
+    // ---- stepping wave ----
+    const __amdgpu_buffer_rsrc_t brs = __builtin_amdgcn_make_buffer_rsrc(
+        p.belief + (size_t)a0 * p.agent_bytes, 0, (int)((uint32_t)rows * p.agent_bytes), 0x00020000);
+    const uint32_t lane_off = (uint32_t)lane * p.agent_bytes;
+    const bool odd = lane & 1;
+    const int ai = a0 + lane;
+    const bool live = ai < p.N;
+    uint32_t *lx = lines + lane * SL_STRIDE;           // SX[g.y]
+    uint32_t *ly = lines + (64 + lane) * SL_STRIDE;    // SY[g.x]
+    const SPlanes pl = splanes(p, live ? ai : a0);
+    Agent g = unpack(live ? p.hot[ai] : make_uint4(0u, 0u, 0u, 0u));
+    uint32_t goal = live ? p.goal[ai] : 0u;
+    uint32_t next_seed = live ? p.next_seed[ai] : 0u;
+    uint4 nd = live ? p.predraw[ai] : make_uint4(0u, 0u, 0u, 0u);   // draw ahead (sp_reset_wave)
+    Room R = load_room(p, g.room);
+    auto xline_off = [&](int y) { return lane_off + 32u * (uint32_t)y; };
+    auto yline_off = [&](int x) { return lane_off + p.sy_off + 32u * (uint32_t)x; };
+    SRows w;                                     // S words + ray record at the agent's (committed) cell
+    {
+        const SLine l0 = sl_pair_load(brs, live ? xline_off(g.y) : SL_OFF, odd);
+        const SLine l1 = sl_pair_load(brs, live ? yline_off(g.x) : SL_OFF, odd);
+        sl_lds_put(lx, l0);
+        sl_lds_put(ly, l1);
+        w.wx = lx[g.z & 7];
+        w.wy = ly[g.z & 7];
+        w.wz = sl_column(l0, g.x & 31);
+        w.rec = live ? p.rays[R.ray_off + (uint32_t)((g.x * R.D + g.y) * R.H + g.z)] : make_uint2(0u, 0u);
+    }
+    vn_touch((uint32_t)R.ray_off);
+    vn_touch((uint32_t)R.total_free);
+    vn_touch((uint32_t)(R.D | (R.H << 8)));
+
+    uint4 r4 = make_uint4(0u, 0u, 0u, 0u);      // Philox block r4blk (4 steps)
+    uint64_t r4blk = ~0ull;
+    SPend pm;                                    // the pending move ...
+    SLine ln;                                    // ... the line it brings in (in flight) ...
+    uint2 rn = make_uint2(0u, 0u);               // ... and its target's ray record (in flight)
+    uint32_t dirty = 0u;                         // 1: the LDS X line is marked, 2: the Y line
+    SLine ev;                                    // the line the last commit replaced, stored after the
+    uint32_t ev_off = SL_OFF;                    // next move's loads (a load of it takes it from here)
+    ev.h0 = ev.h1 = u32x4_t{0u, 0u, 0u, 0u};
+    ln = ev;
+    // the move of launch step k from the committed state; issues the target's loads
+    auto premove = [&](int k, bool act) {
+        uint32_t loff = SL_OFF;
+        uint32_t rcell = 0u;
+        if (act) {
+            const uint64_t t = p.t0 + (uint64_t)k;
+            int a;
+            if (EXT) {
+                a = p.actions[(size_t)k * p.N + ai];
+            } else {
+                if ((t >> 2) != r4blk) {
+                    r4blk = t >> 2;
+                    r4 = philox4x32_10(p.policy_seed, p.gid_base + (uint64_t)ai, t >> 2);
+                }
+                const uint32_t word = (t & 3) == 0 ? r4.x : (t & 3) == 1 ? r4.y : (t & 3) == 2 ? r4.z : r4.w;
+                a = (int)(((uint64_t)word * 6u) >> 32);
+            }
+            const int d = a < 4 ? rel_dir(a, g.facing) : (a == 4 ? 4 : 5);
+            pm.a = a;
+            pm.d = d;
+            pm.facing = a < 4 ? facing_of(d) : g.facing;                 // :164-171
+            pm.moved = (ray_e8(w.rec, d) & 0x7fu) >= 1u;
+            pm.nx = g.x + (pm.moved ? (d == 0 ? 1 : d == 1 ? -1 : 0) : 0);
+            pm.ny = g.y + (pm.moved ? (d == 2 ? 1 : d == 3 ? -1 : 0) : 0);
+            pm.nz = g.z + (pm.moved ? (d == 4 ? 1 : d == 5 ? -1 : 0) : 0);
+            rcell = (uint32_t)((pm.nx * R.D + pm.ny) * R.H + pm.nz);
+            // the line a move along x (y) brings in: SY[nx] (SX[ny]); from ev if it is
+            // the line the last commit replaced (its store is issued after these loads)
+            if (pm.moved && d < 4) {
+                const uint32_t o = d < 2 ? yline_off(pm.nx) : xline_off(pm.ny);
+                if (o != ev_off) loff = o;
+            }
+        }
+        const SLine l = sl_pair_load(brs, loff, odd);
+        const uint2 rc = p.rays[R.ray_off + rcell];
+        if (act) {                               // (a lane without a move keeps its pending one)
+            ln = loff == SL_OFF ? ev : l;        // forwarded (or unused)
+            rn = rc;
+        }
+    };
+    if (p.K > 0) premove(0, live);
+#if VN_SIMPLE_PROF
+    uint64_t prof[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    uint64_t tprev = __builtin_amdgcn_s_memtime();
+#endif
+
+    for (int k = 0; k < p.K; ++k) {
+        const int b = k & 1;
+        float *row = stage + b * 64 * OD + lane * OD;
+        bool trunc = false, term = false;
+        int a = 0;
+        bool moved = false, explored = false, seen = true;
+        if (live) {
+            // ---- commit step k (:109-150) ----
+            if (p.actions_out) p.actions_out[(size_t)k * p.N + ai] = pm.a;
+            g.step_count += 1;
+            trunc = g.step_count >= R.total_free;                      // :111, max_steps = total_free (:409)
+            g.facing = pm.facing;
+            a = pm.a;
+            moved = pm.moved;
+            if (moved) {                                                 // _mark_visited (:273-298)
+                const int ax = pm.d >> 1;
+                // the target's S bit from the word along the move axis
+                seen = ax == 0 ? ((w.wx >> pm.nx) & 1ull) : ax == 1 ? ((w.wy >> pm.ny) & 1ull) : ((w.wz >> pm.nz) & 1u);
+                if (ax < 2) {
+                    // replace the line across the move axis: the old one is stored if marked
+                    uint32_t *slot = ax == 0 ? ly : lx;
+                    const uint32_t dbit = ax == 0 ? 2u : 1u;
+                    if (dirty & dbit) {
+                        ev = sl_lds_get(slot);
+                        ev_off = ax == 0 ? yline_off(g.x) : xline_off(g.y);
+                    }
+                    dirty &= ~dbit;
+                    sl_lds_put(slot, ln);
+                }
+                g.x = pm.nx;
+                g.y = pm.ny;
+                g.z = pm.nz;
+                w.wx = lx[g.z];
+                w.wy = ly[g.z];
+                if (ax < 2) w.wz = sl_column(sl_lds_get(lx), g.x);
+                w.rec = rn;
+            }
+            g.last_action = a;                                           // :137
+        }
+        SB_T(0);
+        // ---- the next step's move and its loads, then the replaced line's
+        // store (a wait for the loads then never waits for the store) ----
+        premove(k + 1, live && k + 1 < p.K);
+        sl_pair_store(brs, ev_off, ev, odd);
+        ev_off = SL_OFF;
+        SB_T(1);
+        if (live) {
+            if (moved) {
+                // a Q cell (internal_grid 2) is entered without counting, but it
+                // is a sensing position all the same, so S is set
+                const bool q = (g.move_mask & 1u) && ((pl.qz[g.x * p.pd + g.y] >> g.z) & 1u);
+                if (!seen) {
+                    w.wx |= 1ull << g.x;
+                    w.wy |= 1ull << g.y;
+                    w.wz |= 1u << g.z;
+                    lx[g.z] = (uint32_t)w.wx;
+                    ly[g.z] = (uint32_t)w.wy;
+                    dirty = 3u;
+                    if (!q) {
+                        g.visited += 1;
+                        explored = true;
+                    }
+                }
+            }
+            SB_T(2);
+            if (!(VN_ABLATE & 4u)) sp_observe<LMAX>(p, pl, g, w, row);   // :139
+            SB_T(3);
+            // compute_reward (:189-217), f64 in the reference's order
+            double r = -0.1;
+            if (!moved) {
+                g.bumps += 1;
+                r += -10.0;
+            }
+            if (a != 2 && a < 4) r += 0.05;
+            const int gx = goal & 0xff, gy = (goal >> 8) & 0xff, gz = (goal >> 16) & 0xff;
+            if (g.x == gx && g.y == gy && g.z >= gz && g.z - gz < 5) {   // SPOT_GOAL_HEIGTH = 5 (:201-206)
+                g.done = true;
+                r += 100.0;
+            }
+            if (trunc) r += 0.0;
+            if (explored) r += 1.0;
+            term = g.done;
+            const size_t o = (size_t)k * p.N + ai;
+            srew[b * 64 + lane] = (float)r;
+            sflg[b * 64 + lane] = (term ? 1u : 0u) | (trunc ? 2u : 0u);
+            if (p.reward64) p.reward64[o] = r;
+            if ((term || trunc) && p.autoreset && p.terminal_obs) {
+                float *to = p.terminal_obs + o * OD;
+                for (int q = 0; q < OD; ++q) to[q] = row[q];
+            }
+        }
+        SB_T(4);
+        // SB3 VecEnv auto-reset
+        const bool need = live && p.autoreset && (term || trunc) && !(VN_ABLATE & 512u);
+        if (__ballot(need)) {
+            sl_reset_wave<LMAX>(p, pl, need, live, next_seed, g, goal, R, w, row, lane, a0, nd, mt_lds, lx, ly);
+            if (need) {
+                next_seed += p.seed_stride;
+                dirty = 3u;                              // the start cell's lines (LDS only)
+            }
+            // from the start cell (the wave's loads are issued together)
+            premove(k + 1, need && k + 1 < p.K);
+        }
+        SB_T(5);
+        lds_handoff();                         // hand buffer b to the store wave
+        SB_T(6);
+    }
+#if VN_SIMPLE_PROF
+    if (lane == 0) {
+        uint64_t tot = 0;
+        for (int q = 0; q < 7; ++q) {
+            atomicAdd(&g_simple_prof[q], (unsigned long long)prof[q]);
+            tot += prof[q];
+        }
+        atomicAdd(&g_simple_prof[7], tot);
+        atomicAdd(&g_simple_prof[8], 1ull);
+    }
+#endif
+    sl_pair_store(brs, (live && (dirty & 1u)) ? xline_off(g.y) : SL_OFF, sl_lds_get(lx), odd);
+    sl_pair_store(brs, (live && (dirty & 2u)) ? yline_off(g.x) : SL_OFF, sl_lds_get(ly), odd);
+    if (live) {
         p.hot[ai] = pack(g);
         p.goal[ai] = goal;
         p.next_seed[ai] = next_seed;
@@ -3164,19 +3662,6 @@ constexpr int SG_APW = 64 / SG;   // agents per wave
 #ifndef VN_SG_MIN_WAVES
 #define VN_SG_MIN_WAVES 4   // <= 128 VGPRs: the 16 waves of 256 agents per CU resident
 #endif
-
-// obs slot of absolute direction j < 4 for facing f: slot k with rel_dir of
-// [fwd, left, right, back][k] == j
-constexpr uint32_t pack_obs_slot() {
-    uint32_t v = 0;
-    const int rel_of_slot[4] = {0, 3, 1, 2};   // forward, left, right, backward (action indices)
-    for (int f = 0; f < 4; ++f)
-        for (int k = 0; k < 4; ++k) v |= (uint32_t)k << (2 * (4 * f + kRelDir[rel_of_slot[k]][f]));
-    return v;
-}
-__device__ __forceinline__ int obs_slot(int j, int facing) {
-    return j >= 4 ? j : (int)((pack_obs_slot() >> (2 * (4 * facing + j))) & 3u);
-}
 
 // QZ words are OR-ed atomically (at L2) by any lane of the group: read them
 // coherently (not from a possibly stale L1 line)
@@ -3445,7 +3930,10 @@ __device__ int8_t sb_belief_cell(const Params &p, int i, const Room &R, int x, i
     auto wall = [&](int cx, int cy, int cz) {
         return ((p.rays[R.ray_off + (uint32_t)((cx * R.D + cy) * R.H + cz)].y >> 16) & 1u) != 0u;
     };
-    auto sbit = [&](int cx, int cy, int cz) { return ((pl.sz[cx * p.pd + cy] >> cz) & 1u) != 0u; };
+    auto sbit = [&](int cx, int cy, int cz) {
+        if (p.sline) return ((reinterpret_cast<const uint32_t *>(pl.sx)[cy * p.ph + cz] >> cx) & 1u) != 0u;
+        return ((pl.sz[cx * p.pd + cy] >> cz) & 1u) != 0u;
+    };
     const bool is_wall = wall(x, y, z);
     if (!is_wall && ((pl.qz[x * p.pd + y] >> z) & 1u)) return 2;
     if (sbit(x, y, z)) return 1;
@@ -3579,6 +4067,7 @@ struct VnEnv {
     int sb_pipe = 1;   // ... software-pipelined by one step (simple_pipe_kernel)
     int sb_aw = 32;   // measured: 32 agents per wave 5.62 vs 64 5.43 G env-steps/s (16: 4.97)
     uint32_t sy_off = 0, sz_off = 0, qz_off = 0;
+    int sline = 0;     // simpleEnv line layout (simple_line_kernel), rooms <= 32 x 32 x 8
     int pcache = 0;    // CubicEnv plane-set mode (PH 8, rooms <= 64 x 64): see pset_fill
     int8_t *d_wimg = nullptr;
     float *d_scratch = nullptr;   // 4 KiB: targets of inactive lanes' output stores
@@ -3652,6 +4141,7 @@ Params base_params(VnEnv *e) {
     p.sy_off = e->sy_off;
     p.sz_off = e->sz_off;
     p.qz_off = e->qz_off;
+    p.sline = e->sline;
     p.wimg = e->d_wimg;
     p.pcache = e->pcache;
     p.scratch = e->d_scratch;
@@ -3684,6 +4174,30 @@ template <bool RESET_ONLY>
 int launch_env(VnEnv *e, const Params &p, hipStream_t s) {
     if (e->variant == VN_VARIANT_SIMPLE) {
         const int L = e->cfg.local_map_length;
+        if (!RESET_ONLY && e->sline) {
+            // line layout: stepping wave + store wave per 64 agents (simple_line_kernel)
+            const size_t lds = (size_t)2 * 64 * e->obs_dim * sizeof(float) + 2 * 64 * 8 + 64 * MT_WS * 4 +
+                               (4 + 2 * 64 * SL_STRIDE) * 4;
+            const dim3 grid((unsigned)((e->N + 63) / 64));
+#define VN_SL_LAUNCH(LM)                                                                   \
+    do {                                                                                   \
+        if (p.actions)                                                                     \
+            hipLaunchKernelGGL((simple_line_kernel<LM, true>), grid, dim3(128), lds, s, p);  \
+        else                                                                               \
+            hipLaunchKernelGGL((simple_line_kernel<LM, false>), grid, dim3(128), lds, s, p); \
+    } while (0)
+            if (L <= 4)
+                VN_SL_LAUNCH(4);
+            else if (L <= 8)
+                VN_SL_LAUNCH(8);
+            else if (L <= 10)
+                VN_SL_LAUNCH(10);
+            else
+                VN_SL_LAUNCH(16);
+#undef VN_SL_LAUNCH
+            VN_HIP(hipGetLastError());
+            return VN_OK;
+        }
         if (!RESET_ONLY && e->sbits && e->sb_group) {
             // 8 lanes per agent (simple_group_kernel)
             const size_t lds = (size_t)4 * SG_APW * e->obs_dim * sizeof(float);
@@ -3703,14 +4217,22 @@ int launch_env(VnEnv *e, const Params &p, hipStream_t s) {
             // software-pipelined stepping wave + store wave per 64 agents (simple_pipe_kernel)
             const size_t lds = (size_t)2 * 64 * e->obs_dim * sizeof(float) + 2 * 64 * 8 + 64 * MT_WS * 4;
             const dim3 grid((unsigned)((e->N + 63) / 64));
+#define VN_SP_LAUNCH(LM)                                                                   \
+    do {                                                                                   \
+        if (p.actions)                                                                     \
+            hipLaunchKernelGGL((simple_pipe_kernel<LM, true>), grid, dim3(128), lds, s, p);  \
+        else                                                                               \
+            hipLaunchKernelGGL((simple_pipe_kernel<LM, false>), grid, dim3(128), lds, s, p); \
+    } while (0)
             if (L <= 4)
-                hipLaunchKernelGGL((simple_pipe_kernel<4>), grid, dim3(128), lds, s, p);
+                VN_SP_LAUNCH(4);
             else if (L <= 8)
-                hipLaunchKernelGGL((simple_pipe_kernel<8>), grid, dim3(128), lds, s, p);
+                VN_SP_LAUNCH(8);
             else if (L <= 10)
-                hipLaunchKernelGGL((simple_pipe_kernel<10>), grid, dim3(128), lds, s, p);
+                VN_SP_LAUNCH(10);
             else
-                hipLaunchKernelGGL((simple_pipe_kernel<16>), grid, dim3(128), lds, s, p);
+                VN_SP_LAUNCH(16);
+#undef VN_SP_LAUNCH
             VN_HIP(hipGetLastError());
             return VN_OK;
         }
@@ -3759,10 +4281,12 @@ std::string kernel_label(const VnEnv *e, bool reset_only, bool ext, bool fast, i
     if (e->variant == VN_VARIANT_SIMPLE) {
         const int L = e->cfg.local_map_length;
         const int lmax = L <= 4 ? 4 : L <= 8 ? 8 : L <= 10 ? 10 : 16;
-        if (!reset_only && e->sbits && e->sb_group)
+        if (!reset_only && e->sline)
+            std::snprintf(buf, sizeof(buf), "simple_line_kernel<%d, %s>", lmax, ext ? "true" : "false");
+        else if (!reset_only && e->sbits && e->sb_group)
             std::snprintf(buf, sizeof(buf), "simple_group_kernel<%d>", lmax);
         else if (!reset_only && e->sbits && e->sb_split && e->sb_pipe)
-            std::snprintf(buf, sizeof(buf), "simple_pipe_kernel<%d>", lmax);
+            std::snprintf(buf, sizeof(buf), "simple_pipe_kernel<%d, %s>", lmax, ext ? "true" : "false");
         else if (!reset_only && e->sbits && e->sb_split)
             std::snprintf(buf, sizeof(buf), "simple_split_kernel<%d>", lmax);
         else if (e->sbits)
@@ -3873,6 +4397,10 @@ int vn_create(const VnRoomSet *rooms, int32_t n_agents, const VnConfig *cfg, int
                     uint2 rec;
                     rec.x = e8[0] | (e8[1] << 8) | (e8[2] << 16) | (e8[3] << 24);
                     rec.y = e8[4] | (e8[5] << 8) | (e8[6] << 16);
+                    // bit 17: some ray from this cell ends at the room's edge (not a
+                    // wall), i.e. may take the edge-quirk mark (simple_pipe_kernel)
+                    for (int d = 0; d < 6; ++d)
+                        if (!(e8[d] & 0x80u) && (e8[d] & 0x7fu) >= 1u && (e8[d] & 0x7fu) < 127u) rec.y |= 1u << 17;
                     rays.push_back(rec);
                 }
         int32_t fixed = -1;
@@ -3945,11 +4473,21 @@ int vn_create(const VnRoomSet *rooms, int32_t n_agents, const VnConfig *cfg, int
         e->pd = maxD;
         e->map_bytes = 0;
         e->nwx = e->nwy = 0;
-        e->sy_off = (uint32_t)(8 * e->pd * e->ph);
-        e->sz_off = e->sy_off + (uint32_t)(8 * e->pw * e->ph);
-        e->qz_off = e->sz_off + (uint32_t)(4 * e->pw * e->pd);
+        const char *sl = getenv("VOXNAV_SIMPLE_LINE");   // A/B knob: 0 keeps the word layout
+        e->sline = (maxW <= 32 && maxD <= 32 && e->ph == 8 && !(sl && sl[0] == '0')) ? 1 : 0;
+        if (e->sline) {
+            // lines: SX u32 [pd][8] (bit x), SY u32 [pw][8] (bit y), QZ u32 [pw][pd]
+            e->sy_off = (uint32_t)(32 * e->pd);
+            e->sz_off = e->sy_off + (uint32_t)(32 * e->pw);   // (no SZ copy)
+            e->qz_off = e->sz_off;
+            e->agent_bytes = (e->qz_off + (uint32_t)(4 * e->pw * e->pd) + 63u) & ~63u;
+        } else {
+            e->sy_off = (uint32_t)(8 * e->pd * e->ph);
+            e->sz_off = e->sy_off + (uint32_t)(8 * e->pw * e->ph);
+            e->qz_off = e->sz_off + (uint32_t)(4 * e->pw * e->pd);
+            e->agent_bytes = (e->qz_off + (uint32_t)(4 * e->pw * e->pd) + 15u) & ~15u;
+        }
         e->xp_off = e->yp_off = 0;
-        e->agent_bytes = (e->qz_off + (uint32_t)(4 * e->pw * e->pd) + 15u) & ~15u;
     } else if (e->variant == VN_VARIANT_SIMPLE) {
         // dense [pw][pd][ph] int8 map, no planes
         e->pw = maxW;

@@ -97,6 +97,7 @@ GROUP_CASES = [("box:8x8x4", 4, 300, 200), ("set:P3_training", 10, 512, 150),
 
 @pytest.mark.parametrize("src,L,N,K", GROUP_CASES, ids=[f"{c[0]}-L{c[1]}" for c in GROUP_CASES])
 def test_simple_group_kernel_matches_oracle(voxnav, monkeypatch, src, L, N, K):
+    monkeypatch.setenv("VOXNAV_SIMPLE_LINE", "0")
     monkeypatch.setenv("VOXNAV_SIMPLE_GROUP", "1")
     _rollout_vs_oracle(src, L, N, K)
 
@@ -107,6 +108,7 @@ SPLIT_CASES = [("box:8x8x4", 4, 300, 200), ("set:P3_training", 10, 512, 150)]
 
 @pytest.mark.parametrize("src,L,N,K", SPLIT_CASES, ids=[f"{c[0]}-L{c[1]}" for c in SPLIT_CASES])
 def test_simple_split_kernel_matches_oracle(voxnav, monkeypatch, src, L, N, K):
+    monkeypatch.setenv("VOXNAV_SIMPLE_LINE", "0")
     monkeypatch.setenv("VOXNAV_SIMPLE_PIPE", "0")
     _rollout_vs_oracle(src, L, N, K)
 
@@ -118,9 +120,24 @@ ONE_WAVE_CASES = [("box:8x8x4", 4, 300, 200, "32"), ("set:P2_training", 10, 1000
 
 @pytest.mark.parametrize("src,L,N,K,aw", ONE_WAVE_CASES, ids=[f"{c[0]}-aw{c[4]}" for c in ONE_WAVE_CASES])
 def test_simple_one_wave_kernel_matches_oracle(voxnav, monkeypatch, src, L, N, K, aw):
+    monkeypatch.setenv("VOXNAV_SIMPLE_LINE", "0")
     monkeypatch.setenv("VOXNAV_SIMPLE_GROUP", "0")
     monkeypatch.setenv("VOXNAV_SIMPLE_SPLIT", "0")
     monkeypatch.setenv("VOXNAV_SIMPLE_AW", aw)
+    _rollout_vs_oracle(src, L, N, K)
+
+
+# the word-layout pipelined kernel (simple_pipe_kernel: the default for rooms
+# higher than 8 or wider / deeper than 32) on rooms the line layout takes by default
+PIPE_CASES = [("box:8x8x4", 4, 300, 200), ("set:P2_training", 4, 1024, 250), ("ctor:12x10x6", 10, 256, 200)]
+
+
+@pytest.mark.parametrize("src,L,N,K", PIPE_CASES, ids=[f"{c[0]}-L{c[1]}" for c in PIPE_CASES])
+def test_simple_word_layout_kernel_matches_oracle(voxnav, monkeypatch, src, L, N, K):
+    monkeypatch.setenv("VOXNAV_SIMPLE_LINE", "0")
+    env = make_env(src, L, n=8)
+    assert env.kernel_label(16).startswith("simple_pipe_kernel<")
+    env.close()
     _rollout_vs_oracle(src, L, N, K)
 
 
@@ -169,14 +186,15 @@ def _rollout_vs_oracle(src, L, N, K):
         np.testing.assert_array_equal(b, oenv.belief(i))
 
 
-def _bench_shaped_run(N, sample, K, F=128, src="box:32x32x8", L=4, policy_seed=42):
+def _bench_shaped_run(N, sample, K, F=128, src="box:32x32x8", L=4, policy_seed=42,
+                      label="simple_line_kernel<4, false>"):
     """The bench's simpleEnv call: ``step_random(out=...)`` in F-step launches
     into a reused [F, N, 6L+7] chunk, f32 reward, no action record; the
     sampled agents compared with the oracle launch by launch (the per-agent
     reset draw-ahead is carried across launches)."""
     from voxnav.env import Rollout
     env = make_env(src, L, n=N, autoreset=True)
-    assert env.kernel_label(F) == "simple_pipe_kernel<4>"
+    assert env.kernel_label(F) == label
     dev = env.device
     D = env.obs_dim
     out = Rollout(torch.empty((F, N, D), dtype=torch.float32, device=dev),
@@ -218,7 +236,7 @@ def _bench_shaped_run(N, sample, K, F=128, src="box:32x32x8", L=4, policy_seed=4
 
 
 def test_simple_bench_instantiation_all_agents(voxnav):
-    """The benched simpleEnv instantiation (simple_pipe_kernel<4>: 32x32x8,
+    """The benched simpleEnv instantiation (simple_line_kernel<4, false>: 32x32x8,
     L=4, 128-step launches, f32 reward) with 256 agents checked in full over
     2,560 steps: goal terminations (a goal-seeking episode ends every ~2k
     steps per agent under the random policy) and resets from the draw-ahead
@@ -237,6 +255,15 @@ def test_simple_bench_instantiation_full_batch_sampled(voxnav):
     sample = blocks * 64 + (blocks * 41 + 9) % 64
     ends = _bench_shaped_run(N, sample, 2560)
     assert ends["terminated"] > 0
+
+
+def test_simple_word_layout_bench_shape_sampled(voxnav, monkeypatch):
+    """The word-layout kernel (VOXNAV_SIMPLE_LINE=0) in the bench's launches:
+    4,096 agents, one sampled per 64-agent block, 1,280 steps."""
+    monkeypatch.setenv("VOXNAV_SIMPLE_LINE", "0")
+    N = 4096
+    blocks = np.arange(N // 64, dtype=np.int64)
+    _bench_shaped_run(N, blocks * 64 + (blocks * 23 + 5) % 64, 1280, label="simple_pipe_kernel<4, false>")
 
 
 def test_simple_step_actions_terminal_obs(voxnav):
