@@ -2440,6 +2440,60 @@ __device__ __forceinline__ void sp_observe(const Params &p, const SPlanes &pl, A
     row[6 * L + 6] = (float)g.last_action;
 }
 
+// Four ray cells at once: entry (bits | (clamp(m - 4c, -1, 4) + 1) << 4) of
+// the table holds the obs values of cells 4c..4c+3 of a ray with min(n, L) = m
+// free cells whose S bits (cells 4c..4c+3) are `bits`: the S bit below m, 2 at
+// m (the wall / edge terminator -- only reached when n < L), -1 beyond.
+constexpr int SL_CLUT = 96;
+__device__ __forceinline__ void sl_build_cell_lut(float4 *lut, int lane) {
+    for (int e = lane; e < SL_CLUT; e += 64) {
+        const int bits = e & 15, r = (e >> 4) - 1;
+        float v[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) v[i] = i < r ? (float)((bits >> i) & 1) : (i == r ? 2.0f : -1.0f);
+        lut[e] = make_float4(v[0], v[1], v[2], v[3]);
+    }
+}
+
+// sp_observe with the 4-cell table, for L == LMAX (the ray cells of a launch
+// written without per-cell compares or branches)
+template <int LMAX>
+__device__ __forceinline__ void sl_observe(const Params &p, const SPlanes &pl, Agent &g, const SRows &w, float *row,
+                                           const float4 *clut) {
+    const bool slow = (g.move_mask & 1u) || ((w.rec.y >> 17) & 1u);
+    if (__builtin_expect(__ballot(slow) != 0ull || p.L != LMAX, 0)) {
+        sb_observe<LMAX>(p, pl, g, w, row);
+        return;
+    }
+    constexpr int L = LMAX;
+#pragma unroll
+    for (int j = 0; j < 6; ++j) {
+        const uint32_t e8 = ray_e8(w.rec, j);
+        const int n = (int)(e8 & 0x7fu);
+        const int m = n < L ? n : L;
+        uint32_t t;   // bit s = the S bit of ray cell s + 1
+        if (j == 0) t = (uint32_t)w.wx >> ((g.x + 1) & 31);
+        else if (j == 2) t = (uint32_t)w.wy >> ((g.y + 1) & 31);
+        else if (j == 4) t = w.wz >> ((g.z + 1) & 31);
+        else if (j == 1) t = __builtin_bitreverse32((uint32_t)w.wx << ((32 - g.x) & 31));
+        else if (j == 3) t = __builtin_bitreverse32((uint32_t)w.wy << ((32 - g.y) & 31));
+        else t = __builtin_bitreverse32(w.wz << ((32 - g.z) & 31));
+        const int slot = obs_slot(j, g.facing);
+        float *out = row + slot * L;
+#pragma unroll
+        for (int c = 0; c < (L + 3) / 4; ++c) {
+            const int r = min(max(m - 4 * c, -1), 4);
+            const float4 q = clut[((t >> (4 * c)) & 15u) | ((uint32_t)(r + 1) << 4)];
+            out[4 * c] = q.x;
+            if (4 * c + 1 < L) out[4 * c + 1] = q.y;
+            if (4 * c + 2 < L) out[4 * c + 2] = q.z;
+            if (4 * c + 3 < L) out[4 * c + 3] = q.w;
+        }
+        row[6 * L + slot] = (float)m * 0.25f;   // round(count * 0.25, 2) is exact
+    }
+    row[6 * L + 6] = (float)g.last_action;
+}
+
 __device__ __forceinline__ void sb_load_rows(const Params &p, const SPlanes &pl, const Agent &g, const Room &R,
                                              SRows &w) {
     w.wx = pl.sx[g.y * p.ph + g.z];
@@ -3289,19 +3343,27 @@ __device__ __forceinline__ u32x4_t dpp_swap_pair4(u32x4_t v) {
 }
 
 // lane-pair line load: each lane gets the line at its byte offset `off`
-// (SL_OFF: none, zeros).  Must run with the whole wave active.
-__device__ __forceinline__ SLine sl_pair_load(__amdgpu_buffer_rsrc_t rs, uint32_t off, bool odd) {
-    const uint32_t off_e = dpp_swap_pair(off), off_o = dpp_swap_pair(off);
-    const uint32_t ae = odd ? off_e : off, ao = odd ? off : off_o;     // the pair's even / odd line
+// (SL_OFF: none, zeros).  Issue and finish (the swap across the pair, which
+// needs the data) are split so the loads stay in flight across a step.  Both
+// must run with the whole wave active.
+__device__ __forceinline__ SLine sl_pair_issue(__amdgpu_buffer_rsrc_t rs, uint32_t off, bool odd) {
+    const uint32_t off_p = dpp_swap_pair(off);
+    const uint32_t ae = odd ? off_p : off, ao = odd ? off : off_p;     // the pair's even / odd line
     const uint32_t half = odd ? 16u : 0u;
-    const u32x4_t r1 = __builtin_amdgcn_raw_buffer_load_b128(rs, ae == SL_OFF ? SL_OFF : ae + half, 0, 0);
-    const u32x4_t r2 = __builtin_amdgcn_raw_buffer_load_b128(rs, ao == SL_OFF ? SL_OFF : ao + half, 0, 0);
-    // even: r1 = own h0, r2 = partner's h0; odd: r1 = partner's h1, r2 = own h1
-    const u32x4_t sw = dpp_swap_pair4(odd ? r1 : r2);
+    SLine r;   // even: h0 = own h0, h1 = partner's h0; odd: h0 = partner's h1, h1 = own h1
+    r.h0 = __builtin_amdgcn_raw_buffer_load_b128(rs, ae == SL_OFF ? SL_OFF : ae + half, 0, 0);
+    r.h1 = __builtin_amdgcn_raw_buffer_load_b128(rs, ao == SL_OFF ? SL_OFF : ao + half, 0, 0);
+    return r;
+}
+__device__ __forceinline__ SLine sl_pair_finish(const SLine &r, bool odd) {
+    const u32x4_t sw = dpp_swap_pair4(odd ? r.h0 : r.h1);
     SLine l;
-    l.h0 = odd ? sw : r1;
-    l.h1 = odd ? r2 : sw;
+    l.h0 = odd ? sw : r.h0;
+    l.h1 = odd ? r.h1 : sw;
     return l;
+}
+__device__ __forceinline__ SLine sl_pair_load(__amdgpu_buffer_rsrc_t rs, uint32_t off, bool odd) {
+    return sl_pair_finish(sl_pair_issue(rs, off, odd), odd);
 }
 
 // lane-pair line store of each lane's line `l` at `off` (SL_OFF: none)
@@ -3390,7 +3452,8 @@ __global__ __launch_bounds__(128) void simple_line_kernel(Params p) {
     float *srew = sm + 2 * 64 * OD;
     uint32_t *sflg = reinterpret_cast<uint32_t *>(srew + 2 * 64);
     uint32_t *mt_lds = sflg + 2 * 64;
-    uint32_t *lines = mt_lds + 64 * MT_WS + 4;   // [2][64][SL_STRIDE]; 16-B aligned (see the launch)
+    uint32_t *lines = mt_lds + 64 * MT_WS + 4;   // [3][64][SL_STRIDE] (X, Y, dummy); 16-B aligned
+    float4 *clut = reinterpret_cast<float4 *>(lines + 3 * 64 * SL_STRIDE);   // [SL_CLUT] (sl_observe)
     const int lane = threadIdx.x & 63;
     const int a0 = blockIdx.x * 64;
     const int rows = min(64, p.N - a0);
@@ -3429,6 +3492,8 @@ __global__ __launch_bounds__(128) void simple_line_kernel(Params p) {
     const bool live = ai < p.N;
     uint32_t *lx = lines + lane * SL_STRIDE;           // SX[g.y]
     uint32_t *ly = lines + (64 + lane) * SL_STRIDE;    // SY[g.x]
+    uint32_t *lz = lines + (128 + lane) * SL_STRIDE;   // target of a commit's line write without a line
+    sl_build_cell_lut(clut, lane);
     const SPlanes pl = splanes(p, live ? ai : a0);
     Agent g = unpack(live ? p.hot[ai] : make_uint4(0u, 0u, 0u, 0u));
     uint32_t goal = live ? p.goal[ai] : 0u;
@@ -3455,16 +3520,21 @@ __global__ __launch_bounds__(128) void simple_line_kernel(Params p) {
     uint4 r4 = make_uint4(0u, 0u, 0u, 0u);      // Philox block r4blk (4 steps)
     uint64_t r4blk = ~0ull;
     SPend pm;                                    // the pending move ...
-    SLine ln;                                    // ... the line it brings in (in flight) ...
+    SLine lr;                                    // ... the line it brings in (raw pair loads, in flight;
+    bool lfwd = false;                           //     or the replaced line: lfwd) ...
+    uint32_t lpend = SL_OFF;                     //     (its offset: a re-issue repeats it) ...
     uint2 rn = make_uint2(0u, 0u);               // ... and its target's ray record (in flight)
     uint32_t dirty = 0u;                         // 1: the LDS X line is marked, 2: the Y line
     SLine ev;                                    // the line the last commit replaced, stored after the
     uint32_t ev_off = SL_OFF;                    // next move's loads (a load of it takes it from here)
     ev.h0 = ev.h1 = u32x4_t{0u, 0u, 0u, 0u};
-    ln = ev;
+    lr = ev;
     // the move of launch step k from the committed state; issues the target's loads
-    auto premove = [&](int k, bool act) {
-        uint32_t loff = SL_OFF;
+    // keep: lanes without `act` keep their pending move.  The line loads are
+    // re-issued for them too: a lane pair's two loads carry both lanes' lines
+    // (sl_pair_issue), so the pair always issues together.
+    auto premove = [&](int k, bool act, bool keep) {
+        uint32_t loff = (keep && !act) ? lpend : SL_OFF;
         uint32_t rcell = 0u;
         if (act) {
             const uint64_t t = p.t0 + (uint64_t)k;
@@ -3488,21 +3558,22 @@ __global__ __launch_bounds__(128) void simple_line_kernel(Params p) {
             pm.ny = g.y + (pm.moved ? (d == 2 ? 1 : d == 3 ? -1 : 0) : 0);
             pm.nz = g.z + (pm.moved ? (d == 4 ? 1 : d == 5 ? -1 : 0) : 0);
             rcell = (uint32_t)((pm.nx * R.D + pm.ny) * R.H + pm.nz);
-            // the line a move along x (y) brings in: SY[nx] (SX[ny]); from ev if it is
-            // the line the last commit replaced (its store is issued after these loads)
+            // the line a move along x (y) brings in: SY[nx] (SX[ny]); from ev (no
+            // request) if it is the line the last commit replaced
             if (pm.moved && d < 4) {
                 const uint32_t o = d < 2 ? yline_off(pm.nx) : xline_off(pm.ny);
                 if (o != ev_off) loff = o;
             }
         }
-        const SLine l = sl_pair_load(brs, loff, odd);
+        lr = sl_pair_issue(brs, loff, odd);
+        lpend = loff;
         const uint2 rc = p.rays[R.ray_off + rcell];
-        if (act) {                               // (a lane without a move keeps its pending one)
-            ln = loff == SL_OFF ? ev : l;        // forwarded (or unused)
+        if (!keep || act) {
+            lfwd = loff == SL_OFF;               // forwarded from ev (or unused)
             rn = rc;
         }
     };
-    if (p.K > 0) premove(0, live);
+    if (p.K > 0) premove(0, live, false);
 #if VN_SIMPLE_PROF
     uint64_t prof[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     uint64_t tprev = __builtin_amdgcn_s_memtime();
@@ -3522,36 +3593,46 @@ __global__ __launch_bounds__(128) void simple_line_kernel(Params p) {
             g.facing = pm.facing;
             a = pm.a;
             moved = pm.moved;
-            if (moved) {                                                 // _mark_visited (:273-298)
-                const int ax = pm.d >> 1;
-                // the target's S bit from the word along the move axis
-                seen = ax == 0 ? ((w.wx >> pm.nx) & 1ull) : ax == 1 ? ((w.wy >> pm.ny) & 1ull) : ((w.wz >> pm.nz) & 1u);
-                if (ax < 2) {
-                    // replace the line across the move axis: the old one is stored if marked
-                    uint32_t *slot = ax == 0 ? ly : lx;
-                    const uint32_t dbit = ax == 0 ? 2u : 1u;
-                    if (dirty & dbit) {
-                        ev = sl_lds_get(slot);
-                        ev_off = ax == 0 ? yline_off(g.x) : xline_off(g.y);
-                    }
-                    dirty &= ~dbit;
-                    sl_lds_put(slot, ln);
-                }
+        }
+        {
+            // _mark_visited (:273-298); straight-line for every lane: a lane
+            // whose move brings no line writes it to its dummy slot
+            const int ax = moved ? pm.d >> 1 : 3;
+            const bool xy = ax < 2;
+            // the target's S bit from the word along the move axis
+            seen = !moved || (ax == 0 ? ((w.wx >> pm.nx) & 1ull) : ax == 1 ? ((w.wy >> pm.ny) & 1ull)
+                                                                            : ((w.wz >> pm.nz) & 1u));
+            // replace the line across the move axis: the old one is stored if marked
+            uint32_t *slot = ax == 0 ? ly : ax == 1 ? lx : lz;
+            const uint32_t dbit = ax == 0 ? 2u : 1u;
+            const SLine lf = sl_pair_finish(lr, odd);
+            const SLine ln = lfwd ? ev : lf;
+            ev = sl_lds_get(slot);
+            ev_off = (xy && (dirty & dbit)) ? (ax == 0 ? yline_off(g.x) : xline_off(g.y)) : SL_OFF;
+            dirty &= xy ? ~dbit : ~0u;
+            sl_lds_put(slot, ln);
+            if (moved) {
                 g.x = pm.nx;
                 g.y = pm.ny;
                 g.z = pm.nz;
-                w.wx = lx[g.z];
-                w.wy = ly[g.z];
-                if (ax < 2) w.wz = sl_column(sl_lds_get(lx), g.x);
                 w.rec = rn;
             }
+            w.wx = lx[g.z];
+            w.wy = ly[g.z];
+            const uint32_t col = sl_column(sl_lds_get(lx), g.x);
+            if (xy) w.wz = col;
+        }
+        if (live) {
             g.last_action = a;                                           // :137
         }
         SB_T(0);
-        // ---- the next step's move and its loads, then the replaced line's
-        // store (a wait for the loads then never waits for the store) ----
-        premove(k + 1, live && k + 1 < p.K);
+        // ---- the replaced line's store, then the next step's move and its
+        // loads: vmcnt retires in issue order, so the wait for the loads (a
+        // step later) covers the older store at no cost; a store issued after
+        // them would be waited for as well (the compiler's counts do not
+        // include stores on this target and it waits vmcnt(0) for the last load) ----
         sl_pair_store(brs, ev_off, ev, odd);
+        premove(k + 1, live && k + 1 < p.K, false);
         ev_off = SL_OFF;
         SB_T(1);
         if (live) {
@@ -3573,7 +3654,7 @@ __global__ __launch_bounds__(128) void simple_line_kernel(Params p) {
                 }
             }
             SB_T(2);
-            if (!(VN_ABLATE & 4u)) sp_observe<LMAX>(p, pl, g, w, row);   // :139
+            if (!(VN_ABLATE & 4u)) sl_observe<LMAX>(p, pl, g, w, row, clut);   // :139
             SB_T(3);
             // compute_reward (:189-217), f64 in the reference's order
             double r = -0.1;
@@ -3609,7 +3690,7 @@ __global__ __launch_bounds__(128) void simple_line_kernel(Params p) {
                 dirty = 3u;                              // the start cell's lines (LDS only)
             }
             // from the start cell (the wave's loads are issued together)
-            premove(k + 1, need && k + 1 < p.K);
+            premove(k + 1, need && k + 1 < p.K, true);
         }
         SB_T(5);
         lds_handoff();                         // hand buffer b to the store wave
@@ -4177,7 +4258,7 @@ int launch_env(VnEnv *e, const Params &p, hipStream_t s) {
         if (!RESET_ONLY && e->sline) {
             // line layout: stepping wave + store wave per 64 agents (simple_line_kernel)
             const size_t lds = (size_t)2 * 64 * e->obs_dim * sizeof(float) + 2 * 64 * 8 + 64 * MT_WS * 4 +
-                               (4 + 2 * 64 * SL_STRIDE) * 4;
+                               (4 + 3 * 64 * SL_STRIDE) * 4 + SL_CLUT * 16;
             const dim3 grid((unsigned)((e->N + 63) / 64));
 #define VN_SL_LAUNCH(LM)                                                                   \
     do {                                                                                   \
