@@ -453,6 +453,10 @@ constexpr uint32_t KNOWN = 0x80u, WALLB = 0xC0u;
 // LDS table: [0,256) obs value of each belief byte; [256,262) f32(a/5);
 // [264,281) f32(c/L)   (get_obs :273-275, :284, :287)
 constexpr int TAB_ACTION = 256, TAB_CID = 264, TAB_SIZE = 288;
+// after the CubicEnv table in the same device buffer: the simpleEnv reward of
+// each event code (bit 0 bump, 1 repeated move, 2 goal, 3 explored), 16 f32
+// then 16 f64, each the reference's f64 sum in its order (envs/simpleEnv.py:189-217)
+constexpr int TAB_SREW = TAB_SIZE, TAB_SREW64 = TAB_SIZE + 16, TAB_ALL = TAB_SIZE + 48;
 
 __device__ __forceinline__ int decode_count(uint32_t b) {   // center cell: known free or unknown
     return (b & KNOWN) ? (int)(b & 0x3fu) : -1;
@@ -1798,7 +1802,15 @@ __global__ __launch_bounds__(PCM ? VN_PC_BLOCK : BLOCK, PCM ? VN_PC_MIN_WAVES : 
             SetLoad<RT> pl;
             if (shifted) tile_shift_issue<PH>(p, map, tile, dir, g.x, g.y, R, dirty, q, sl);
             if (PC && shifted) pset_shift_issue(p, map, ps, dir, g.x, g.y, R, pdirty, q, pl);
-            const uint2 rec = p.rays[R.ray_off + (uint32_t)((g.x * R.D + g.y) * R.H + g.z)];
+            uint2 rec;
+            if (VN_ABLATE & 8192u) {   // diagnostics: the record computed for a walled box (exact for box rooms only)
+                const uint32_t ex = (uint32_t)(R.W - 2 - g.x) | 0x80u, wx = (uint32_t)(g.x - 1) | 0x80u;
+                const uint32_t ey = (uint32_t)(R.D - 2 - g.y) | 0x80u, wy = (uint32_t)(g.y - 1) | 0x80u;
+                const uint32_t ez = (uint32_t)(R.H - 2 - g.z) | 0x80u, wz = (uint32_t)(g.z - 1) | 0x80u;
+                rec = make_uint2(ex | (wx << 8) | (ey << 16) | (wy << 24), ez | (wz << 8));
+            } else {
+                rec = p.rays[R.ray_off + (uint32_t)((g.x * R.D + g.y) * R.H + g.z)];
+            }
             if (!PC) plane_prefetch<PH>(p, map, pc_, g.x, g.y, g.z, q);
             ENV_T(0);
             if (shifted) {
@@ -3454,6 +3466,8 @@ __global__ __launch_bounds__(128) void simple_line_kernel(Params p) {
     uint32_t *mt_lds = sflg + 2 * 64;
     uint32_t *lines = mt_lds + 64 * MT_WS + 4;   // [3][64][SL_STRIDE] (X, Y, dummy); 16-B aligned
     float4 *clut = reinterpret_cast<float4 *>(lines + 3 * 64 * SL_STRIDE);   // [SL_CLUT] (sl_observe)
+    float *srt = reinterpret_cast<float *>(clut + SL_CLUT);   // [16] f32, then [16] f64 rewards (TAB_SREW)
+    const double *srt64 = reinterpret_cast<const double *>(srt + 16);
     const int lane = threadIdx.x & 63;
     const int a0 = blockIdx.x * 64;
     const int rows = min(64, p.N - a0);
@@ -3494,6 +3508,7 @@ __global__ __launch_bounds__(128) void simple_line_kernel(Params p) {
     uint32_t *ly = lines + (64 + lane) * SL_STRIDE;    // SY[g.x]
     uint32_t *lz = lines + (128 + lane) * SL_STRIDE;   // target of a commit's line write without a line
     sl_build_cell_lut(clut, lane);
+    if (lane < 48) srt[lane] = p.lut[TAB_SREW + lane];
     const SPlanes pl = splanes(p, live ? ai : a0);
     Agent g = unpack(live ? p.hot[ai] : make_uint4(0u, 0u, 0u, 0u));
     uint32_t goal = live ? p.goal[ai] : 0u;
@@ -3656,25 +3671,19 @@ __global__ __launch_bounds__(128) void simple_line_kernel(Params p) {
             SB_T(2);
             if (!(VN_ABLATE & 4u)) sl_observe<LMAX>(p, pl, g, w, row, clut);   // :139
             SB_T(3);
-            // compute_reward (:189-217), f64 in the reference's order
-            double r = -0.1;
-            if (!moved) {
-                g.bumps += 1;
-                r += -10.0;
-            }
-            if (a != 2 && a < 4) r += 0.05;
+            // compute_reward (:189-217): the reference's f64 sum for the step's
+            // events, tabulated on the host in its order (TAB_SREW)
             const int gx = goal & 0xff, gy = (goal >> 8) & 0xff, gz = (goal >> 16) & 0xff;
-            if (g.x == gx && g.y == gy && g.z >= gz && g.z - gz < 5) {   // SPOT_GOAL_HEIGTH = 5 (:201-206)
-                g.done = true;
-                r += 100.0;
-            }
-            if (trunc) r += 0.0;
-            if (explored) r += 1.0;
+            const bool hit = g.x == gx && g.y == gy && g.z >= gz && g.z - gz < 5;   // SPOT_GOAL_HEIGTH = 5
+            if (!moved) g.bumps += 1;
+            if (hit) g.done = true;
+            const uint32_t ev = (moved ? 0u : 1u) | ((a != 2 && a < 4) ? 2u : 0u) | (hit ? 4u : 0u) |
+                                (explored ? 8u : 0u);
             term = g.done;
             const size_t o = (size_t)k * p.N + ai;
-            srew[b * 64 + lane] = (float)r;
+            srew[b * 64 + lane] = srt[ev];
             sflg[b * 64 + lane] = (term ? 1u : 0u) | (trunc ? 2u : 0u);
-            if (p.reward64) p.reward64[o] = r;
+            if (p.reward64) p.reward64[o] = srt64[ev];
             if ((term || trunc) && p.autoreset && p.terminal_obs) {
                 float *to = p.terminal_obs + o * OD;
                 for (int q = 0; q < OD; ++q) to[q] = row[q];
@@ -4258,7 +4267,7 @@ int launch_env(VnEnv *e, const Params &p, hipStream_t s) {
         if (!RESET_ONLY && e->sline) {
             // line layout: stepping wave + store wave per 64 agents (simple_line_kernel)
             const size_t lds = (size_t)2 * 64 * e->obs_dim * sizeof(float) + 2 * 64 * 8 + 64 * MT_WS * 4 +
-                               (4 + 3 * 64 * SL_STRIDE) * 4 + SL_CLUT * 16;
+                               (4 + 3 * 64 * SL_STRIDE) * 4 + SL_CLUT * 16 + 48 * 4;
             const dim3 grid((unsigned)((e->N + 63) / 64));
 #define VN_SL_LAUNCH(LM)                                                                   \
     do {                                                                                   \
@@ -4604,8 +4613,18 @@ int vn_create(const VnRoomSet *rooms, int32_t n_agents, const VnConfig *cfg, int
     // LDS table (TAB_SIZE floats): obs value of every belief byte (decode,
     // clip to [-2, 20], (v + 2) / 22 in IEEE f32 -- :273-275), f32(a / 5.0)
     // (:284) and f32(c / L) (:287), all computed on the host.
-    float lut[TAB_SIZE];
-    for (int k = 0; k < TAB_SIZE; ++k) lut[k] = 0.0f;
+    float lut[TAB_ALL];
+    for (int k = 0; k < TAB_ALL; ++k) lut[k] = 0.0f;
+    for (int ev = 0; ev < 16; ++ev) {   // simpleEnv compute_reward (:189-217) by event code, in its order
+        volatile double r = -0.1;
+        if (ev & 1) r = r + -10.0;
+        if (ev & 2) r = r + 0.05;
+        if (ev & 4) r = r + 100.0;
+        if (ev & 8) r = r + 1.0;        // (the truncation term adds 0.0: no change)
+        const double rv = r;
+        lut[TAB_SREW + ev] = (float)rv;
+        std::memcpy(&lut[TAB_SREW64 + 2 * ev], &rv, sizeof(double));
+    }
     for (int b = 0; b < 256; ++b) {
         int v = (b & 0x80) ? ((b & 0x40) ? -2 : (b & 0x3f)) : -1;
         if (v > 20) v = 20;
