@@ -8,9 +8,11 @@ set -u
 cd "${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-BARGS="${BENCH_ARGS:-} --single-step-check 0 --collector none --simple 0 --fuse-check 0"
+BARGS="${BENCH_ARGS:-} --single-step-check 0 --collector none --simple 0 --fuse-check 0 --room-sets none"
+# the driver's own window (--steps 20 --warmup 5): the headline launches only
+DARGS="--steps 20 --warmup 5 --cpu-seconds 0 --episode-window 0 $BARGS"
 TAG=${TAG:-r02}
-PASSES=${PASSES:-trace,simple,simple_fetch,simple_write,trace_f1,fetch,write,l2,sq,sqw,tcp}
+PASSES=${PASSES:-dtrace,dfetch,dwrite,trace,simple,simple_fetch,simple_write,trace_f1,fetch,write,l2,sq,sqw,tcp}
 step() {
   local name=$1 t=$2; shift 2
   [[ ",$PASSES," == *",$name,"* ]] || return 0
@@ -19,10 +21,13 @@ step() {
   echo "[$name] rc=$rc"; grep -h '"metric"' "gpurun_out/${TAG}_$name.log" | cut -c1-200
   [ $rc -eq 0 ] || exit $rc
 }
+step dtrace 300 rocprofv3 --kernel-trace --stats -d gpurun_out/${TAG}_dtrace -o trace --output-format csv -- python3 bench.py $DARGS
+step dfetch 300 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/${TAG}_dfetch -o fetch --output-format csv -- python3 bench.py $DARGS
+step dwrite 300 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/${TAG}_dwrite -o write --output-format csv -- python3 bench.py $DARGS
 step trace 400 rocprofv3 --kernel-trace --stats -d gpurun_out/${TAG}_trace -o trace --output-format csv -- python3 bench.py --steps 5408 --warmup 32 --cpu-seconds 0 $BARGS
-step simple 400 rocprofv3 --kernel-trace --stats -d gpurun_out/${TAG}_simple -o trace --output-format csv -- python3 bench.py --steps 5408 --warmup 32 --cpu-seconds 0 --single-step-check 0 --collector none --simple 1 --fuse-check 0 --episode-window 0
-step simple_fetch 400 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/${TAG}_simple_fetch -o fetch --output-format csv -- python3 bench.py --steps 5408 --warmup 32 --cpu-seconds 0 --single-step-check 0 --collector none --simple 1 --fuse-check 0 --episode-window 0
-step simple_write 400 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/${TAG}_simple_write -o write --output-format csv -- python3 bench.py --steps 5408 --warmup 32 --cpu-seconds 0 --single-step-check 0 --collector none --simple 1 --fuse-check 0 --episode-window 0
+step simple 400 rocprofv3 --kernel-trace --stats -d gpurun_out/${TAG}_simple -o trace --output-format csv -- python3 bench.py --steps 5408 --warmup 32 --cpu-seconds 0 --single-step-check 0 --collector none  --simple 1 --fuse-check 0 --episode-window 0 --room-sets none
+step simple_fetch 400 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/${TAG}_simple_fetch -o fetch --output-format csv -- python3 bench.py --steps 5408 --warmup 32 --cpu-seconds 0 --single-step-check 0 --collector none  --simple 1 --fuse-check 0 --episode-window 0 --room-sets none
+step simple_write 400 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/${TAG}_simple_write -o write --output-format csv -- python3 bench.py --steps 5408 --warmup 32 --cpu-seconds 0 --single-step-check 0 --collector none  --simple 1 --fuse-check 0 --episode-window 0 --room-sets none
 step trace_f1 400 rocprofv3 --kernel-trace --stats -d gpurun_out/${TAG}_trace_f1 -o trace --output-format csv -- python3 bench.py --steps 200 --warmup 20 --cpu-seconds 0 $BARGS --fuse 1
 step fetch 400 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/${TAG}_fetch -o fetch --output-format csv -- python3 bench.py --steps 5408 --warmup 32 --cpu-seconds 0 $BARGS
 step write 400 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/${TAG}_write -o write --output-format csv -- python3 bench.py --steps 5408 --warmup 32 --cpu-seconds 0 $BARGS
