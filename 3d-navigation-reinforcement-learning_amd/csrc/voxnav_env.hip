@@ -1462,6 +1462,9 @@ __global__ __launch_bounds__(PCM ? VN_PC_BLOCK : BLOCK, PCM ? VN_PC_MIN_WAVES : 
     if (p.N < 0) lds_pad[threadIdx.x] = 0ull;
     if (p.N < 0) p.obs[0] = (float)lds_pad[threadIdx.x ^ 1];
 #endif
+#if VN_ENV_PROF
+    const uint64_t tkern = __builtin_amdgcn_s_memtime();
+#endif
     const int q = threadIdx.x & (GROUP - 1);
     const int i = (int)((blockIdx.x * blockDim.x + threadIdx.x) / GROUP);
     const bool active = i < p.N;
@@ -1957,9 +1960,14 @@ __global__ __launch_bounds__(PCM ? VN_PC_BLOCK : BLOCK, PCM ? VN_PC_MIN_WAVES : 
     if ((VN_ABLATE & 4096u) && abl_sink == 12345.f) p.obs[0] = abl_sink;
 #if VN_ENV_PROF
     if (FAST && PC && (threadIdx.x & 63) == 0) {
+        __builtin_amdgcn_s_waitcnt(0);   // the flush's stores issued and retired
+        const uint64_t tend = __builtin_amdgcn_s_memtime();
         for (int k = 0; k < 7; ++k) atomicAdd(&g_env_prof[k], (unsigned long long)eprof[k]);
         atomicAdd(&g_env_prof[7], (unsigned long long)(tprev - tstart));
         atomicAdd(&g_env_prof[8], 1ull);
+        atomicAdd(&g_env_prof[9], (unsigned long long)(tstart - tkern));   // prologue: LUT, state, fill
+        atomicAdd(&g_env_prof[10], (unsigned long long)(tend - tprev));    // epilogue: flush, state
+        atomicMax(&g_env_prof[11], (unsigned long long)(tend - tkern));    // longest wave
     }
 #endif
 }

@@ -229,12 +229,27 @@ class BatchedGridEnv:
             tr = torch.empty((K, N), dtype=torch.uint8, device=self.device)
             act = torch.empty((K, N), dtype=torch.int32, device=self.device) if record_actions else None
         else:
+            self._check_rollout(out, K, reward_f64)
             obs, rew, te, tr, act = out
         _native.check(self.lib.vn_step_random(self._h, int(policy_seed), int(t0), K, _ptr(act), _ptr(obs),
                                               None if reward_f64 else _ptr(rew), _ptr(rew) if reward_f64 else None,
                                               _ptr(te), _ptr(tr), None, self._stream()), "vn_step_random")
         self._t = int(t0) + K
         return Rollout(obs, rew, te, tr, act)
+
+    def _check_rollout(self, out: Rollout, K: int, reward_f64: bool):
+        """A caller-owned [K, N, ...] rollout chunk: the kernel writes all K
+        steps, so a short or mistyped buffer is refused here."""
+        N, dev = self.num_agents, self.device
+        obs, rew, te, tr, act = out
+        rdt = torch.float64 if reward_f64 else torch.float32
+        for name, t, dt, shape in (("obs", obs, torch.float32, (K, N, self.obs_dim)), ("reward", rew, rdt, (K, N)),
+                                   ("terminated", te, torch.uint8, (K, N)), ("truncated", tr, torch.uint8, (K, N))):
+            if t.dtype != dt or tuple(t.shape) != shape or not t.is_contiguous() or t.device != dev:
+                raise ValueError(f"out.{name}: expected contiguous {dt} {shape} on {dev}")
+        if act is not None and (act.dtype != torch.int32 or tuple(act.shape) != (K, N) or not act.is_contiguous()
+                                or act.device != dev):
+            raise ValueError(f"out.actions: expected contiguous int32 {(K, N)} on {dev}")
 
     def step_random_launcher(self, k_steps: int, policy_seed: int, t0: int, out: Rollout, reward_f64: bool = False):
         """``step_random(k_steps, policy_seed, t0, out=out)`` prepared: the
@@ -243,10 +258,9 @@ class BatchedGridEnv:
         loops whose host overhead per launch should be the launch itself)."""
         if not self._was_reset:
             raise RuntimeError("call reset() before step_random()")
-        K, N = int(k_steps), self.num_agents
+        K = int(k_steps)
+        self._check_rollout(out, K, reward_f64)
         obs, rew, te, tr, act = out
-        if tuple(obs.shape) != (K, N, self.obs_dim) or tuple(rew.shape) != (K, N) or not obs.is_contiguous():
-            raise ValueError("out: expected contiguous [K, N, obs_dim] obs and [K, N] rewards")
         args = (self._h, int(policy_seed), int(t0), K, _ptr(act), _ptr(obs), None if reward_f64 else _ptr(rew),
                 _ptr(rew) if reward_f64 else None, _ptr(te), _ptr(tr), None, self._stream())
         fn = self.lib.vn_step_random

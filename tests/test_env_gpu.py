@@ -160,6 +160,29 @@ def test_step_with_actions_f32_matches_oracle(voxnav):
         np.testing.assert_array_equal(res.terminal_obs.cpu().numpy()[done], orc["terminal_obs"][k][done])
 
 
+def test_step_random_refuses_short_rollout_buffers(voxnav):
+    """A caller-owned rollout chunk shorter than k_steps (or mistyped) is
+    refused before the launch: the kernel writes all K steps."""
+    from voxnav.env import Rollout
+    N = 64
+    env = make_env(voxnav, "box:8x8x4", 4, n=N, autoreset=True)
+    env.reset(seed=3)
+    dev = env.device
+
+    def chunk(K, rdt=torch.float32):
+        return Rollout(torch.empty((K, N, 80), device=dev), torch.empty((K, N), dtype=rdt, device=dev),
+                       torch.empty((K, N), dtype=torch.uint8, device=dev),
+                       torch.empty((K, N), dtype=torch.uint8, device=dev), None)
+    with pytest.raises(ValueError):
+        env.step_random(5, out=chunk(1))
+    with pytest.raises(ValueError):
+        env.step_random(2, out=chunk(2, torch.float64))
+    with pytest.raises(ValueError):
+        env.step_random_launcher(3, 7, 0, chunk(2))
+    env.step_random(2, out=chunk(2))          # the right shape runs
+    torch.cuda.synchronize()
+
+
 def test_step_with_actions_autoreset_terminal_obs(voxnav):
     """vn_step with explicit actions: obs/terminal_obs/flags vs oracle (SB3 semantics)."""
     src, L, N, K = "box:8x8x4", 4, 384, 160
