@@ -731,6 +731,76 @@ int policy_head_launch(const T *latent_pi, const T *latent_vf, int32_t N, int32_
 }  // namespace
 
 
+// One launch after the collector's env step (vn_collect_post_step): what
+// episode_start_kernel, monitor_kernel, boot_compact_kernel and
+// collect_stash_kernel did in four, one lane per agent.  The truncated
+// agents' stash rows are claimed with one atomic per wave (rows are in wave
+// order within a wave, waves in completion order: the bootstrap is per row,
+// so the order does not change any value).  Done agents' state rows are
+// zeroed by their wave together (zB LSTMs; 0: none).
+__global__ __launch_bounds__(256) void collect_post_kernel(
+    const uint8_t *__restrict__ term, const uint8_t *__restrict__ trunc, int N, int t, float *__restrict__ starts,
+    const double *__restrict__ r64, const float *__restrict__ r32, double *__restrict__ ep_ret,
+    int32_t *__restrict__ ep_len, double *__restrict__ rec_ret, int32_t *__restrict__ rec_len,
+    const float *__restrict__ tobs, int obs_dim, const uint8_t *__restrict__ h, int h_bytes,
+    const float *__restrict__ c, int H, float *__restrict__ st_obs, uint8_t *__restrict__ st_h,
+    float *__restrict__ st_c, int32_t *__restrict__ st_flat, int cap, int32_t *__restrict__ st_count,
+    float *__restrict__ zh, float *__restrict__ zc, uint16_t *__restrict__ zh_bf, int zB) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    const int lane = threadIdx.x & 63;
+    const int a0 = i - lane;
+    const bool live = i < N;
+    const bool te = live && term[i] != 0, tr = live && trunc[i] != 0;
+    const bool done = te || tr;
+    if (live && starts) starts[i] = done ? 1.0f : 0.0f;
+    if (live && ep_ret) {                         // SB3 Monitor (as monitor_kernel)
+        const double r = ep_ret[i] + (r64 ? r64[i] : (double)r32[i]);
+        const int32_t l = ep_len[i] + 1;
+        rec_ret[i] = done ? r : 0.0;
+        rec_len[i] = done ? l : 0;
+        ep_ret[i] = done ? 0.0 : r;
+        ep_len[i] = done ? 0 : l;
+    }
+    // the truncated (not terminated) agents' terminal obs + critic state into the stash
+    uint64_t m = __ballot(tr && !te);
+    if (m) {
+        int base = 0;
+        if (lane == 0) base = atomicAdd(st_count, __popcll(m));
+        base = __shfl(base, 0);
+        while (m) {
+            const int src = __ffsll((unsigned long long)m) - 1;
+            m &= m - 1;
+            const int r = base++;
+            if (r >= cap) continue;                  // dropped; the caller checks the count against cap
+            const int a = a0 + src;
+            if (lane == 0) st_flat[r] = t * N + a;
+            for (int k = lane; k < obs_dim; k += 64) st_obs[(size_t)r * obs_dim + k] = tobs[(size_t)a * obs_dim + k];
+            if (h) {
+                const int hw = H * h_bytes / 4;
+                const uint32_t *hs = reinterpret_cast<const uint32_t *>(h) + (size_t)a * hw;
+                uint32_t *hd = reinterpret_cast<uint32_t *>(st_h) + (size_t)r * hw;
+                for (int k = lane; k < hw; k += 64) hd[k] = hs[k];
+                for (int k = lane; k < H; k += 64) st_c[(size_t)r * H + k] = c[(size_t)a * H + k];
+            }
+        }
+    }
+    // zero the (h, c) rows of done agents where the next step reads the state arrays
+    uint64_t md = __ballot(done && zB > 0);
+    while (md) {
+        const int src = __ffsll((unsigned long long)md) - 1;
+        md &= md - 1;
+        const int a = a0 + src;
+        for (int b = 0; b < zB; ++b) {
+            const size_t so = ((size_t)b * N + a) * H;
+            for (int k = lane; k < H; k += 64) {
+                zh[so + k] = 0.0f;
+                zc[so + k] = 0.0f;
+                if (zh_bf) zh_bf[so + k] = 0;
+            }
+        }
+    }
+}
+
 // SB3 Monitor (stable_baselines3/common/monitor.py, wrapping every worker at
 // train/Grid_Train.py:125): per agent the running episode return (f64, summed
 // in step order from 0 like Monitor's sum(self.rewards)) and length; on
@@ -893,6 +963,29 @@ int vn_episode_start(const uint8_t *terminated, const uint8_t *truncated, int32_
     const int64_t threads = n_lstm ? (int64_t)n_lstm * N * (H / 4) : (int64_t)N;
     hipLaunchKernelGGL(episode_start_kernel, dim3(blocks_for(threads)), dim3(256), 0, (hipStream_t)stream,
                        terminated, truncated, (int)N, episode_starts, h, c, h_bf16, (int)n_lstm, (int)H);
+    VN_HIP(hipGetLastError());
+    return VN_OK;
+}
+
+int vn_collect_post_step(const uint8_t *terminated, const uint8_t *truncated, int32_t N, int32_t t,
+                         float *episode_starts, const double *reward64, const float *reward, double *ep_return,
+                         int32_t *ep_length, double *rec_return, int32_t *rec_length, const float *terminal_obs,
+                         int32_t obs_dim, const void *h_critic, int32_t h_bytes, const float *c_critic, int32_t H,
+                         float *stash_obs, void *stash_h, float *stash_c, int32_t *stash_flat, int32_t cap,
+                         int32_t *stash_count, float *h, float *c, uint16_t *h_bf16, int32_t n_lstm, void *stream) {
+    if (!terminated || !truncated || !terminal_obs || !stash_obs || !stash_flat || !stash_count)
+        return fail(VN_ERR_INVALID, "NULL argument");
+    if (N < 1 || t < 0 || obs_dim < 1 || cap < 0) return fail(VN_ERR_INVALID, "bad sizes N=%d t=%d obs_dim=%d", N, t, obs_dim);
+    if (ep_return && (!ep_length || !rec_return || !rec_length || (!reward64 && !reward)))
+        return fail(VN_ERR_INVALID, "incomplete monitor arguments");
+    if (h_critic && (!c_critic || !stash_h || !stash_c || H < 1 || (h_bytes != 2 && h_bytes != 4) || ((H * h_bytes) & 3)))
+        return fail(VN_ERR_INVALID, "bad critic-state arguments");
+    if (n_lstm < 0 || (n_lstm > 0 && (!h || !c || H < 1))) return fail(VN_ERR_INVALID, "bad state-zeroing arguments");
+    hipLaunchKernelGGL(collect_post_kernel, dim3(blocks_for(N)), dim3(256), 0, (hipStream_t)stream, terminated,
+                       truncated, (int)N, (int)t, episode_starts, reward64, reward, ep_return, ep_length, rec_return,
+                       rec_length, terminal_obs, (int)obs_dim, reinterpret_cast<const uint8_t *>(h_critic),
+                       (int)h_bytes, c_critic, (int)H, stash_obs, reinterpret_cast<uint8_t *>(stash_h), stash_c,
+                       stash_flat, (int)cap, stash_count, h, c, h_bf16, (int)n_lstm);
     VN_HIP(hipGetLastError());
     return VN_OK;
 }

@@ -86,6 +86,8 @@ _SIGS = {
     "vn_collect_stash": (C.c_int, [P, P, P, P, C.c_int32, C.c_int32, P, C.c_int32, P, C.c_int32, P, C.c_int32, P, P,
                                    P, P, C.c_int32, P]),
     "vn_monitor_step": (C.c_int, [P, P, P, P, C.c_int32, P, P, P, P, P]),
+    "vn_collect_post_step": (C.c_int, [P, P, C.c_int32, C.c_int32, P, P, P, P, P, P, P, P, C.c_int32, P, C.c_int32,
+                                       P, C.c_int32, P, P, P, P, C.c_int32, P, P, P, P, C.c_int32, P]),
     "vn_episode_start": (C.c_int, [P, P, C.c_int32, P, P, P, P, C.c_int32, C.c_int32, P]),
     "vn_lstm_seq_fwd_cell": (C.c_int, [P, C.c_int64, C.c_int64, P, C.c_int64, P, P, P, P, C.c_int64, C.c_int32,
                                        C.c_int32, C.c_int32, P]),

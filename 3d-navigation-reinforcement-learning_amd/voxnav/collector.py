@@ -14,15 +14,14 @@ per step t
      ``vn_policy_head`` (logits, value, Categorical draw, log-prob)
   2. ``BatchedGridEnv.step_into`` -> obs[t+1], reward[t], terminated,
      truncated, terminal_obs (SB3 auto-reset inside the env kernel)
-  3. ``vn_collect_compact`` -> ordered indices of the truncated agents
-     (SB3: ``done and info["TimeLimit.truncated"]``); ``vn_collect_stash``
-     appends their terminal obs and critic state after step t to a device
-     stash (the count never leaves the GPU)
-  4. ``vn_episode_start`` -> episode_starts[t+1] = done, zero the (h, c) of
-     those agents (``_process_sequence``'s ``(1 - episode_start)`` mask)
-
-  5. ``vn_monitor_step`` -> the SB3 Monitor's per-agent episode return
-     (f64) / length and the episodes that ended at step t (voxnav.monitor)
+  3. ``vn_collect_post_step`` (one launch) -> episode_starts[t+1] = done;
+     the SB3 Monitor's per-agent episode return (f64) / length and the
+     episodes that ended at step t (voxnav.monitor); the truncated agents
+     (SB3: ``done and info["TimeLimit.truncated"]``) append their terminal
+     obs and critic state after step t to a device stash (the count never
+     leaves the GPU); the (h, c) of finished agents zeroed where the next
+     step reads the state arrays (``_process_sequence``'s
+     ``(1 - episode_start)`` mask; the f32 buffer path masks on read)
 
 after T steps: the stashed terminal values V(terminal_obs; critic state)
 in one batch (equal to the per-step values up to the GEMMs' rounding), added
@@ -219,8 +218,6 @@ class RolloutCollector:
         self._term = z(N, dt=torch.uint8)
         self._trunc = z(N, dt=torch.uint8)
         self._tobs = z(N, env.obs_dim)
-        self._boot_idx = z(N, dt=torch.int32)
-        self._boot_cnt = z(1, dt=torch.int32)
         self._last_values = z(N)
         self.recurrent = self.w.recurrent
         # the f32 MLP kernels' per-layer outputs, [branch][rows][width]; sized
@@ -251,7 +248,7 @@ class RolloutCollector:
         self._flush_every = min(T, 4 * fmin)
         self._stash_cap = N * ((self._flush_every - 1) // fmin + 1)
         cap = self._stash_cap
-        self._stash_base = z(T + 1, dt=torch.int32)
+        self._stash_cnt = z(1, dt=torch.int32)       # stash rows used (vn_collect_post_step's running count)
         self._stash_obs = z(cap, env.obs_dim)
         self._stash_flat = z(cap, dt=torch.int32)
         if self.recurrent:
@@ -483,8 +480,7 @@ class RolloutCollector:
         mon = self.monitor
         if mon is not None:
             mon.begin()
-        self._stash_base.zero_()
-        sb = self._stash_base
+        self._stash_cnt.zero_()
         rec = self.recurrent
         # with the buffer, the fused bf16 step keeps the cell state in lstm_c
         # only (vn_lstm_fused_bf16_masked) and the f32 step both h and c in
@@ -496,40 +492,38 @@ class RolloutCollector:
             self._forward(self._obs[t], t, in_rollout=True)
             self.env.step_into(self.actions[t], self._obs[t + 1], self.rewards[t], self._term, self._trunc,
                                self._tobs, reward64=self._r64)
-            if mon is not None:
-                mon.step(t, self._term, self._trunc, reward64=self._r64)
-            _native.check(lib.vn_collect_compact(_p(self._term), _p(self._trunc), N, _p(self._boot_idx),
-                                                 _p(self._boot_cnt), s()), "vn_collect_compact")
-            # the truncated agents' terminal obs and critic state (before the
-            # episode-start mask below) into the stash; no host read here.  The
-            # fused path's h_bf is a ping-pong pair: read it after this step's swap
+            # after the step, in one launch: episode_starts[t+1], the Monitor, the
+            # truncated agents' terminal obs and critic state (before the
+            # episode-start mask) into the bootstrap stash -- no host read -- and
+            # the (h, c) rows of finished agents zeroed only where the next step
+            # reads the state arrays themselves (the f32 buffer path reads
+            # lstm_h / lstm_c[t+1] and masks on read).  The fused path's h_bf is
+            # a ping-pong pair: read it after this step's swap
             hsrc = (self._hs[t + 1] if hbuf else self.h_bf if self.fused else self.h) if rec else None
-            _native.check(lib.vn_collect_stash(
-                _p(self._boot_idx), _p(self._boot_cnt), _p(sb[t]), _p(sb[t + 1]), t, N, _p(self._tobs),
-                self.env.obs_dim, _p(hsrc[1]) if rec else None, hsrc.element_size() if rec else 0,
-                _p(self._cs[t + 1][1] if csbuf else self.c[1]) if rec else None, self.w.H if rec else 0,
-                _p(self._stash_obs),
-                _p(self._stash_h) if rec else None, _p(self._stash_c) if rec else None, _p(self._stash_flat),
-                self._stash_cap, s()), "vn_collect_stash")
-            # episode_starts[t+1]; the (h, c) rows of finished agents are zeroed
-            # only where the next step reads the state arrays themselves (the
-            # f32 buffer path reads lstm_h / lstm_c[t+1] and masks on read)
             zs = rec and not hbuf
-            _native.check(lib.vn_episode_start(_p(self._term), _p(self._trunc), N, _p(self._starts[t + 1]),
-                                               _p(self.h) if zs else None, _p(self.c) if zs else None,
-                                               _p(self.h_bf) if zs else None, 2 if zs else 0,
-                                               self.w.H if zs else 0, s()), "vn_episode_start")
+            _native.check(lib.vn_collect_post_step(
+                _p(self._term), _p(self._trunc), N, t, _p(self._starts[t + 1]),
+                _p(self._r64) if mon is not None else None, None,
+                _p(mon.ep_return) if mon is not None else None, _p(mon.ep_length) if mon is not None else None,
+                _p(mon.rec_return[t]) if mon is not None else None, _p(mon.rec_length[t]) if mon is not None else None,
+                _p(self._tobs), self.env.obs_dim,
+                _p(hsrc[1]) if rec else None, hsrc.element_size() if rec else 0,
+                _p(self._cs[t + 1][1] if csbuf else self.c[1]) if rec else None, self.w.H if rec else 0,
+                _p(self._stash_obs), _p(self._stash_h) if rec else None, _p(self._stash_c) if rec else None,
+                _p(self._stash_flat), self._stash_cap, _p(self._stash_cnt),
+                _p(self.h) if zs else None, _p(self.c) if zs else None, _p(self.h_bf) if zs else None,
+                2 if zs else 0, s()), "vn_collect_post_step")
             self.t_global += 1
             if (t + 1) % self._flush_every == 0 and t + 1 < T:
-                self._bootstrap(sb[t + 1])       # bounded stash: flush, restart at row 0
-                sb[t + 1].zero_()
+                self._bootstrap(self._stash_cnt)   # bounded stash: flush, restart at row 0
+                self._stash_cnt.zero_()
         if csbuf:   # the current (masked) state: lstm_c[T] (lstm_h[T]) with the episode-start mask
             done = self._starts[T][None, :, None] != 0
             torch.where(done, self._zero, self._cs[T], out=self.c)      # no rollout-sized temporaries
             if hbuf:
                 torch.where(done, self._zero, self._hs[T], out=self.h)
         # the truncation bootstrap of the rest of the rollout
-        self._bootstrap(sb[T])
+        self._bootstrap(self._stash_cnt)
         # V(last obs) under the current (masked) critic state
         if self.recurrent:
             hsrc = self.h_bf if self.fused else self.h

@@ -53,6 +53,20 @@ class EpisodeMonitor:
         self.last_episodes: Dict[str, torch.Tensor] = {}
         self.total_episodes = 0
         self._t0 = None
+        self._warm()
+
+    def _warm(self):
+        """Run harvest's device ops once on a tiny record with finished
+        episodes: ROCm loads a kernel's code object at its first launch
+        (measured: ~40 ms for these, which otherwise land in the first rollout
+        whose episodes finish)."""
+        rr = torch.zeros((2, 3), dtype=torch.float64, device=self.device)
+        rl = torch.zeros((2, 3), dtype=torch.int32, device=self.device)
+        rl[1, 2] = 4
+        rr[1, 2] = 1.5
+        idx = torch.nonzero(rl > 0)
+        rec = (rr[idx[:, 0], idx[:, 1]], rl[idx[:, 0], idx[:, 1]])
+        rec[0][0:].tolist(), rec[1][0:].tolist(), idx[:, 0][0:].tolist()
 
     def begin(self):
         self._t0 = time.time()

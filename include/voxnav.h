@@ -363,6 +363,27 @@ int vn_monitor_step(const double *reward64, const float *reward, const uint8_t *
                     int32_t N, double *ep_return, int32_t *ep_length, double *rec_return, int32_t *rec_length,
                     void *stream);
 
+/*
+ * Everything the collector does after its env step t, in one launch:
+ * episode_starts[n] = terminated | truncated (may be NULL); the Monitor step
+ * (as vn_monitor_step, when ep_return is non-NULL; rec_* are the caller's
+ * row t); the truncated (not terminated) agents' terminal obs and critic
+ * state appended to the bootstrap stash (as vn_collect_compact +
+ * vn_collect_stash, rows claimed atomically from *stash_count -- the
+ * running count, read by the caller at a flush; rows past cap are dropped;
+ * row order is not agent order, which the per-row bootstrap does not see);
+ * and, for n_lstm > 0, the done agents' state rows h, c [n_lstm][N][H]
+ * (and h_bf16, may be NULL) zeroed (as vn_episode_start).
+ * Replaces sb3_contrib RecurrentPPO.collect_rollouts' per-step bookkeeping
+ * after env.step (train/Grid_Train.py:228).
+ */
+int vn_collect_post_step(const uint8_t *terminated, const uint8_t *truncated, int32_t N, int32_t t,
+                         float *episode_starts, const double *reward64, const float *reward, double *ep_return,
+                         int32_t *ep_length, double *rec_return, int32_t *rec_length, const float *terminal_obs,
+                         int32_t obs_dim, const void *h_critic, int32_t h_bytes, const float *c_critic, int32_t H,
+                         float *stash_obs, void *stash_h, float *stash_c, int32_t *stash_flat, int32_t cap,
+                         int32_t *stash_count, float *h, float *c, uint16_t *h_bf16, int32_t n_lstm, void *stream);
+
 /* ------------------------------------------------------------------------
  * PPO learner: the LSTM re-run of sb3_contrib RecurrentPPO.train
  * (RecurrentActorCriticPolicy.evaluate_actions -> _process_sequence, from

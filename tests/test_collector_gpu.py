@@ -262,6 +262,64 @@ def test_compaction_and_episode_start(voxnav):
         assert rew.cpu().numpy().tobytes() == want_r.tobytes()
 
 
+@pytest.mark.parametrize("N,hb", [(1, 4), (1000, 4), (70001, 4), (3000, 2)])
+def test_collect_post_step(voxnav, N, hb):
+    """vn_collect_post_step against its definition: episode starts, the
+    Monitor step, the truncated agents' stash rows (as a set keyed by the flat
+    reward index: rows are claimed atomically), and the zeroed state rows."""
+    import ctypes as C
+    lib = voxnav.load_library()
+    rng = np.random.default_rng(N + hb)
+    p = lambda t: C.c_void_p(t.data_ptr())  # noqa: E731
+    dev = "cuda"
+    t, od, H = 5, 80, 16
+    te = torch.from_numpy((rng.random(N) < 0.05).astype(np.uint8)).to(dev)
+    tr = torch.from_numpy((rng.random(N) < 0.1).astype(np.uint8)).to(dev)
+    tobs = torch.from_numpy(rng.standard_normal((N, od)).astype(np.float32)).to(dev)
+    hdt = torch.float32 if hb == 4 else torch.bfloat16
+    hc = torch.from_numpy(rng.standard_normal((N, H)).astype(np.float32)).to(dev).to(hdt)
+    cc = torch.from_numpy(rng.standard_normal((N, H)).astype(np.float32)).to(dev)
+    r64 = torch.from_numpy(rng.standard_normal(N)).to(dev)
+    ep_ret0 = torch.from_numpy(rng.standard_normal(N)).to(dev)
+    ep_len0 = torch.from_numpy(rng.integers(0, 100, N).astype(np.int32)).to(dev)
+    ep_ret, ep_len = ep_ret0.clone(), ep_len0.clone()
+    rec_ret = torch.full((N,), 9.0, dtype=torch.float64, device=dev)
+    rec_len = torch.full((N,), 9, dtype=torch.int32, device=dev)
+    starts = torch.full((N,), 7.0, device=dev)
+    cap = N
+    st_obs = torch.zeros((cap, od), device=dev)
+    st_h = torch.zeros((cap, H), dtype=hdt, device=dev)
+    st_c = torch.zeros((cap, H), device=dev)
+    st_flat = torch.full((cap,), -1, dtype=torch.int32, device=dev)
+    cnt = torch.full((1,), 3, dtype=torch.int32, device=dev)     # a running count carried from earlier steps
+    zh = torch.ones((2, N, H), device=dev)
+    zc = torch.ones((2, N, H), device=dev)
+    assert lib.vn_collect_post_step(p(te), p(tr), N, t, p(starts), p(r64), None, p(ep_ret), p(ep_len), p(rec_ret),
+                                    p(rec_len), p(tobs), od, p(hc), hb, p(cc), H, p(st_obs), p(st_h), p(st_c),
+                                    p(st_flat), cap, p(cnt), p(zh), p(zc), None, 2, None) == 0
+    torch.cuda.synchronize()
+    ten, trn = te.cpu().numpy().astype(bool), tr.cpu().numpy().astype(bool)
+    done = ten | trn
+    assert np.array_equal(starts.cpu().numpy(), done.astype(np.float32))
+    r = ep_ret0.cpu().numpy() + r64.cpu().numpy()
+    l = ep_len0.cpu().numpy() + 1
+    assert np.array_equal(rec_ret.cpu().numpy(), np.where(done, r, 0.0))
+    assert np.array_equal(rec_len.cpu().numpy(), np.where(done, l, 0))
+    assert np.array_equal(ep_ret.cpu().numpy(), np.where(done, 0.0, r))
+    assert np.array_equal(ep_len.cpu().numpy(), np.where(done, 0, l))
+    want = np.nonzero(trn & ~ten)[0]
+    M = int(cnt.item()) - 3
+    assert M == len(want)
+    flat = st_flat[3:3 + M].cpu().numpy()
+    assert sorted(flat.tolist()) == sorted((t * N + want).tolist())
+    agents = flat - t * N
+    assert np.array_equal(st_obs[3:3 + M].cpu().numpy(), tobs.cpu().numpy()[agents])
+    assert torch.equal(st_h[3:3 + M].cpu(), hc.cpu()[agents])
+    assert np.array_equal(st_c[3:3 + M].cpu().numpy(), cc.cpu().numpy()[agents])
+    assert float(zh[:, done].abs().sum()) == 0.0 and bool((zh[:, ~done] == 1).all())
+    assert float(zc[:, done].abs().sum()) == 0.0 and bool((zc[:, ~done] == 1).all())
+
+
 def test_fused_mfma_lstm_exact_mapping(voxnav):
     """vn_lstm_fused_bf16 against a float64 restatement on data that bf16
     holds exactly (multiples of 1/8), so the gate sums are exact in f32 and
