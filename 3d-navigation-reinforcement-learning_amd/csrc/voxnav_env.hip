@@ -144,6 +144,8 @@ struct Params {
     const int8_t *wimg;      // plane-set mode (CubicEnv, PH 8, rooms <= 64 x 64): latent-wall room images
     int pcache;
     float *scratch;          // 4 KiB: targets of inactive lanes' output stores
+    uint32_t *stood;         // plane-set mode PCM 2: per agent 32 words, stood-column rows (bit x of row y)
+    uint2 *pnz;              // ... and per agent the plane sets whose HBM copy may be nonzero (x: rows y', y: cols x')
 };
 
 __device__ __forceinline__ Agent unpack(uint4 s) {
@@ -697,6 +699,32 @@ __device__ __forceinline__ bool mark(Col<PH> &c, int z, const Rays &ry, int r, i
 // one set (written back if dirty, like a tile column), so a ray mark costs an
 // LDS word instead of an HBM row write plus one blind byte store per new cell.
 // ----------------------------------------------------------------------------
+// Stood-column map (PCM 2, rooms <= 32 x 32; VN_STOOD).  In plane-set mode
+// only the agent's own column ever reaches the byte map (visit count, z-ray
+// marks); every other column of the HBM map stays the room image the reset
+// copied, and a plane set stays all-zero in HBM until it is first written
+// back dirty.  Two small per-agent records say which is which:
+//   * S: one bit per column the agent has stood in (32 rows of u32, kept in
+//     LDS for the launch).  A column entering the window that was never stood
+//     in is read from the room image (L2-resident, one copy per room) instead
+//     of the agent's HBM map -- identical bytes, no HBM read;
+//   * xnz / ynz: one bit per x-plane set (row y') / y-plane set (column x')
+//     written back since the reset.  An entering set without its bit is zero:
+//     no load at all.
+// Early in an episode (the bench's window) ~90 % of the entering columns and
+// ~70 % of the entering sets are pristine.  The HBM contents are exactly
+// those of the unrecorded scheme (only reads are skipped), so the exported
+// belief is unchanged.
+#ifndef VN_STOOD
+#define VN_STOOD 1
+#endif
+constexpr int kStoodStride = 33;   // u32 per agent in LDS (32 rows + 1: bank spread)
+struct Stood {
+    uint32_t *row;                 // the agent's S rows in LDS (nullptr when off)
+    uint32_t xnz, ynz;             // plane sets whose HBM copy may be nonzero
+    uint32_t chg;                  // S shares (rows 8q .. 8q + 7) changed in this launch
+};
+
 // RT, the plane row word: uint32_t when every room of the set is at most
 // 32 x 32 (PCM 2), else uint64_t.  It is the row width in HBM as well as in
 // LDS, so a set is 8 x sizeof(RT) bytes in HBM (32 B for PCM 2: the four sets
@@ -743,16 +771,17 @@ __device__ __forceinline__ uint64_t pset_known(const RT *ps, int cx, int cy) {
 }
 
 // launch start: lane q loads its share of each of the 8 sets
-template <typename RT>
-__device__ __forceinline__ void pset_fill(const Params &p, int8_t *map, RT *ps, const Agent &g, const Room &R, int q) {
+template <typename RT, bool SB = false>
+__device__ __forceinline__ void pset_fill(const Params &p, int8_t *map, RT *ps, const Agent &g, const Room &R, int q,
+                                          const Stood &st) {
     PsetShare<RT> v[8];
 #pragma unroll
     for (int s = 0; s < 4; ++s) {
         const int yy = g.y - 2 + s, xx = g.x - 2 + s;
         v[s] = pset_zero<RT>();
         v[4 + s] = pset_zero<RT>();
-        if (yy >= 0 && yy < R.D) v[s] = pset_hbm<RT>(p, map, true, yy)[q];
-        if (xx >= 0 && xx < R.W) v[4 + s] = pset_hbm<RT>(p, map, false, xx)[q];
+        if (yy >= 0 && yy < R.D && (!SB || ((st.xnz >> yy) & 1u))) v[s] = pset_hbm<RT>(p, map, true, yy)[q];
+        if (xx >= 0 && xx < R.W && (!SB || ((st.ynz >> xx) & 1u))) v[4 + s] = pset_hbm<RT>(p, map, false, xx)[q];
     }
 #pragma unroll
     for (int s = 0; s < 4; ++s) {
@@ -763,16 +792,20 @@ __device__ __forceinline__ void pset_fill(const Params &p, int8_t *map, RT *ps, 
 }
 
 // launch end: the dirty sets back to HBM
-template <typename RT>
+template <typename RT, bool SB = false>
 __device__ __forceinline__ void pset_flush(const Params &p, int8_t *map, const RT *ps, const Agent &g, const Room &R,
-                                           uint32_t pdirty, int q) {
+                                           uint32_t pdirty, int q, Stood &st) {
 #pragma unroll
     for (int s = 0; s < 4; ++s) {
         const int yy = g.y - 2 + s, xx = g.x - 2 + s;
-        if (((pdirty >> (yy & 3)) & 1u) && yy >= 0 && yy < R.D)
+        if (((pdirty >> (yy & 3)) & 1u) && yy >= 0 && yy < R.D) {
             pset_hbm<RT>(p, map, true, yy)[q] = pset_get(ps, yy & 3, q);
-        if (((pdirty >> (4 + (xx & 3))) & 1u) && xx >= 0 && xx < R.W)
+            if (SB) st.xnz |= 1u << yy;
+        }
+        if (((pdirty >> (4 + (xx & 3))) & 1u) && xx >= 0 && xx < R.W) {
             pset_hbm<RT>(p, map, false, xx)[q] = pset_get(ps, 4 + (xx & 3), q);
+            if (SB) st.ynz |= 1u << xx;
+        }
     }
 }
 
@@ -786,17 +819,25 @@ struct SetLoad {
 // coordinate (y-plane set of the entering x for an x move, x-plane set of the
 // entering y for a y move) replaces the leaving one.  Load first, then the
 // write-back (vmcnt retires in issue order).
-template <typename RT>
+template <typename RT, bool SB = false>
 __device__ __forceinline__ void pset_shift_issue(const Params &p, int8_t *map, const RT *ps, int dir, int x, int y,
-                                                 const Room &R, uint32_t pdirty, int q, SetLoad<RT> &sl) {
+                                                 const Room &R, uint32_t pdirty, int q, SetLoad<RT> &sl, Stood &st) {
     const bool xm = dir < 2;
     const int e = xm ? (dir == 0 ? x + 1 : x - 2) : (dir == 2 ? y + 1 : y - 2);
     const int l = (dir == 0 || dir == 2) ? e - 4 : e + 4;
     const int lim = xm ? R.W : R.D;
     sl.slot = xm ? 4 + (e & 3) : (e & 3);
     sl.v = pset_zero<RT>();
-    if (!(VN_ABLATE & 1u) && e >= 0 && e < lim) sl.v = pset_hbm<RT>(p, map, !xm, e)[q];
-    if (((pdirty >> sl.slot) & 1u) && l >= 0 && l < lim) pset_hbm<RT>(p, map, !xm, l)[q] = pset_get(ps, sl.slot, q);
+    // SB: a set never written back since the reset is zero (no load)
+    if (!(VN_ABLATE & 1u) && e >= 0 && e < lim && (!SB || (((xm ? st.ynz : st.xnz) >> e) & 1u)))
+        sl.v = pset_hbm<RT>(p, map, !xm, e)[q];
+    if (((pdirty >> sl.slot) & 1u) && l >= 0 && l < lim) {
+        pset_hbm<RT>(p, map, !xm, l)[q] = pset_get(ps, sl.slot, q);
+        if (SB) {
+            if (xm) st.ynz |= 1u << l;
+            else st.xnz |= 1u << l;
+        }
+    }
 }
 
 template <typename RT>
@@ -871,17 +912,20 @@ struct PlaneCache {      // lane 0: x-plane row, lane 1: y-plane row
 
 // Fill the tile from HBM (launch start): lane q loads its 4 window columns.
 // PC: the plane sets (ps, already filled) add their known bits.
-template <int PH, bool PC, typename RT>
+template <int PH, bool PC, typename RT, bool SB = false>
 __device__ __forceinline__ void tile_fill(const Params &p, const int8_t *map, uint64_t *tile, const RT *ps,
-                                          const Agent &g, const Room &R, int q) {
+                                          const Agent &g, const Room &R, int q, const Stood &st) {
     const int cy = g.y + q - 2;
+    const int8_t *img = SB ? p.wimg + (size_t)g.room * p.map_bytes : map;
+    const uint32_t srow = SB && cy >= 0 && cy < R.D ? st.row[cy] : ~0u;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
         const int cx = g.x + i - 2;
         Col<PH> c;
         col_zero<PH>(c);
         if (cx >= 0 && cx < R.W && cy >= 0 && cy < R.D) {
-            col_load<PH>(map + boff<PH>(cx, cy, 0, p.nby), c);
+            // SB: a column never stood in is the room image's
+            col_load<PH>((!SB || ((srow >> cx) & 1u) ? map : img) + boff<PH>(cx, cy, 0, p.nby), c);
             if constexpr (PC) c.w[0] |= pset_known(ps, cx, cy);
         }
         tile_write<PH>(tile, tslot(cx, cy), c);
@@ -919,9 +963,10 @@ struct ShiftLoad {
     bool in;             // ... inside the room
 };
 
-template <int PH>
+template <int PH, bool SB = false>
 __device__ __forceinline__ void tile_shift_issue(const Params &p, int8_t *map, const uint64_t *tile, int dir, int x,
-                                                 int y, const Room &R, uint32_t dirty, int q, ShiftLoad<PH> &sl) {
+                                                 int y, const Room &R, uint32_t dirty, int q, ShiftLoad<PH> &sl,
+                                                 const Stood &st, int room) {
     int ex, ey, lx, ly;
     if (dir < 2) {
         ex = dir == 0 ? x + 1 : x - 2;
@@ -943,7 +988,14 @@ __device__ __forceinline__ void tile_shift_issue(const Params &p, int8_t *map, c
     // the load first: vmcnt retires in issue order, so a store issued ahead
     // of it would hold its data until the store completes
     col_zero<PH>(sl.c);
-    if (!(VN_ABLATE & 1u) && sl.in) col_load<PH>(map + boff<PH>(ex, ey, 0, p.nby), sl.c);
+    if ((VN_ABLATE & 131072u) && sl.in) {   // diagnostics: the entering column from the room image (L2)
+        col_load<PH>(p.wimg + boff<PH>(ex, ey, 0, p.nby), sl.c);
+    } else if (!(VN_ABLATE & 1u) && sl.in) {
+        // SB: a column never stood in is the room image's (L2), not an HBM read
+        const bool stood = !SB || ((st.row[ey] >> ex) & 1u);
+        col_load<PH>((stood ? (const int8_t *)map : p.wimg + (size_t)room * p.map_bytes) + boff<PH>(ex, ey, 0, p.nby),
+                     sl.c);
+    }
     if (!(VN_ABLATE & 8u) && ((dirty >> sl.s) & 1u) && lx >= 0 && lx < R.W && ly >= 0 && ly < R.D) {
         Col<PH> old;
         tile_read<PH>(tile, sl.s, old);
@@ -1323,11 +1375,11 @@ __device__ __noinline__ uint32_t reset_prepare(const EnvConst *ec, uint32_t seed
 // the new room's bricks and planes in HBM by the 4 lanes, a zero tile, then
 // sensing from the start cell.  The old episode's dirty tile is dropped.
 // ----------------------------------------------------------------------------
-template <int PH, bool PC, typename RT>
+template <int PH, bool PC, typename RT, bool SB = false>
 __device__ __forceinline__ void group_reset(const Params &p, int8_t *map, uint64_t *tile, uint32_t &dirty,
                                             PlaneCache &pc_, RT *ps, uint32_t &pdirty, bool need,
                                             uint32_t seed, Agent &g, Room &R, const float *tab, float *obs_row,
-                                            uint32_t *stage, int aslot, int q) {
+                                            uint32_t *stage, int aslot, int q, Stood &st) {
     if (need) {
         const uint32_t drawn = reset_prepare<PH, PC>(p.envc, seed, map, q);
         const int room = (int)(drawn >> 24);
@@ -1352,9 +1404,16 @@ __device__ __forceinline__ void group_reset(const Params &p, int8_t *map, uint64
             for (int k = 0; k < 8; ++k) pset_put(ps, 2 * q + (k >> 2), k & 3, pset_zero<RT>());
             pdirty = 0;
         }
+        if (SB) {                         // nothing stood in, no set written back (the planes were cleared)
+#pragma unroll
+            for (int k = 0; k < 8; ++k) st.row[8 * q + k] = 0u;
+            st.xnz = st.ynz = 0u;
+            st.chg = 0xfu;
+        }
     }
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
     if (need) {
+        if (SB && q == 0) st.row[g.y] |= 1u << g.x;   // the start column
         bool explored = false;
         const uint2 rec = p.rays[R.ray_off + (uint32_t)((g.x * R.D + g.y) * R.H + g.z)];
         sense_observe<PH, true, PC, RT>(p, map, tile, dirty, pc_, ps, pdirty, g, R, false, explored, tab,
@@ -1457,6 +1516,8 @@ __global__ __launch_bounds__(PCM ? VN_PC_BLOCK : BLOCK, PCM ? VN_PC_MIN_WAVES : 
     constexpr int kStageWords = PC ? STAGE_WORDS : STAGE_WORDS_F;
     __shared__ __attribute__((aligned(16))) uint32_t stage[(kAgents / 16) * kStageWords];
     __shared__ __attribute__((aligned(16))) RT psets[PC ? kAgents * PsetGeom<RT>::STRIDE : 2];
+    constexpr bool SB = PCM == 2 && VN_STOOD && !DEFER_K;
+    __shared__ uint32_t stood_lds[SB ? kAgents * kStoodStride : 1];
 #ifdef VN_LDS_PAD_U64            // diagnostics: occupancy at a larger LDS footprint
     __shared__ uint64_t lds_pad[VN_LDS_PAD_U64];
     if (p.N < 0) lds_pad[threadIdx.x] = 0ull;
@@ -1472,6 +1533,15 @@ __global__ __launch_bounds__(PCM ? VN_PC_BLOCK : BLOCK, PCM ? VN_PC_MIN_WAVES : 
     // the agent's state loads are in flight while the block stages its LUT
     const uint4 hot0 = p.hot[ai];
     uint32_t next_seed = p.next_seed[ai];
+    // SB: lane q's share of the stood rows (8q .. 8q + 7) and the nonzero-set masks
+    uint4 sr0 = make_uint4(0u, 0u, 0u, 0u), sr1 = sr0;
+    uint2 nz0 = make_uint2(0u, 0u);
+    if (SB && !RESET_ONLY) {
+        const uint4 *sp = reinterpret_cast<const uint4 *>(p.stood + (size_t)ai * 32u + 8u * (uint32_t)q);
+        sr0 = sp[0];
+        sr1 = sp[1];
+        nz0 = p.pnz[ai];
+    }
     for (int k = threadIdx.x; k < TAB_SIZE; k += blockDim.x) tab[k < 256 ? tab_ix((uint32_t)k) : k] = p.lut[k];
     __syncthreads();
     // a wave without agents leaves (no block-wide barrier follows)
@@ -1490,15 +1560,34 @@ __global__ __launch_bounds__(PCM ? VN_PC_BLOCK : BLOCK, PCM ? VN_PC_MIN_WAVES : 
     pc_.w[0] = pc_.w[1] = 0ull;
     RT *ps = psets + (PC ? (threadIdx.x / GROUP) * PsetGeom<RT>::STRIDE : 0);
     uint32_t pdirty = 0;
+    Stood st;
+    st.row = SB ? stood_lds + (threadIdx.x / GROUP) * kStoodStride : nullptr;
+    st.xnz = nz0.x;
+    st.ynz = nz0.y;
+    st.chg = 0u;
+    if (SB && !RESET_ONLY) {
+        uint32_t *r = st.row + 8 * q;
+        r[0] = sr0.x; r[1] = sr0.y; r[2] = sr0.z; r[3] = sr0.w;
+        r[4] = sr1.x; r[5] = sr1.y; r[6] = sr1.z; r[7] = sr1.w;
+        __builtin_amdgcn_wave_barrier();
+    }
 
     if (RESET_ONLY) {
         const bool need = active && (p.mask == nullptr || p.mask[i] != 0);
         const uint32_t seed = need ? (uint32_t)p.seeds[i] : 0u;
-        group_reset<PH, PC, RT>(p, map, tile, dirty, pc_, ps, pdirty, need, seed, g, R, tab,
-                                need ? p.obs + (size_t)i * VN_OBS_DIM : nullptr, nullptr, 0, q);
+        group_reset<PH, PC, RT, SB>(p, map, tile, dirty, pc_, ps, pdirty, need, seed, g, R, tab,
+                                    need ? p.obs + (size_t)i * VN_OBS_DIM : nullptr, nullptr, 0, q, st);
         if (need) {
             tile_flush<PH>(p, map, tile, g, R, dirty, q);
-            if (PC) pset_flush(p, map, ps, g, R, pdirty, q);
+            if (PC) pset_flush<RT, SB>(p, map, ps, g, R, pdirty, q, st);
+            if (SB) {
+                __builtin_amdgcn_wave_barrier();
+                const uint32_t *r = st.row + 8 * q;
+                uint4 *sp = reinterpret_cast<uint4 *>(p.stood + (size_t)i * 32u + 8u * (uint32_t)q);
+                sp[0] = make_uint4(r[0], r[1], r[2], r[3]);
+                sp[1] = make_uint4(r[4], r[5], r[6], r[7]);
+                if (q == 0) p.pnz[i] = make_uint2(st.xnz, st.ynz);
+            }
             if (q == 0) {
                 p.hot[i] = pack(g);
                 p.next_seed[i] = seed + p.seed_stride;
@@ -1550,8 +1639,10 @@ __global__ __launch_bounds__(PCM ? VN_PC_BLOCK : BLOCK, PCM ? VN_PC_MIN_WAVES : 
                 }
             }
         }
-        if (PC) pset_fill(p, map, ps, gf, R, q);
-        tile_fill<PH, PC, RT>(p, map, tile, ps, gf, R, q);
+        if (!(VN_ABLATE & 16384u)) {   // diagnostics: 16384 skips the launch's fill
+            if (PC) pset_fill<RT, SB>(p, map, ps, gf, R, q, st);
+            tile_fill<PH, PC, RT, SB>(p, map, tile, ps, gf, R, q, st);
+        }
     }
 #if VN_ENV_PROF
     uint64_t eprof[8] = {0, 0, 0, 0, 0, 0, 0, 0};
@@ -1666,8 +1757,8 @@ __global__ __launch_bounds__(PCM ? VN_PC_BLOCK : BLOCK, PCM ? VN_PC_MIN_WAVES : 
             // the step's loads, all in flight together: entering window
             // column (and plane set), the new cell's ray record, its plane rows
             shifted = moved && dir < 4;
-            if (shifted) tile_shift_issue<PH>(p, map, tile, dir, g.x, g.y, R, dirty, q, sl);
-            if (PC && shifted) pset_shift_issue(p, map, ps, dir, g.x, g.y, R, pdirty, q, pl);
+            if (shifted) tile_shift_issue<PH>(p, map, tile, dir, g.x, g.y, R, dirty, q, sl, st, g.room);
+            if (PC && shifted) pset_shift_issue(p, map, ps, dir, g.x, g.y, R, pdirty, q, pl, st);
             rec = p.rays[R.ray_off + (uint32_t)((g.x * R.D + g.y) * R.H + g.z)];
             if (!PC) plane_prefetch<PH>(p, map, pc_, g.x, g.y, g.z, q);
         }
@@ -1726,8 +1817,8 @@ __global__ __launch_bounds__(PCM ? VN_PC_BLOCK : BLOCK, PCM ? VN_PC_MIN_WAVES : 
         const bool need = p.autoreset && finished;
         if (__ballot(need)) {
             const uint32_t seed = next_seed;
-            group_reset<PH, PC, RT>(p, map, tile, dirty, pc_, ps, pdirty, need, seed, g, R, tab,
-                                    need ? p.obs + row * VN_OBS_DIM : nullptr, wst, aslot, q);
+            group_reset<PH, PC, RT, SB>(p, map, tile, dirty, pc_, ps, pdirty, need, seed, g, R, tab,
+                                        need ? p.obs + row * VN_OBS_DIM : nullptr, wst, aslot, q, st);
             if (need) next_seed = seed + p.seed_stride;
         }
         if (!DEFER) flush_obs();
@@ -1803,8 +1894,8 @@ __global__ __launch_bounds__(PCM ? VN_PC_BLOCK : BLOCK, PCM ? VN_PC_MIN_WAVES : 
             const bool shifted = moved && dir < 4 && !(PREMOVE && k == 0);
             ShiftLoad<PH> sl;
             SetLoad<RT> pl;
-            if (shifted) tile_shift_issue<PH>(p, map, tile, dir, g.x, g.y, R, dirty, q, sl);
-            if (PC && shifted) pset_shift_issue(p, map, ps, dir, g.x, g.y, R, pdirty, q, pl);
+            if (shifted) tile_shift_issue<PH, SB>(p, map, tile, dir, g.x, g.y, R, dirty, q, sl, st, g.room);
+            if (PC && shifted) pset_shift_issue<RT, SB>(p, map, ps, dir, g.x, g.y, R, pdirty, q, pl, st);
             uint2 rec;
             if (VN_ABLATE & 8192u) {   // diagnostics: the record computed for a walled box (exact for box rooms only)
                 const uint32_t ex = (uint32_t)(R.W - 2 - g.x) | 0x80u, wx = (uint32_t)(g.x - 1) | 0x80u;
@@ -1822,6 +1913,13 @@ __global__ __launch_bounds__(PCM ? VN_PC_BLOCK : BLOCK, PCM ? VN_PC_MIN_WAVES : 
                     if (sl.in) sl.c.w[0] |= pset_known(ps, sl.ex, sl.ey);
                 }
                 dirty = tile_shift_commit<PH>(tile, sl, dirty);
+            }
+            if (SB && moved && dir < 4 && q == 0) {       // the agent's new column: stood in
+                const uint32_t o = st.row[g.y], b = 1u << g.x;
+                if (!(o & b)) {
+                    st.row[g.y] = o | b;
+                    st.chg |= 1u << (g.y >> 3);
+                }
             }
             ENV_T(1);
 
@@ -1896,8 +1994,8 @@ __global__ __launch_bounds__(PCM ? VN_PC_BLOCK : BLOCK, PCM ? VN_PC_MIN_WAVES : 
         const bool need = p.autoreset && finished;
         if (__ballot(need)) {
             const uint32_t seed = next_seed;
-            group_reset<PH, PC, RT>(p, map, tile, dirty, pc_, ps, pdirty, need, seed, g, R, tab,
-                                    need ? p.obs + row * VN_OBS_DIM : nullptr, wst, aslot, q);
+            group_reset<PH, PC, RT, SB>(p, map, tile, dirty, pc_, ps, pdirty, need, seed, g, R, tab,
+                                        need ? p.obs + row * VN_OBS_DIM : nullptr, wst, aslot, q, st);
             if (need) next_seed = seed + p.seed_stride;
         }
         ENV_T(4);
@@ -1950,12 +2048,25 @@ __global__ __launch_bounds__(PCM ? VN_PC_BLOCK : BLOCK, PCM ? VN_PC_MIN_WAVES : 
     }
     }
     if (active) {
-        tile_flush<PH>(p, map, tile, g, R, dirty, q);
-        if (PC) pset_flush(p, map, ps, g, R, pdirty, q);
+        if (!(VN_ABLATE & 32768u)) {   // diagnostics: 32768 skips the launch's flush
+            tile_flush<PH>(p, map, tile, g, R, dirty, q);
+            if (PC) pset_flush<RT, SB>(p, map, ps, g, R, pdirty, q, st);
+        }
         if (q == 0) {
             p.hot[i] = pack(g);
             p.next_seed[i] = next_seed;
         }
+    }
+    if (SB) {
+        const uint32_t c = group_or(st.chg);
+        __builtin_amdgcn_wave_barrier();
+        if (active && ((c >> q) & 1u)) {
+            const uint32_t *r = st.row + 8 * q;
+            uint4 *sp = reinterpret_cast<uint4 *>(p.stood + (size_t)i * 32u + 8u * (uint32_t)q);
+            sp[0] = make_uint4(r[0], r[1], r[2], r[3]);
+            sp[1] = make_uint4(r[4], r[5], r[6], r[7]);
+        }
+        if (active && q == 0) p.pnz[i] = make_uint2(st.xnz, st.ynz);   // (8 B; no compare: no register held)
     }
     if ((VN_ABLATE & 4096u) && abl_sink == 12345.f) p.obs[0] = abl_sink;
 #if VN_ENV_PROF
@@ -4169,6 +4280,7 @@ struct VnEnv {
     int pcache = 0;    // CubicEnv plane-set mode (PH 8, rooms <= 64 x 64): see pset_fill
     int8_t *d_wimg = nullptr;
     float *d_scratch = nullptr;   // 4 KiB: targets of inactive lanes' output stores
+    uint32_t *d_stood = nullptr;  // PCM 2: per agent 32 stood rows, then per agent the nonzero-set masks (uint2)
 };
 
 namespace {
@@ -4243,6 +4355,8 @@ Params base_params(VnEnv *e) {
     p.wimg = e->d_wimg;
     p.pcache = e->pcache;
     p.scratch = e->d_scratch;
+    p.stood = e->d_stood;
+    p.pnz = e->d_stood ? reinterpret_cast<uint2 *>(e->d_stood + (size_t)e->N * 32u) : nullptr;
     return p;
 }
 
@@ -4415,6 +4529,7 @@ void free_env(VnEnv *e) {
     (void)hipFree(e->d_goal);
     (void)hipFree(e->d_predraw);
     (void)hipFree(e->d_wimg);
+    (void)hipFree(e->d_stood);
     (void)hipFree(e->d_scratch);
     delete e;
 }
@@ -4670,6 +4785,7 @@ int vn_create(const VnRoomSet *rooms, int32_t n_agents, const VnConfig *cfg, int
     VN_ALLOC(e->d_goal, (size_t)n_agents * sizeof(uint32_t));
     VN_ALLOC(e->d_predraw, (size_t)n_agents * sizeof(uint4));
     if (e->pcache) VN_ALLOC(e->d_wimg, (size_t)nr * e->map_bytes);
+    if (e->pcache == 2) VN_ALLOC(e->d_stood, (size_t)n_agents * 34u * sizeof(uint32_t));
     VN_ALLOC(e->d_scratch, 4096);
 #undef VN_ALLOC
     hipError_t he = hipSuccess;
@@ -4685,6 +4801,7 @@ int vn_create(const VnRoomSet *rooms, int32_t n_agents, const VnConfig *cfg, int
     if (he == hipSuccess) he = hipMemset(e->d_goal, 0, (size_t)n_agents * sizeof(uint32_t));
     if (he == hipSuccess) he = hipMemset(e->d_predraw, 0, (size_t)n_agents * sizeof(uint4));
     if (he == hipSuccess) he = hipMemset(e->d_err, 0, sizeof(int32_t));
+    if (he == hipSuccess && e->d_stood) he = hipMemset(e->d_stood, 0, (size_t)n_agents * 34u * sizeof(uint32_t));
     if (he == hipSuccess && e->pcache) {
         // per room: the bricked byte map of a fresh episode -- 0x40 (latent
         // wall, still unknown) at every wall cell, 0 elsewhere
