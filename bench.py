@@ -468,7 +468,10 @@ def roofline_block(bstep, N, F, steps, timed, kern_ms, traffic_rec, kernel_label
             "algorithmic_bytes_per_env_step": bstep, "env_steps_per_launch": N * F}
     if traffic_rec is not None:
         roof["traffic"] = traffic_rec["hbm_bytes_per_launch"]
-        roof["traffic_bytes_per_env_step"] = round(traffic_rec["hbm_bytes_per_launch"] / (N * F), 1)
+        # per env-step of the launches the record was taken over (a window
+        # shorter than F runs shorter launches than N * F env-steps)
+        roof["traffic_bytes_per_env_step"] = round(
+            traffic_rec["hbm_bytes_per_launch"] / traffic_rec.get("env_steps_per_launch", N * F), 1)
         roof["traffic_source"] = traffic_rec.get("source")
     return roof
 
