@@ -360,3 +360,52 @@ def test_launch_mix_belief_matches_oracle(voxnav, monkeypatch, pcache, src, L, N
     for a in range(N):
         W, D, H = rooms[int(st[a, 13])].shape
         np.testing.assert_array_equal(b[a, :W, :D, :H], np.minimum(orc_env.belief(a), 63), err_msg=f"agent {a}")
+
+
+@pytest.mark.parametrize("src", ["box:32x32x8", "box:16x16x8"])
+def test_masked_reset_mid_episode_matches_fresh_env(voxnav, src):
+    """vn_reset with a mask in the middle of an episode (plane-set mode with
+    the stood-column map for these rooms): the reset agents then step exactly
+    like a fresh env reset with the same seeds, and the others exactly like an
+    env that was never partly reset -- obs, f64 rewards, flags and belief maps,
+    over launches of 1 and 7 steps.  Covers the per-agent stood rows and
+    nonzero-set masks a reset must clear (envs/CubicEnv.py:77-108)."""
+    N, L = 64, 10
+    rng = np.random.default_rng(5)
+    a_pre = rng.integers(0, 6, size=(37, N)).astype(np.int32)
+    a_post = rng.integers(0, 6, size=(41, N)).astype(np.int32)
+    odd = torch.zeros(N, dtype=torch.uint8)
+    odd[1::2] = 1
+    new_seeds = 1000 + np.arange(N, dtype=np.int64) * 7
+
+    def run(env, steps):
+        out = []
+        for t in range(steps.shape[0]):
+            r = env.step(torch.as_tensor(steps[t]), reward_f64=True)
+            out.append((r.obs.cpu().numpy(), r.reward.cpu().numpy(), r.terminated.cpu().numpy(),
+                        r.truncated.cpu().numpy()))
+        return out
+
+    A = make_env(voxnav, src, L, n=N)
+    C = make_env(voxnav, src, L, n=N)
+    B = make_env(voxnav, src, L, n=N)
+    for e in (A, C):
+        e.reset(seed=42)
+        run(e, a_pre)
+        e.step_random(7, policy_seed=3, t0=0)          # a fused launch in the middle
+    A.reset(seed=new_seeds, mask=odd)
+    B.reset(seed=new_seeds)
+    ra, rb, rc = run(A, a_post), run(B, a_post), run(C, a_post)
+    o, e_ = odd.numpy().astype(bool), ~odd.numpy().astype(bool)
+    for t in range(len(ra)):
+        for k in range(4):
+            assert ra[t][k][o].tobytes() == rb[t][k][o].tobytes(), (t, k)
+            assert ra[t][k][e_].tobytes() == rc[t][k][e_].tobytes(), (t, k)
+    ba, bb, bc = (x.belief().cpu().numpy() for x in (A, B, C))
+    np.testing.assert_array_equal(ba[o], bb[o])
+    np.testing.assert_array_equal(ba[e_], bc[e_])
+    sa, sb, sc = (x.export_state().cpu().numpy() for x in (A, B, C))
+    np.testing.assert_array_equal(sa[o], sb[o])
+    np.testing.assert_array_equal(sa[e_], sc[e_])
+    for e in (A, B, C):
+        e.close()
