@@ -2038,10 +2038,18 @@ __global__ __launch_bounds__(PCM ? VN_PC_BLOCK : BLOCK, PCM ? VN_PC_MIN_WAVES : 
             const uint32_t ev = (uint32_t)(ev4 >> (16 * q)) & 0xffffu;
             const double r = reward_of_events(ev, p.crash_penalty);
             const size_t o = (size_t)(kb + q - s0) * (size_t)p.N + (size_t)i;
+            if (VN_ABLATE & 262144u) {          // diagnostics: the block's rewards computed, not stored
+                abl_sink += (float)r + (float)ev;
+            } else if (VN_ABLATE & 524288u) {   // diagnostics: the same stores into p.scratch (L2)
+                p.scratch[lane] = (float)r;
+                reinterpret_cast<uint8_t *>(p.scratch + 64)[lane] = (uint8_t)((ev >> 10) & 1u);
+                reinterpret_cast<uint8_t *>(p.scratch + 96)[lane] = (uint8_t)(ev >> 11);
+            } else {
             p.reward[o] = (float)r;
             if (p.reward64) p.reward64[o] = r;       // the Monitor's exact f64 reward (once per 4-step block)
             p.term[o] = (uint8_t)((ev >> 10) & 1u);
             p.trunc[o] = (uint8_t)(ev >> 11);
+            }
         }
         ENV_T(6);
     }
@@ -2068,7 +2076,7 @@ __global__ __launch_bounds__(PCM ? VN_PC_BLOCK : BLOCK, PCM ? VN_PC_MIN_WAVES : 
         }
         if (active && q == 0) p.pnz[i] = make_uint2(st.xnz, st.ynz);   // (8 B; no compare: no register held)
     }
-    if ((VN_ABLATE & 4096u) && abl_sink == 12345.f) p.obs[0] = abl_sink;
+    if ((VN_ABLATE & (4096u | 262144u)) && abl_sink == 12345.f) p.obs[0] = abl_sink;
 #if VN_ENV_PROF
     if (FAST && PC && (threadIdx.x & 63) == 0) {
         __builtin_amdgcn_s_waitcnt(0);   // the flush's stores issued and retired
