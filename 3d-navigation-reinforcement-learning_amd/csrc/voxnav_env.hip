@@ -1424,6 +1424,9 @@ __device__ __forceinline__ void group_reset(const Params &p, int8_t *map, uint64
 // ----------------------------------------------------------------------------
 // the step kernel: 4 lanes per agent, K fused steps, SB3 auto-reset
 // ----------------------------------------------------------------------------
+#ifndef VN_SET_PREFETCH
+#define VN_SET_PREFETCH 0   // A/B knob
+#endif
 #ifndef VN_PHILOX16
 #define VN_PHILOX16 1        // one Philox call per lane per 16 steps (striped over the quad)
 #endif
@@ -1842,6 +1845,7 @@ __global__ __launch_bounds__(PCM ? VN_PC_BLOCK : BLOCK, PCM ? VN_PC_MIN_WAVES : 
     //    evaluates step q's f64 reward and stores its reward / terminated /
     //    truncated (one store instruction per output per block).
     constexpr bool STRIPE_R = FAST && VN_REWARD_STRIPE;
+    uint32_t set_pf = 0u;                                 // VN_SET_PREFETCH's touch
     for (int k = 0; k < p.K;) {
     const uint64_t tb = p.t0 + (uint64_t)k;
     uint32_t acts = 0;                                    // 4 actions, 8 bits each, by (t & 3)
@@ -1920,6 +1924,18 @@ __global__ __launch_bounds__(PCM ? VN_PC_BLOCK : BLOCK, PCM ? VN_PC_MIN_WAVES : 
                     st.row[g.y] = o | b;
                     st.chg |= 1u << (g.y >> 3);
                 }
+            }
+            if (SB && VN_SET_PREFETCH) {
+                // lane q touches the plane set a next move in direction q
+                // (0 +x, 1 -x, 2 +y, 3 -y) would bring in, if it is nonzero in
+                // HBM, so that load finds it in L2; the previous touch is
+                // consumed first (issued a step ago)
+                vn_touch(set_pf);
+                const bool xm = q < 2;
+                const int e = q == 0 ? g.x + 2 : q == 1 ? g.x - 3 : q == 2 ? g.y + 2 : g.y - 3;
+                if (e >= 0 && e < (xm ? R.W : R.D) && ((((xm ? st.ynz : st.xnz) >> e) & 1u)))
+                    set_pf = *reinterpret_cast<const uint32_t *>(map + (xm ? p.yp_off : p.xp_off) +
+                                                                   (uint32_t)e * (8u * sizeof(RT)));
             }
             ENV_T(1);
 
