@@ -90,43 +90,6 @@ def test_simple_random_rollout_matches_oracle(voxnav, src, L, N, K):
     _rollout_vs_oracle(src, L, N, K)
 
 
-# the 4-lanes-per-agent kernel (simple_group_kernel, VOXNAV_SIMPLE_GROUP=1)
-GROUP_CASES = [("box:8x8x4", 4, 300, 200), ("set:P3_training", 10, 512, 150),
-               ("file:P3_training/kitchen2.txt", 16, 256, 200), ("set:P1_training", 7, 200, 150)]
-
-
-@pytest.mark.parametrize("src,L,N,K", GROUP_CASES, ids=[f"{c[0]}-L{c[1]}" for c in GROUP_CASES])
-def test_simple_group_kernel_matches_oracle(voxnav, monkeypatch, src, L, N, K):
-    monkeypatch.setenv("VOXNAV_SIMPLE_LINE", "0")
-    monkeypatch.setenv("VOXNAV_SIMPLE_GROUP", "1")
-    _rollout_vs_oracle(src, L, N, K)
-
-
-# the stepping + store wave kernel without the one-step pipeline
-SPLIT_CASES = [("box:8x8x4", 4, 300, 200), ("set:P3_training", 10, 512, 150)]
-
-
-@pytest.mark.parametrize("src,L,N,K", SPLIT_CASES, ids=[f"{c[0]}-L{c[1]}" for c in SPLIT_CASES])
-def test_simple_split_kernel_matches_oracle(voxnav, monkeypatch, src, L, N, K):
-    monkeypatch.setenv("VOXNAV_SIMPLE_LINE", "0")
-    monkeypatch.setenv("VOXNAV_SIMPLE_PIPE", "0")
-    _rollout_vs_oracle(src, L, N, K)
-
-
-# the one-wave bit-plane kernel; VOXNAV_SIMPLE_AW sets its agents per wave
-ONE_WAVE_CASES = [("box:8x8x4", 4, 300, 200, "32"), ("set:P2_training", 10, 1000, 150, "64"),
-                  ("file:P3_training/kitchen2.txt", 16, 200, 150, "16")]
-
-
-@pytest.mark.parametrize("src,L,N,K,aw", ONE_WAVE_CASES, ids=[f"{c[0]}-aw{c[4]}" for c in ONE_WAVE_CASES])
-def test_simple_one_wave_kernel_matches_oracle(voxnav, monkeypatch, src, L, N, K, aw):
-    monkeypatch.setenv("VOXNAV_SIMPLE_LINE", "0")
-    monkeypatch.setenv("VOXNAV_SIMPLE_GROUP", "0")
-    monkeypatch.setenv("VOXNAV_SIMPLE_SPLIT", "0")
-    monkeypatch.setenv("VOXNAV_SIMPLE_AW", aw)
-    _rollout_vs_oracle(src, L, N, K)
-
-
 # the word-layout pipelined kernel (simple_pipe_kernel: the default for rooms
 # higher than 8 or wider / deeper than 32) on rooms the line layout takes by default
 PIPE_CASES = [("box:8x8x4", 4, 300, 200), ("set:P2_training", 4, 1024, 250), ("ctor:12x10x6", 10, 256, 200)]
