@@ -742,10 +742,14 @@ __global__ __launch_bounds__(256) void collect_post_kernel(
     const uint8_t *__restrict__ term, const uint8_t *__restrict__ trunc, int N, int t, float *__restrict__ starts,
     const double *__restrict__ r64, const float *__restrict__ r32, double *__restrict__ ep_ret,
     int32_t *__restrict__ ep_len, double *__restrict__ rec_ret, int32_t *__restrict__ rec_len,
-    const float *__restrict__ tobs, int obs_dim, const uint8_t *__restrict__ h, int h_bytes,
-    const float *__restrict__ c, int H, float *__restrict__ st_obs, uint8_t *__restrict__ st_h,
+    const float *__restrict__ tobs, int obs_dim, const uint8_t *h, int h_bytes,
+    const float *c, int H, float *__restrict__ st_obs, uint8_t *__restrict__ st_h,
     float *__restrict__ st_c, int32_t *__restrict__ st_flat, int cap, int32_t *__restrict__ st_count,
-    float *__restrict__ zh, float *__restrict__ zc, uint16_t *__restrict__ zh_bf, int zB) {
+    float *zh, float *zc, uint16_t *zh_bf, int zB) {
+    // h / c (the stash's source) may be the very rows zh / zc / zh_bf zero
+    // below (the collector's non-buffer paths pass the live state arrays for
+    // both): no __restrict__ on them, so the zeroing stores stay behind the
+    // stash's loads of the same rows (same wave, program order)
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     const int lane = threadIdx.x & 63;
     const int a0 = i - lane;

@@ -172,6 +172,7 @@ int grid_for(int n_lstm, int B, int H, dim3 &grid) {
 // ----------------------------------------------------------------------------
 struct Blas {
     decltype(&rocblas_create_handle) create = nullptr;
+    decltype(&rocblas_destroy_handle) destroy = nullptr;
     decltype(&rocblas_set_stream) set_stream = nullptr;
     decltype(&rocblas_sgemm_strided_batched) sgemm_sb = nullptr;
     bool ok = false;
@@ -186,26 +187,43 @@ Blas &blas() {
         if (!h) h = dlopen("librocblas.so", RTLD_NOW | RTLD_LOCAL);
         if (!h) return;
         b.create = reinterpret_cast<decltype(&rocblas_create_handle)>(dlsym(h, "rocblas_create_handle"));
+        b.destroy = reinterpret_cast<decltype(&rocblas_destroy_handle)>(dlsym(h, "rocblas_destroy_handle"));
         b.set_stream = reinterpret_cast<decltype(&rocblas_set_stream)>(dlsym(h, "rocblas_set_stream"));
         b.sgemm_sb =
             reinterpret_cast<decltype(&rocblas_sgemm_strided_batched)>(dlsym(h, "rocblas_sgemm_strided_batched"));
-        b.ok = b.create && b.set_stream && b.sgemm_sb;
+        b.ok = b.create && b.destroy && b.set_stream && b.sgemm_sb;
     });
     return b;
 }
 
+// The calling thread's handles, one per device, destroyed when the thread
+// exits (a thread pool's short-lived workers do not leak them).
+struct ThreadHandles {
+    rocblas_handle h[64] = {};
+    ~ThreadHandles() {
+        Blas &b = blas();
+        for (int d = 0; d < 64; ++d)
+            if (h[d] && b.destroy) {
+                int cur = -1;
+                if (hipGetDevice(&cur) == hipSuccess && cur != d) (void)hipSetDevice(d);
+                (void)b.destroy(h[d]);
+                if (cur >= 0 && cur != d) (void)hipSetDevice(cur);
+            }
+    }
+};
+
 // the calling thread's handle for its current device, bound to `stream`.
 // One handle per (thread, device): a handle carries its stream, so a handle
 // shared between threads driving different streams would let one thread's
-// GEMMs run on the other's stream.  (A thread's handles live until process
-// exit; the learner runs from one thread per device.)
+// GEMMs run on the other's stream.
 int blas_handle(hipStream_t stream, rocblas_handle &out) {
     Blas &b = blas();
     if (!b.ok) return fail(VN_ERR_HIP, "rocBLAS (librocblas.so.5) could not be loaded");
     int dev = 0;
     VN_HIP(hipGetDevice(&dev));
     if (dev < 0 || dev >= 64) return fail(VN_ERR_INVALID, "device %d out of range", dev);
-    thread_local rocblas_handle handles[64] = {};
+    thread_local ThreadHandles th;
+    rocblas_handle *handles = th.h;
     if (!handles[dev] && b.create(&handles[dev]) != rocblas_status_success)
         return fail(VN_ERR_HIP, "rocblas_create_handle failed");
     if (b.set_stream(handles[dev], stream) != rocblas_status_success) return fail(VN_ERR_HIP, "rocblas_set_stream failed");

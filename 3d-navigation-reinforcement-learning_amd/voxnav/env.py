@@ -264,11 +264,14 @@ class BatchedGridEnv:
         args = (self._h, int(policy_seed), int(t0), K, _ptr(act), _ptr(obs), None if reward_f64 else _ptr(rew),
                 _ptr(rew) if reward_f64 else None, _ptr(te), _ptr(tr), None, self._stream())
         fn = self.lib.vn_step_random
+        t_end = int(t0) + K
 
         def launch():
             rc = fn(*args)
             if rc:
                 _native.check(rc, "vn_step_random")
+            self._t = t_end          # a later step_random() without t0 continues after this launch
+        launch.out = out             # args holds raw device pointers: keep the tensors alive with the callable
         return launch
 
     def kernel_label(self, k_steps: int = 16, explicit_actions: bool = False, fast: bool = True) -> str:

@@ -48,18 +48,19 @@ def shard_for(n_local: int, rank: Optional[int] = None, world: Optional[int] = N
 
 
 def allgather_rollout(buffers: Dict[str, torch.Tensor], agent_dim: int = 1, group=None,
-                      flat: bool = False) -> Dict[str, torch.Tensor]:
+                      flat: bool = True) -> Dict[str, torch.Tensor]:
     """All-gather per-shard trajectory buffers along the agent dimension.
 
     Each tensor is [T, n_local, ...] (agent dim ``agent_dim``), contiguous.
     One ``all_gather_into_tensor`` per buffer straight from the buffer into
     a [world * T, n_local, ...] output (ranks concatenated: no copy before
-    the collective), returned as a zero-copy strided view with the rank as
-    a new dimension in front of the agent dimension: [T, world, n_local,
-    ...], so ``out[:, r, i]`` is global agent ``r * n_local + i`` and the
-    view enumerates agents in global-id order (its C-order bytes are those
-    of a [T, n_global, ...] buffer).  ``flat=True`` materialises that
-    [T, n_global, ...] tensor (one copy) for callers that need it.  Large
+    the collective).  The default (``flat=True``) returns [T, n_global, ...]
+    in global-id order (one copy after the collective; with one rank the
+    buffer itself).  ``flat=False`` skips that copy and returns a zero-copy
+    strided view with the rank as a new dimension in front of the agent
+    dimension: [T, world, n_local, ...], so ``out[:, r, i]`` is global agent
+    ``r * n_local + i`` (the view's C-order bytes are those of the flat
+    buffer); the bench's timed gather uses it.  Large
     messages, back to back: the xGMI ring is per-link bound, so few big
     transfers.
     """
@@ -68,6 +69,9 @@ def allgather_rollout(buffers: Dict[str, torch.Tensor], agent_dim: int = 1, grou
     for name, t in buffers.items():
         if not t.is_contiguous():
             raise ValueError(f"{name}: allgather_rollout gathers contiguous buffers in place")
+        if world == 1 and flat:
+            out[name] = t
+            continue
         if world == 1:
             g = t.unsqueeze(0)
         else:

@@ -126,6 +126,7 @@ class VoxnavVecEnv(_VecEnvBase):
         self._tobs = z(n, od)
         self.monitor = EpisodeMonitor(self.env.lib, n, 1, dev) if monitor else None
         self._base_seed = int(seed)
+        self._reset_done = False
         self._next_seeds: Optional[np.ndarray] = None
         self._waiting = False
         self.closed = False
@@ -140,13 +141,24 @@ class VoxnavVecEnv(_VecEnvBase):
         return self._next_seeds.tolist()
 
     def reset(self) -> np.ndarray:
-        seeds = self._next_seeds if self._next_seeds is not None else self._base_seed
+        # SB3 resets its workers with seed=None after the first reset, so an
+        # env's RNG continues: here the first reset takes the base seed (or
+        # the seeds from seed()), later ones each agent's next seed of the
+        # pinned auto-reset schedule (the state's next_seed field), so no
+        # reset replays an earlier episode.  The Monitor's t_start stays at
+        # construction, as Monitor's does.
+        if self._next_seeds is not None:
+            seeds = self._next_seeds
+        elif not self._reset_done:
+            seeds = self._base_seed
+        else:
+            seeds = self.env.export_state()[:, 15].to(torch.int64)
         self.env.reset(seed=seeds, out=self._obs)
         self._next_seeds = None
+        self._reset_done = True
         if self.monitor is not None:
             self.monitor.ep_return.zero_()
             self.monitor.ep_length.zero_()
-            self.monitor.t_start = time.time()
         self.reset_infos = [{} for _ in range(self.num_envs)]
         return self._obs.cpu().numpy()
 

@@ -341,7 +341,7 @@ def allgather_leg(torch, dist, dev, rank, world, buf, reps=3):
         t0 = time.perf_counter()
         got = {}
         for k, t in bufs.items():
-            got.update(allgather_rollout({k: t}, agent_dim=dims[k]))
+            got.update(allgather_rollout({k: t}, agent_dim=dims[k], flat=False))
         sync()
         el = time.perf_counter() - t0
         tt = torch.tensor([el], dtype=torch.float64, device=dev)

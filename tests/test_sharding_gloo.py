@@ -45,8 +45,8 @@ def _worker(rank, world, port, q):
         r = env.run_random(seeds, policy_seed=3, K=K, gid_base=sh.agent_id_base, seed_stride=sh.seed_stride)
         bufs = {"obs": torch.from_numpy(r["obs"]), "reward": torch.from_numpy(r["reward"]),
                 "terminated": torch.from_numpy(r["terminated"]), "truncated": torch.from_numpy(r["truncated"])}
-        g = allgather_rollout(bufs)
-        g_flat = allgather_rollout({"r": bufs["reward"]}, flat=True)["r"]
+        g = allgather_rollout(bufs, flat=False)
+        g_flat = allgather_rollout({"r": bufs["reward"]})["r"]
         slowest = max_over_ranks(float(rank + 1))
         if rank == 0:
             full = oracle_env(SRC, L, n_agents=N_LOCAL * world).run_random(

@@ -87,4 +87,11 @@ def test_vec_env_matches_oracle_autoreset_replay():
     obs = venv.reset()
     ref = np.stack([oracle_env(src, L).reset(0, 1000 + i) for i in range(N)])
     assert obs.tobytes() == ref.tobytes()
+    # a reset without seed() continues each env's pinned seed schedule (SB3
+    # resets with seed=None): env i's next seed is 1000 + i + N, no replay
+    t_start = venv.monitor.t_start
+    obs = venv.reset()
+    ref2 = np.stack([oracle_env(src, L).reset(0, 1000 + N + i) for i in range(N)])
+    assert obs.tobytes() == ref2.tobytes()
+    assert venv.monitor.t_start == t_start          # Monitor keeps t_start from construction
     venv.close()
