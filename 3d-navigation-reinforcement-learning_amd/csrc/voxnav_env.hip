@@ -558,15 +558,91 @@ __device__ __forceinline__ void plane_prefetch(const Params &p, const int8_t *ma
     }
 }
 
+// Deferred plane marks (byte-mark mode with rows of at most 2 words, PCM 3):
+// a sensing pass records its x / y ray spans here, and the marks -- the new
+// bits of the agent's plane rows, their HBM words and the blind byte marks
+// of the newly known cells outside the window -- are applied at the start of
+// the NEXT step (before its entering column is loaded, which may hold such a
+// cell), so the plane row loaded for this step (plane_prefetch) has a whole
+// step to arrive instead of being waited for inside the sensing.  The cells
+// inside the window are marked in the tile by the sensing itself, and a
+// reset drops the pending marks of the episode it ends (the planes and the
+// map are cleared).
+struct PendMarks {
+    int valid;
+    int x, y, z;
+    uint32_t nf4;        // the step's free run lengths +x, -x, +y, -y (8 bits each)
+    int pa, pw0, rowi;   // lanes 0 / 1: the x / y row span start, its first word, the row index
+    uint64_t pm0, pm1;   // lanes 0 / 1: the span masks of words pw0, pw0 + 1
+};
+
+template <int PH>
+__device__ __forceinline__ void pend_apply(const Params &p, int8_t *map, PlaneCache &pc_, PendMarks &pend, int q) {
+    if (!pend.valid) return;
+    pend.valid = 0;
+    const int x = pend.x, y = pend.y, z = pend.z, nby = p.nby;
+    uint64_t rel = 0;                      // lanes 0/1: new bits relative to the span start pa
+    if (q < 2) {
+        // the row words: plane_prefetch of the pending step left row rowi in pc_
+        const bool xr = q == 0;
+        const int nw = xr ? p.nwx : p.nwy;
+        uint64_t *prow = reinterpret_cast<uint64_t *>(map + (xr ? p.xp_off : p.yp_off)) + (size_t)pend.rowi * nw;
+        const int pofs = pend.pw0 - pc_.w0;
+        const uint64_t pn0 = pofs == 0 ? pc_.w[0] : pc_.w[1];
+        const uint64_t pn1 = pofs == 0 ? pc_.w[1] : 0ull;
+        const uint64_t nwd0 = pend.pm0 & ~pn0, nwd1 = pend.pm1 & ~pn1;
+        if (nwd0) {
+            const uint64_t nv = pn0 | pend.pm0;
+            if (pofs == 0) pc_.w[0] = nv;
+            else pc_.w[1] = nv;
+            if (!(VN_ABLATE & 32u)) prow[pend.pw0] = nv;
+        }
+        if (nwd1) {
+            const uint64_t nv = pn1 | pend.pm1;
+            if (pofs == 0) pc_.w[1] = nv;
+            if (!(VN_ABLATE & 32u)) prow[pend.pw0 + 1] = nv;
+        }
+        const int sh = pend.pa - pend.pw0 * 64;   // 0..63
+        rel = sh == 0 ? nwd0 : (nwd0 >> sh) | (nwd1 << (64 - sh));
+        const int c = (xr ? x : y) - pend.pa;     // the agent's own bit; window cells are c-2 .. c+1
+        rel &= ~(c >= 2 ? (0xfull << (c - 2)) : ((1ull << (c + 2)) - 1ull));
+    }
+    const uint32_t rxl = group_bcast<0>((uint32_t)rel);
+    const uint32_t rxh = group_bcast<0>((uint32_t)(rel >> 32));
+    const uint32_t ryl = group_bcast<1>((uint32_t)rel);
+    const uint32_t ryh = group_bcast<1>((uint32_t)(rel >> 32));
+    const int pax = group_bcast<0>(pend.pa), pay = group_bcast<1>(pend.pa);
+    const uint64_t lane_sel = 0x1111111111111111ull << q;
+    uint64_t mx = (VN_ABLATE & 96u) ? 0ull : (((uint64_t)rxh << 32) | rxl) & lane_sel;
+    uint64_t my = (VN_ABLATE & 96u) ? 0ull : (((uint64_t)ryh << 32) | ryl) & lane_sel;
+    const int nf0 = (int)(pend.nf4 & 0xffu), nf1 = (int)((pend.nf4 >> 8) & 0xffu);
+    const int nf2 = (int)((pend.nf4 >> 16) & 0xffu), nf3 = (int)(pend.nf4 >> 24);
+    while (mx) {
+        const int pos = pax + __ffsll((unsigned long long)mx) - 1;
+        mx &= mx - 1;
+        const int d = pos - x;
+        const uint32_t v = (d == nf0 + 1 || d == -nf1 - 1) ? WALLB : KNOWN;
+        map[boff<PH>(pos, y, z, nby)] = (int8_t)v;
+    }
+    while (my) {
+        const int pos = pay + __ffsll((unsigned long long)my) - 1;
+        my &= my - 1;
+        const int d = pos - y;
+        const uint32_t v = (d == nf2 + 1 || d == -nf3 - 1) ? WALLB : KNOWN;
+        map[boff<PH>(x, pos, z, nby)] = (int8_t)v;
+    }
+}
+
 // One sensing pass (get_obs :254-312 with _sense_direction :345-397 and the
 // visit update of _mark_visited/do_action :156-166) on the agent's tile.
 // Returns the center cell's visit count after the update.
 // PC: plane-set mode (ps = the agent's LDS plane sets, pdirty their dirty bits).
-template <int PH, bool FRESH, bool PC, typename RT>
+// DM: byte-mark mode with deferred plane marks (PendMarks; PCM 3).
+template <int PH, bool FRESH, bool PC, typename RT, bool DM>
 __device__ __forceinline__ int sense_observe(const Params &p, int8_t *map, uint64_t *tile, uint32_t &dirty,
                                              PlaneCache &pc_, RT *ps, uint32_t &pdirty, Agent &g,
                                              const Room &R, bool moved, bool &explored, const float *tab, ObsDst dst,
-                                             uint2 rec, int q, bool lut_stale = true) {
+                                             uint2 rec, int q, PendMarks &pend, bool lut_stale = true) {
     const int x = g.x, y = g.y, z = g.z, nby = p.nby, L = p.L;
 
     // ---- x / y marked-bit plane rows (lane 0: x row (y,z), lane 1: y row (x,z)) ----
@@ -720,6 +796,19 @@ __device__ __forceinline__ int sense_observe(const Params &p, int8_t *map, uint6
             }
         }
         pdirty |= group_or(pd);
+    } else if constexpr (DM) {
+        // the marks are applied at the start of the next step (pend_apply)
+        pend.valid = 1;
+        pend.x = x;
+        pend.y = y;
+        pend.z = z;
+        pend.nf4 = (uint32_t)ry.nf[0] | ((uint32_t)ry.nf[1] << 8) | ((uint32_t)ry.nf[2] << 16) |
+                   ((uint32_t)ry.nf[3] << 24);
+        pend.pa = pa;
+        pend.pw0 = pw0;
+        pend.rowi = rowi;
+        pend.pm0 = pm[0];
+        pend.pm1 = pm[1];
     } else {
 
     // new marks: row bits set now for the first time.  Those inside the window
@@ -882,12 +971,13 @@ __device__ __noinline__ uint32_t reset_prepare(const EnvConst *ec, uint32_t seed
 // the new room's bricks and planes in HBM by the 4 lanes, a zero tile, then
 // sensing from the start cell.  The old episode's dirty tile is dropped.
 // ----------------------------------------------------------------------------
-template <int PH, bool PC, typename RT, bool SB = false>
+template <int PH, bool PC, typename RT, bool SB, bool DM>
 __device__ __forceinline__ void group_reset(const Params &p, int8_t *map, uint64_t *tile, uint32_t &dirty,
                                             PlaneCache &pc_, RT *ps, uint32_t &pdirty, bool need,
                                             uint32_t seed, Agent &g, Room &R, const float *tab, float *obs_row,
-                                            uint32_t *stage, int aslot, int q, Stood &st) {
+                                            uint32_t *stage, int aslot, int q, Stood &st, PendMarks &pend) {
     if (need) {
+        pend.valid = 0;          // the ended episode's deferred marks: its map and planes are cleared
         const uint32_t drawn = reset_prepare<PH, PC>(p.envc, seed, map, q);
         const int room = (int)(drawn >> 24);
         R = load_room(p, room);
@@ -923,17 +1013,14 @@ __device__ __forceinline__ void group_reset(const Params &p, int8_t *map, uint64
         if (SB && q == 0) st.row[g.y] |= 1u << g.x;   // the start column
         bool explored = false;
         const uint2 rec = p.rays[R.ray_off + (uint32_t)((g.x * R.D + g.y) * R.H + g.z)];
-        sense_observe<PH, true, PC, RT>(p, map, tile, dirty, pc_, ps, pdirty, g, R, false, explored, tab,
-                                        ObsDst{obs_row, nullptr, stage, false, false, aslot}, rec, q);
+        sense_observe<PH, true, PC, RT, DM>(p, map, tile, dirty, pc_, ps, pdirty, g, R, false, explored, tab,
+                                            ObsDst{obs_row, nullptr, stage, false, false, aslot}, rec, q, pend);
     }
 }
 
 // ----------------------------------------------------------------------------
 // the step kernel: 4 lanes per agent, K fused steps, SB3 auto-reset
 // ----------------------------------------------------------------------------
-#ifndef VN_SET_PREFETCH
-#define VN_SET_PREFETCH 0   // A/B knob
-#endif
 #ifndef VN_PHILOX16
 #define VN_PHILOX16 1        // one Philox call per lane per 16 steps (striped over the quad)
 #endif
@@ -999,12 +1086,6 @@ __device__ unsigned long long g_env_prof[16];
 #ifndef VN_PC_MIN_WAVES
 #define VN_PC_MIN_WAVES 4   // waves per SIMD the VGPR budget is set for
 #endif
-#ifndef VN_DEFER_PC
-#define VN_DEFER_PC 0     // deferred stores: measured slower
-#endif
-#ifndef VN_DEFER_ALL
-#define VN_DEFER_ALL 0      // byte-mark kernels: deferring spills them (VGPRs) -- measured slower
-#endif
 // rows fwd, right, back, left; cols facing N,E,S,W; dirs 0 +x, 1 -x, 2 +y, 3 -y
 constexpr uint32_t kMoveDir = (2u << 0) | (0u << 2) | (3u << 4) | (1u << 6)       // fwd
                               | (0u << 8) | (3u << 10) | (1u << 12) | (2u << 14)   // right
@@ -1014,9 +1095,10 @@ template <int PH, bool EXT, bool FAST, bool RESET_ONLY, int PCM>
 #ifndef VN_MIN_WAVES_PER_SIMD
 #define VN_MIN_WAVES_PER_SIMD 4   // <= 128 VGPRs: the 16 waves of 256 agents per CU resident at once
 #endif
-__global__ __launch_bounds__(PCM ? VN_PC_BLOCK : BLOCK, PCM ? VN_PC_MIN_WAVES : VN_MIN_WAVES_PER_SIMD) void env_kernel(Params p) {
-    constexpr bool PC = PCM != 0;
-    constexpr bool DEFER_K = (PC && VN_DEFER_PC) || VN_DEFER_ALL;
+__global__ __launch_bounds__((PCM == 1 || PCM == 2) ? VN_PC_BLOCK : BLOCK,
+                             (PCM == 1 || PCM == 2) ? VN_PC_MIN_WAVES : VN_MIN_WAVES_PER_SIMD) void env_kernel(Params p) {
+    constexpr bool PC = PCM == 1 || PCM == 2;   // plane-set mode
+    constexpr bool DM = PCM == 3;                // byte-mark mode, deferred plane marks
     using RT = typename std::conditional<PCM == 2, uint32_t, uint64_t>::type;
     constexpr int kAgents = (PC ? VN_PC_BLOCK : BLOCK) / GROUP;
     static_assert(!PC || kAgents <= 64, "tc_slot has 64 obs[72] codes per block");
@@ -1026,7 +1108,7 @@ __global__ __launch_bounds__(PCM ? VN_PC_BLOCK : BLOCK, PCM ? VN_PC_MIN_WAVES : 
     constexpr int kStageWords = PC ? STAGE_WORDS : STAGE_WORDS_F;
     __shared__ __attribute__((aligned(16))) uint32_t stage[(kAgents / 16) * kStageWords];
     __shared__ __attribute__((aligned(16))) RT psets[PC ? kAgents * PsetGeom<RT>::STRIDE : 2];
-    constexpr bool SB = PCM == 2 && VN_STOOD && !DEFER_K;
+    constexpr bool SB = PCM == 2 && VN_STOOD;
     __shared__ uint32_t stood_lds[SB ? kAgents * kStoodStride : 1];
 #ifdef VN_LDS_PAD_U64            // diagnostics: occupancy at a larger LDS footprint
     __shared__ uint64_t lds_pad[VN_LDS_PAD_U64];
@@ -1068,6 +1150,8 @@ __global__ __launch_bounds__(PCM ? VN_PC_BLOCK : BLOCK, PCM ? VN_PC_MIN_WAVES : 
     pc_.row = -1;
     pc_.w0 = 0;
     pc_.w[0] = pc_.w[1] = 0ull;
+    PendMarks pend;                        // DM: the previous sensing pass's plane marks, not yet applied
+    pend.valid = 0;
     RT *ps = psets + (PC ? (threadIdx.x / GROUP) * PsetGeom<RT>::STRIDE : 0);
     uint32_t pdirty = 0;
     Stood st;
@@ -1085,9 +1169,10 @@ __global__ __launch_bounds__(PCM ? VN_PC_BLOCK : BLOCK, PCM ? VN_PC_MIN_WAVES : 
     if (RESET_ONLY) {
         const bool need = active && (p.mask == nullptr || p.mask[i] != 0);
         const uint32_t seed = need ? (uint32_t)p.seeds[i] : 0u;
-        group_reset<PH, PC, RT, SB>(p, map, tile, dirty, pc_, ps, pdirty, need, seed, g, R, tab,
-                                    need ? p.obs + (size_t)i * VN_OBS_DIM : nullptr, nullptr, 0, q, st);
+        group_reset<PH, PC, RT, SB, DM>(p, map, tile, dirty, pc_, ps, pdirty, need, seed, g, R, tab,
+                                        need ? p.obs + (size_t)i * VN_OBS_DIM : nullptr, nullptr, 0, q, st, pend);
         if (need) {
+            if constexpr (DM) pend_apply<PH>(p, map, pc_, pend, q);
             tile_flush<PH>(p, map, tile, g, R, dirty, q);
             if (PC) pset_flush<RT, SB>(p, map, ps, g, R, pdirty, q, st);
             if (SB) {
@@ -1115,7 +1200,7 @@ __global__ __launch_bounds__(PCM ? VN_PC_BLOCK : BLOCK, PCM ? VN_PC_MIN_WAVES : 
 #ifndef VN_PREMOVE
 #define VN_PREMOVE 1
 #endif
-    constexpr bool PREMOVE = VN_PREMOVE && !DEFER_K;
+    constexpr bool PREMOVE = VN_PREMOVE;
     uint32_t a16[4] = {0u, 0u, 0u, 0u};          // VN_PHILOX16: the actions of the current 16-step chunk
     auto philox_chunk = [&](uint64_t tb) {
         const uint4 o = philox4x32_10(p.policy_seed, p.gid_base + (uint64_t)ai, ((tb >> 2) & ~3ull) + (uint64_t)q);
@@ -1126,7 +1211,8 @@ __global__ __launch_bounds__(PCM ? VN_PC_BLOCK : BLOCK, PCM ? VN_PC_MIN_WAVES : 
         a16[2] = group_bcast<2>(mine);
         a16[3] = group_bcast<3>(mine);
     };
-    if (!EXT && VN_PHILOX16 && !DEFER_K) philox_chunk(p.t0);
+    if (!EXT && VN_PHILOX16) philox_chunk(p.t0);
+    uint2 rec0 = make_uint2(0u, 0u);                // PREMOVE: step 0's ray record, loaded with the fill
     if (active) {
         Agent gf = g;                               // the fill's window center
         if (PREMOVE && p.K > 0) {
@@ -1141,12 +1227,18 @@ __global__ __launch_bounds__(PCM ? VN_PC_BLOCK : BLOCK, PCM ? VN_PC_MIN_WAVES : 
                 const uint32_t t3 = (uint32_t)p.t0 & 3u;
                 a = (int)__umulhi(t3 == 0u ? o.x : t3 == 1u ? o.y : t3 == 2u ? o.z : o.w, 6u);
             }
-            if (a < 4) {
-                const int dir = (int)((kMoveDir >> (2 * (a * 4 + g.facing))) & 3u);
-                if ((g.move_mask >> dir) & 1u) {
-                    gf.x += (dir == 0) - (dir == 1);
-                    gf.y += (dir == 2) - (dir == 3);
-                }
+            const int dir = a < 4 ? (int)((kMoveDir >> (2 * (a * 4 + g.facing))) & 3u) : (a == 4) ? 4 : 5;
+            if ((g.move_mask >> dir) & 1u) {
+                gf.x += (dir == 0) - (dir == 1);
+                gf.y += (dir == 2) - (dir == 3);
+                gf.z += (dir == 4) - (dir == 5);
+            }
+            // step 0's ray record depends on the state alone: issued ahead of
+            // the fill, so a one-step launch waits for one load round trip
+            // after the state instead of two
+            if (!(VN_ABLATE & 8192u)) {
+                rec0 = p.rays[R.ray_off + (uint32_t)((gf.x * R.D + gf.y) * R.H + gf.z)];
+                __builtin_amdgcn_sched_barrier(0);
             }
         }
         if (!(VN_ABLATE & 16384u)) {   // diagnostics: 16384 skips the launch's fill
@@ -1166,179 +1258,9 @@ __global__ __launch_bounds__(PCM ? VN_PC_BLOCK : BLOCK, PCM ? VN_PC_MIN_WAVES : 
     const int aslot = (threadIdx.x & 63) >> 2;
     float abl_sink = 0.f;                             // VN_ABLATE 4096 (diagnostics)
 
-    // Outputs of step k (the staged obs rows, reward, flags) are stored after
-    // step k+1's loads are issued (DEFER): vmcnt retires in issue order, so
-    // stores ahead of a step's loads would hold the loads' data until they
-    // complete.  The store sequence is branch-free -- the first call stores
-    // placeholders into step 0's rows (rewritten by the real store later),
-    // lanes past the wave's last agent repeat its last float4 or store to
-    // p.scratch, all 4 lanes of an agent store its reward -- so the
-    // compiler's vmcnt waits stay exact.
-    constexpr bool DEFER = DEFER_K;
     const int lane = threadIdx.x & 63;
     const int nvalid = (p.N - wave_agent0) * (VN_OBS_DIM / 4);       // float4s of the wave's agents (> 0)
-    int pk = -1;                                                      // the step whose outputs are pending
-    float pr = 0.f;
-    double pr64 = 0.0;
-    uint8_t pte = 0, ptr8 = 0;
-    auto flush_obs = [&]() {
-        const size_t kk = (size_t)(pk < 0 ? 0 : pk);
-        if (VN_STAGE_OBS && !(VN_ABLATE & 16u)) {
-            float4 *dst4 = reinterpret_cast<float4 *>(p.obs + (kk * p.N + wave_agent0) * VN_OBS_DIM);
-            if constexpr (PC) {
-#pragma unroll 1
-                for (int jj = 0; jj < (64 / GROUP) * (VN_OBS_DIM / 4) / 64; ++jj) {
-                    const int f = lane + 64 * jj < nvalid ? lane + 64 * jj : nvalid - 1;
-                    obs_store(dst4 + f, code_float4(wst[f], tab));
-                }
-            } else {
-                const float4 *ws4 = reinterpret_cast<const float4 *>(wst);
-#pragma unroll
-                for (int jj = 0; jj < (64 / GROUP) * (VN_OBS_DIM / 4) / 64; ++jj) {
-                    const int f = lane + 64 * jj < nvalid ? lane + 64 * jj : nvalid - 1;
-                    obs_store(dst4 + f, ws4[f]);
-                }
-            }
-        }
-    };
-    auto store_rewards = [&]() {
-        const size_t kk = (size_t)(pk < 0 ? 0 : pk);
-        if (!(VN_ABLATE & 128u)) {
-            const size_t o = kk * (size_t)p.N + (size_t)ai;
-            if (FAST || p.reward) *(active ? p.reward + o : p.scratch + lane) = pr;
-            if (p.reward64) *(active ? p.reward64 + o : reinterpret_cast<double *>(p.scratch + 128) + lane) = pr64;
-            if (FAST || p.term) *(active ? p.term + o : reinterpret_cast<uint8_t *>(p.scratch + 64) + lane) = pte;
-            if (FAST || p.trunc) *(active ? p.trunc + o : reinterpret_cast<uint8_t *>(p.scratch + 96) + lane) = ptr8;
-        }
-    };
-
-    if constexpr (DEFER) {
-    // outer loop: one Philox call per agent per 4-step block of the global
-    // step counter; inner loop: the steps of that block
-    for (int k = 0; k < p.K;) {
-    const uint64_t tb = p.t0 + (uint64_t)k;
-    uint32_t acts = 0;                                    // 4 actions, 8 bits each, by (t & 3)
-    if (!EXT) {
-        const uint4 o = philox4x32_10(p.policy_seed, p.gid_base + (uint64_t)ai, tb >> 2);
-        acts = __umulhi(o.x, 6u) | (__umulhi(o.y, 6u) << 8) | (__umulhi(o.z, 6u) << 16) | (__umulhi(o.w, 6u) << 24);
-    }
-    const int jn = (4 - (int)(tb & 3u)) < (p.K - k) ? (4 - (int)(tb & 3u)) : (p.K - k);
-    for (int j = 0; j < jn; ++j, ++k) {
-        bool finished = false;
-        const size_t row = (size_t)k * (size_t)p.N + (size_t)i;
-        const uint64_t tt = tb + (uint64_t)j;
-        if (!DEFER) {        // no pending outputs cross the step
-            pr = 0.f;
-            pr64 = 0.0;
-            pte = ptr8 = 0;
-        }
-        int a = 0;
-        bool moved = false, shifted = false, truncated = false;
-        ShiftLoad<PH> sl;
-        SetLoad<RT> pl;
-        uint2 rec = make_uint2(0u, 0u);
-        if (active) {
-            a = EXT ? p.actions[row] : (int)((acts >> (8 * (uint32_t)(tt & 3u))) & 0xffu);
-            if (!FAST && p.actions_out && q == 0) p.actions_out[row] = a;
-
-            // step() prologue (:111-116)
-            if (g.near_wall) {
-                g.was_near_wall = true;
-                g.near_wall = false;
-            }
-            if (g.step_count < 0xffffffu) ++g.step_count;
-            truncated = g.step_count >= R.total_free;
-
-            // do_action (:134-166): relative move table by facing -> axis dir
-            int dir;
-            if (a < 4) {
-                // rows fwd, right, back, left; cols facing N,E,S,W; dirs 0 +x, 1 -x, 2 +y, 3 -y
-                dir = (int)((kMoveDir >> (2 * (a * 4 + g.facing))) & 3u);
-                g.facing = (int)((0x8Du >> (2 * dir)) & 3u);  // +x->E(1) -x->W(3) +y->N(0) -y->S(2)
-            } else {
-                dir = (a == 4) ? 4 : 5;
-            }
-            moved = (g.move_mask >> dir) & 1u;
-            if (moved) {
-                g.x += (dir == 0) - (dir == 1);
-                g.y += (dir == 2) - (dir == 3);
-                g.z += (dir == 4) - (dir == 5);
-            }
-            // the step's loads, all in flight together: entering window
-            // column (and plane set), the new cell's ray record, its plane rows
-            shifted = moved && dir < 4;
-            if (shifted) tile_shift_issue<PH>(p, map, tile, dir, g.x, g.y, R, dirty, q, sl, st, g.room);
-            if (PC && shifted) pset_shift_issue(p, map, ps, dir, g.x, g.y, R, pdirty, q, pl, st);
-            rec = p.rays[R.ray_off + (uint32_t)((g.x * R.D + g.y) * R.H + g.z)];
-            if (!PC) plane_prefetch<PH>(p, map, pc_, g.x, g.y, g.z, q);
-        }
-        if (DEFER) {                                      // step k-1's outputs, behind step k's loads
-            flush_obs();
-            store_rewards();
-        }
-        if (active) {
-            if (shifted) {
-                if constexpr (PC) {
-                    pdirty = pset_shift_commit(ps, pl, pdirty, q);
-                    if (sl.in) sl.c.w[0] |= pset_known(ps, sl.ex, sl.ey);
-                }
-                dirty = tile_shift_commit<PH>(tile, sl, dirty);
-            }
-
-            bool explored = false;
-            const ObsDst dst{p.obs + row * VN_OBS_DIM,
-                             p.terminal_obs ? p.terminal_obs + row * VN_OBS_DIM : nullptr, wst,
-                             p.autoreset != 0, truncated, aslot};
-            const int vv = sense_observe<PH, false, PC, RT>(p, map, tile, dirty, pc_, ps, pdirty, g, R, moved,
-                                                            explored, tab, dst, rec, q, k == 0);
-
-            // compute_reward (:169-224), f64 in the reference's order
-            double r = -0.05;
-            const double pen = (double)vv * 0.02;
-            r -= (0.5 < pen) ? 0.5 : pen;
-            if (!moved) {
-                g.last_bump = true;
-                if (g.bumps < 0x3ffffffu) ++g.bumps;
-                r += p.crash_penalty;
-            } else {
-                g.last_bump = false;
-                if (g.was_near_wall) {
-                    g.was_near_wall = false;
-                    r += 0.15;
-                }
-                if (g.last_action != 2 && a == g.last_action && g.last_action < 4) r += 0.05;
-                if (g.last_action == 2 && a == 2) r -= 0.5;
-            }
-            if (explored) r += 1.0;
-            if (g.visited >= R.finish_visits) {            // visited / total >= 0.84 (:212-215)
-                g.done = true;
-                r += 100.0;
-            }
-            if (truncated) r += -5.0;
-            g.last_action = a;
-            pr = (float)r;
-            pr64 = r;
-            pte = g.done ? 1 : 0;
-            ptr8 = truncated ? 1 : 0;
-            finished = g.done || truncated;
-        }
-        pk = k;
-        if (!DEFER) store_rewards();                      // nothing carried across the reset
-        const bool need = p.autoreset && finished;
-        if (__ballot(need)) {
-            const uint32_t seed = next_seed;
-            group_reset<PH, PC, RT, SB>(p, map, tile, dirty, pc_, ps, pdirty, need, seed, g, R, tab,
-                                        need ? p.obs + row * VN_OBS_DIM : nullptr, wst, aslot, q, st);
-            if (need) next_seed = seed + p.seed_stride;
-        }
-        if (!DEFER) flush_obs();
-    }
-    }
-    if (DEFER) {
-        flush_obs();
-        store_rewards();
-    }
-    } else {
+    {
     // the step's outputs stored within the step (measured faster than the
     // deferred order, which also needs more VGPRs than the byte-mark kernels
     // have at 4 waves/SIMD)
@@ -1352,7 +1274,6 @@ __global__ __launch_bounds__(PCM ? VN_PC_BLOCK : BLOCK, PCM ? VN_PC_MIN_WAVES : 
     //    evaluates step q's f64 reward and stores its reward / terminated /
     //    truncated (one store instruction per output per block).
     constexpr bool STRIPE_R = FAST && VN_REWARD_STRIPE;
-    uint32_t set_pf = 0u;                                 // VN_SET_PREFETCH's touch
     for (int k = 0; k < p.K;) {
     const uint64_t tb = p.t0 + (uint64_t)k;
     uint32_t acts = 0;                                    // 4 actions, 8 bits each, by (t & 3)
@@ -1374,6 +1295,8 @@ __global__ __launch_bounds__(PCM ? VN_PC_BLOCK : BLOCK, PCM ? VN_PC_MIN_WAVES : 
         const size_t row = (size_t)k * (size_t)p.N + (size_t)i;
         const uint64_t tt = tb + (uint64_t)j;
         if (active) {
+            // DM: the previous step's plane marks, before this step's tile shift reads the entering column
+            if constexpr (DM) pend_apply<PH>(p, map, pc_, pend, q);
             const int a = EXT ? p.actions[row] : (int)((acts >> (8 * (uint32_t)(tt & 3u))) & 0xffu);
             if (!FAST && p.actions_out && q == 0) p.actions_out[row] = a;
 
@@ -1413,6 +1336,8 @@ __global__ __launch_bounds__(PCM ? VN_PC_BLOCK : BLOCK, PCM ? VN_PC_MIN_WAVES : 
                 const uint32_t ey = (uint32_t)(R.D - 2 - g.y) | 0x80u, wy = (uint32_t)(g.y - 1) | 0x80u;
                 const uint32_t ez = (uint32_t)(R.H - 2 - g.z) | 0x80u, wz = (uint32_t)(g.z - 1) | 0x80u;
                 rec = make_uint2(ex | (wx << 8) | (ey << 16) | (wy << 24), ez | (wz << 8));
+            } else if (PREMOVE && k == 0) {
+                rec = rec0;
             } else {
                 rec = p.rays[R.ray_off + (uint32_t)((g.x * R.D + g.y) * R.H + g.z)];
             }
@@ -1432,26 +1357,14 @@ __global__ __launch_bounds__(PCM ? VN_PC_BLOCK : BLOCK, PCM ? VN_PC_MIN_WAVES : 
                     st.chg |= 1u << (g.y >> 3);
                 }
             }
-            if (SB && VN_SET_PREFETCH) {
-                // lane q touches the plane set a next move in direction q
-                // (0 +x, 1 -x, 2 +y, 3 -y) would bring in, if it is nonzero in
-                // HBM, so that load finds it in L2; the previous touch is
-                // consumed first (issued a step ago)
-                vn_touch(set_pf);
-                const bool xm = q < 2;
-                const int e = q == 0 ? g.x + 2 : q == 1 ? g.x - 3 : q == 2 ? g.y + 2 : g.y - 3;
-                if (e >= 0 && e < (xm ? R.W : R.D) && ((((xm ? st.ynz : st.xnz) >> e) & 1u)))
-                    set_pf = *reinterpret_cast<const uint32_t *>(map + (xm ? p.yp_off : p.xp_off) +
-                                                                   (uint32_t)e * (8u * sizeof(RT)));
-            }
             ENV_T(1);
 
             bool explored = false;
             const ObsDst dst{p.obs + row * VN_OBS_DIM,
                              p.terminal_obs ? p.terminal_obs + row * VN_OBS_DIM : nullptr, wst,
                              p.autoreset != 0, truncated, aslot};
-            const int vv = sense_observe<PH, false, PC, RT>(p, map, tile, dirty, pc_, ps, pdirty, g, R, moved,
-                                                            explored, tab, dst, rec, q, k == 0);
+            const int vv = sense_observe<PH, false, PC, RT, DM>(p, map, tile, dirty, pc_, ps, pdirty, g, R,
+                                                                moved, explored, tab, dst, rec, q, pend, k == 0);
             ENV_T(2);
 
             if constexpr (STRIPE_R) {
@@ -1517,8 +1430,8 @@ __global__ __launch_bounds__(PCM ? VN_PC_BLOCK : BLOCK, PCM ? VN_PC_MIN_WAVES : 
         const bool need = p.autoreset && finished;
         if (__ballot(need)) {
             const uint32_t seed = next_seed;
-            group_reset<PH, PC, RT, SB>(p, map, tile, dirty, pc_, ps, pdirty, need, seed, g, R, tab,
-                                        need ? p.obs + row * VN_OBS_DIM : nullptr, wst, aslot, q, st);
+            group_reset<PH, PC, RT, SB, DM>(p, map, tile, dirty, pc_, ps, pdirty, need, seed, g, R, tab,
+                                            need ? p.obs + row * VN_OBS_DIM : nullptr, wst, aslot, q, st, pend);
             if (need) next_seed = seed + p.seed_stride;
         }
         ENV_T(4);
@@ -1579,6 +1492,7 @@ __global__ __launch_bounds__(PCM ? VN_PC_BLOCK : BLOCK, PCM ? VN_PC_MIN_WAVES : 
     }
     }
     if (active) {
+        if constexpr (DM) pend_apply<PH>(p, map, pc_, pend, q);   // the last step's deferred marks
         if (!(VN_ABLATE & 32768u)) {   // diagnostics: 32768 skips the launch's flush
             tile_flush<PH>(p, map, tile, g, R, dirty, q);
             if (PC) pset_flush<RT, SB>(p, map, ps, g, R, pdirty, q, st);
@@ -1601,7 +1515,7 @@ __global__ __launch_bounds__(PCM ? VN_PC_BLOCK : BLOCK, PCM ? VN_PC_MIN_WAVES : 
     }
     if ((VN_ABLATE & (4096u | 262144u)) && abl_sink == 12345.f) p.obs[0] = abl_sink;
 #if VN_ENV_PROF
-    if (FAST && PC && (threadIdx.x & 63) == 0) {
+    if (FAST && (threadIdx.x & 63) == 0) {
         __builtin_amdgcn_s_waitcnt(0);   // the flush's stores issued and retired
         const uint64_t tend = __builtin_amdgcn_s_memtime();
         for (int k = 0; k < 7; ++k) atomicAdd(&g_env_prof[k], (unsigned long long)eprof[k]);
@@ -1726,6 +1640,7 @@ struct VnEnv {
     int sbits = 0;     // simpleEnv bit-plane layouts (rooms <= 64 x 64 x 31), else the dense map
     uint32_t sy_off = 0, sz_off = 0, qz_off = 0;
     int sline = 0;     // simpleEnv line layout (simple_line_kernel), rooms <= 32 x 32 x 8
+    int defer = 0;     // CubicEnv byte-mark mode with deferred plane marks (PCM 3; rows <= 2 words)
     int pcache = 0;    // CubicEnv plane-set mode (PH 8, rooms <= 64 x 64): see pset_fill
     int8_t *d_wimg = nullptr;
     float *d_scratch = nullptr;   // 4 KiB: targets of inactive lanes' output stores
@@ -1797,7 +1712,7 @@ Params base_params(VnEnv *e) {
 
 template <int PH, bool RESET_ONLY, int PCM>
 int launch_ph(int N, hipStream_t s, const Params &p) {
-    const int bs = PCM ? VN_PC_BLOCK : BLOCK;
+    const int bs = (PCM == 1 || PCM == 2) ? VN_PC_BLOCK : BLOCK;
     const dim3 block((unsigned)bs);
     const dim3 grid((unsigned)(((size_t)N * GROUP + bs - 1) / bs));
     // FAST: the rollout-buffer call (f32 reward, flags; the f64 reward for the
@@ -1817,15 +1732,28 @@ int launch_ph(int N, hipStream_t s, const Params &p) {
     return VN_OK;
 }
 
+// The kernel mode of a CubicEnv: PCM 1/2 plane sets (PH 8, VnEnv::pcache),
+// PCM 3 byte marks with deferred plane marks (rows of <= 2 words, VnEnv::defer),
+// else PCM 0.
+static int env_pcm(const VnEnv *e) {
+    if (e->ph == 8 && e->pcache) return e->pcache;
+    return e->defer ? 3 : 0;
+}
+
 template <bool RESET_ONLY>
 int launch_env(VnEnv *e, const Params &p, hipStream_t s) {
     if (e->variant == VN_VARIANT_SIMPLE)
         return vn_simple::launch(RESET_ONLY, e->sline, e->sbits, e->cfg.local_map_length, e->N, e->obs_dim, &p, s);
-    if (e->ph == 8 && e->pcache == 2) return launch_ph<8, RESET_ONLY, 2>(e->N, s, p);
-    if (e->ph == 8 && e->pcache == 1) return launch_ph<8, RESET_ONLY, 1>(e->N, s, p);
-    if (e->ph == 8) return launch_ph<8, RESET_ONLY, 0>(e->N, s, p);
-    if (e->ph == 16) return launch_ph<16, RESET_ONLY, 0>(e->N, s, p);
-    return launch_ph<32, RESET_ONLY, 0>(e->N, s, p);
+    const int pcm = env_pcm(e);
+    if (e->ph == 8) {
+        if (pcm == 2) return launch_ph<8, RESET_ONLY, 2>(e->N, s, p);
+        if (pcm == 1) return launch_ph<8, RESET_ONLY, 1>(e->N, s, p);
+        if (pcm == 3) return launch_ph<8, RESET_ONLY, 3>(e->N, s, p);
+        return launch_ph<8, RESET_ONLY, 0>(e->N, s, p);
+    }
+    if (e->ph == 16)
+        return pcm == 3 ? launch_ph<16, RESET_ONLY, 3>(e->N, s, p) : launch_ph<16, RESET_ONLY, 0>(e->N, s, p);
+    return pcm == 3 ? launch_ph<32, RESET_ONLY, 3>(e->N, s, p) : launch_ph<32, RESET_ONLY, 0>(e->N, s, p);
 }
 
 // The kernel instantiation launch_env picks for a call shape (diagnostics /
@@ -1835,7 +1763,7 @@ std::string kernel_label(const VnEnv *e, bool reset_only, bool ext, bool fast, i
     if (e->variant == VN_VARIANT_SIMPLE)
         return vn_simple::label(reset_only, ext, e->sline, e->sbits, e->cfg.local_map_length);
     (void)k_steps;
-    const int pcm = e->ph == 8 ? e->pcache : 0;
+    const int pcm = env_pcm(e);
     const bool x = !reset_only && ext, f = !reset_only && fast;
     std::snprintf(buf, sizeof(buf), "env_kernel<%d, %s, %s, %s, %d>", e->ph, x ? "true" : "false",
                   f ? "true" : "false", reset_only ? "true" : "false", pcm);
@@ -2041,6 +1969,10 @@ int vn_create(const VnRoomSet *rooms, int32_t n_agents, const VnConfig *cfg, int
             const int v = atoi(pc);
             if (v >= 0 && v < e->pcache) e->pcache = v;
         }
+        // byte-mark mode with plane rows of <= 2 words: defer each pass's plane marks
+        // to the next step (PendMarks) so the row loads hide behind a step
+        const char *df = getenv("VOXNAV_DEFER");   // A/B knob: 0 marks in the sensing pass
+        e->defer = (e->pcache == 0 && e->nwx <= 2 && e->nwy <= 2 && !(df && df[0] == '0')) ? 1 : 0;
         const int rowb = e->pcache == 2 ? 4 : 8;                            // plane row bytes
         e->xp_off = e->map_bytes;                                           // rows (y, z): pd * ph * nwx words
         e->yp_off = e->xp_off + (uint32_t)(e->pd * e->ph * e->nwx * rowb);  // rows (x, z): pw * ph * nwy words

@@ -1,0 +1,349 @@
+// voxnav_gemm_f32.hip -- the PPO learner's matrix products on the f32 matrix
+// cores (v_mfma_f32_32x32x2_f32: exact f32 products at the f32 peak), the
+// reference's dtype (SB3 policies are f32; train/Grid_Train.py:74-80).
+//
+// One kernel family covers every product of the learner step (sb3
+// RecurrentPPO.train / PPO.train) -- no library GEMM:
+//   forward   Y = act(X W^T + b)          X [M][K] row-major, W [N][K] row-major
+//   backward  dX = dZ W                   dZ [M][K=out] row-major, W [K][N] k-major
+//             dW = dZ^T X  (split-K)      dZ [K=rows][M] k-major, X [K][N] k-major
+//   with dZ = dY (1 - Y^2) formed on load (AGRAD: the Tanh's backward fused
+//   into the operand fetch, no dZ array) and, for dW, the bias gradient
+//   sum_k dZ[k][m] from the same staged tiles.
+//
+// Block: 256 threads, a 128 x 128 tile of C, wave w owns rows 64 (w & 1) and
+// columns 64 (w >> 1) as 2 x 2 accumulators.  K is staged through LDS in
+// chunks of 16, double-buffered (the next chunk's global loads in flight
+// during this chunk's MFMAs).  Both operands are staged k-major ([k][row],
+// [k][col]) so every MFMA operand is one conflict-free ds_read_b32 (lane l
+// supplies A[row l%32][k l/32], B[k l/32][col l%32]); a row-major operand is
+// transposed on its way into LDS.  Split-K (gridDim.z > 1 along K) writes
+// per-split partials that gemm_reduce_kernel sums in split order (the result
+// does not depend on timing).
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "vn_common.h"
+
+using vn_detail::fail;
+
+namespace {
+
+typedef __attribute__((ext_vector_type(16))) float f32x16_t;
+
+constexpr int GT = 128;        // tile rows / cols
+#ifndef VN_GEMM_GK
+#define VN_GEMM_GK 32
+#endif
+constexpr int GK = VN_GEMM_GK;  // K per chunk (A/B knob: 16 or 32)
+constexpr int GNF = GK * GT / 4 / 256;   // float4 of one operand chunk per thread
+constexpr int GKQ = GK / 4;               // float4 per row of a row-major chunk
+constexpr int GP = GT + 4;     // LDS pitch
+
+__device__ __forceinline__ f32x16_t zero16() {
+    f32x16_t z;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) z[r] = 0.0f;
+    return z;
+}
+
+struct GemmArgs {
+    const float *a, *a2;   // A (and Y for AGRAD: element = a * (1 - a2 * a2))
+    const float *b;
+    const float *bias;     // EPI 1/2: [N]
+    float *c;              // C [M][N] (ldc) or split partials [splits][M][N]
+    float *colsum;         // optional (AGRAD, A k-major): split partials of sum_k A[k][m], [splits][M]
+    int64_t lda, ldb, ldc;
+    int64_t sa, sb, sc, sbias;   // batch strides (blockIdx.y = batch)
+    int M, N, K, kper;     // kper: K per split (multiple of GK, except the last split)
+};
+
+// EPI: 0 store, 1 tanh(acc + bias), 2 acc + bias, 3 split partial (c + split * M * N)
+template <bool A_KM, bool B_KM, bool AGRAD, int EPI>
+__global__ __launch_bounds__(256, 2) void gemm_f32_kernel(GemmArgs g) {
+    __shared__ float As[2][GK][GP];
+    __shared__ float Bs[2][GK][GP];
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const int ntn = (g.N + GT - 1) / GT;
+    const int tm = (int)blockIdx.x / ntn, tn = (int)blockIdx.x - tm * ntn;
+    const int bt = (int)blockIdx.y, split = (int)blockIdx.z;
+    const int m0 = tm * GT, n0 = tn * GT;
+    const int k0 = split * g.kper;
+    const int k1 = min(g.K, k0 + g.kper);
+    const float *A = g.a + bt * g.sa;
+    const float *A2 = AGRAD ? g.a2 + bt * g.sa : nullptr;
+    const float *Bm = g.b + bt * g.sb;
+    const int nchunks = (k1 - k0 + GK - 1) / GK;
+    // staging: thread covers 8 floats of each operand chunk (2 float4)
+    //  k-major operand: chunk [GK][GT]: float4 f = tid + 256 i -> (k = f / 32, col 4 (f % 32))
+    //  row-major operand: chunk [GT][GK]: float4 f -> (row = f / GKQ, k 4 (f % GKQ))
+    float4 ra[GNF], rb[GNF];
+    auto ld_op = [&](const float *P, const float *P2, int64_t ld, int base, int lim, bool km, bool grad, int kc,
+                     float4 *r) {
+#pragma unroll
+        for (int i = 0; i < GNF; ++i) {
+            const int f = tid + 256 * i;
+            float4 v = make_float4(0.f, 0.f, 0.f, 0.f), y = v;
+            if (km) {
+                const int k = kc + (f >> 5), cc = base + 4 * (f & 31);
+                if (k < k1) {
+                    const int64_t o = (int64_t)k * ld + cc;
+                    if (cc + 3 < lim && (ld & 3) == 0) {
+                        v = *reinterpret_cast<const float4 *>(P + o);
+                        if (grad) y = *reinterpret_cast<const float4 *>(P2 + o);
+                    } else {
+                        v.x = cc + 0 < lim ? P[o + 0] : 0.f;
+                        v.y = cc + 1 < lim ? P[o + 1] : 0.f;
+                        v.z = cc + 2 < lim ? P[o + 2] : 0.f;
+                        v.w = cc + 3 < lim ? P[o + 3] : 0.f;
+                        if (grad) {
+                            y.x = cc + 0 < lim ? P2[o + 0] : 0.f;
+                            y.y = cc + 1 < lim ? P2[o + 1] : 0.f;
+                            y.z = cc + 2 < lim ? P2[o + 2] : 0.f;
+                            y.w = cc + 3 < lim ? P2[o + 3] : 0.f;
+                        }
+                    }
+                }
+            } else {
+                const int rr = base + f / GKQ, k = kc + 4 * (f % GKQ);
+                if (rr < lim) {
+                    const int64_t o = (int64_t)rr * ld + k;
+                    if (k + 3 < k1 && (ld & 3) == 0) {
+                        v = *reinterpret_cast<const float4 *>(P + o);
+                        if (grad) y = *reinterpret_cast<const float4 *>(P2 + o);
+                    } else {
+                        v.x = k + 0 < k1 ? P[o + 0] : 0.f;
+                        v.y = k + 1 < k1 ? P[o + 1] : 0.f;
+                        v.z = k + 2 < k1 ? P[o + 2] : 0.f;
+                        v.w = k + 3 < k1 ? P[o + 3] : 0.f;
+                        if (grad) {
+                            y.x = k + 0 < k1 ? P2[o + 0] : 0.f;
+                            y.y = k + 1 < k1 ? P2[o + 1] : 0.f;
+                            y.z = k + 2 < k1 ? P2[o + 2] : 0.f;
+                            y.w = k + 3 < k1 ? P2[o + 3] : 0.f;
+                        }
+                    }
+                }
+            }
+            if (grad) {   // dZ = dY (1 - Y^2): the Tanh backward, as torch's tanh_backward
+                v.x = v.x * (1.0f - y.x * y.x);
+                v.y = v.y * (1.0f - y.y * y.y);
+                v.z = v.z * (1.0f - y.z * y.z);
+                v.w = v.w * (1.0f - y.w * y.w);
+            }
+            r[i] = v;
+        }
+    };
+    auto st_op = [&](float (*S)[GP], bool km, const float4 *r) {
+#pragma unroll
+        for (int i = 0; i < GNF; ++i) {
+            const int f = tid + 256 * i;
+            if (km) {
+                *reinterpret_cast<float4 *>(&S[f >> 5][4 * (f & 31)]) = r[i];
+            } else {
+                const int rr = f / GKQ, k = 4 * (f % GKQ);
+                S[k + 0][rr] = r[i].x;
+                S[k + 1][rr] = r[i].y;
+                S[k + 2][rr] = r[i].z;
+                S[k + 3][rr] = r[i].w;
+            }
+        }
+    };
+    // column sums of A (the bias gradient of dW = dZ^T X): thread owns A column
+    // tid & 127 (k-major A only), half the chunk's k each
+    float csum = 0.0f;
+
+    f32x16_t acc[2][2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[i][j] = zero16();
+    const int wr = 64 * (wv & 1), wc = 64 * (wv >> 1);
+    const int col = lane & 31, kh = lane >> 5;
+
+    if (nchunks > 0) {
+        ld_op(A, A2, g.lda, m0, g.M, A_KM, AGRAD, k0, ra);
+        ld_op(Bm, nullptr, g.ldb, n0, g.N, B_KM, false, k0, rb);
+        st_op(As[0], A_KM, ra);
+        st_op(Bs[0], B_KM, rb);
+    }
+    __syncthreads();
+    for (int ch = 0; ch < nchunks; ++ch) {
+        const int bf = ch & 1;
+        if (ch + 1 < nchunks) {
+            ld_op(A, A2, g.lda, m0, g.M, A_KM, AGRAD, k0 + (ch + 1) * GK, ra);
+            ld_op(Bm, nullptr, g.ldb, n0, g.N, B_KM, false, k0 + (ch + 1) * GK, rb);
+        }
+        if (g.colsum && A_KM && tn == 0) {
+            const int cc = tid & 127, kb = (tid >> 7) * (GK / 2);
+#pragma unroll
+            for (int k = 0; k < GK / 2; ++k) csum += As[bf][kb + k][cc];
+        }
+        {
+            // k-step s + 1's operands read before k-step s's MFMAs (4 LDS reads,
+            // then 4 MFMAs, enforced on the scheduler)
+            float pa0, pa1, pb0, pb1, qa0, qa1, qb0, qb1;
+#define GM_RD(s_, A0, A1, B0, B1)                                                                            \
+    {                                                                                                        \
+        const int kk_ = 2 * (s_) + kh;                                                                       \
+        A0 = As[bf][kk_][wr + col];                                                                          \
+        A1 = As[bf][kk_][wr + 32 + col];                                                                     \
+        B0 = Bs[bf][kk_][wc + col];                                                                          \
+        B1 = Bs[bf][kk_][wc + 32 + col];                                                                     \
+    }
+#define GM_MM(A0, A1, B0, B1)                                                                                \
+    {                                                                                                        \
+        acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(A0, B0, acc[0][0], 0, 0, 0);                        \
+        acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(A0, B1, acc[0][1], 0, 0, 0);                        \
+        acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(A1, B0, acc[1][0], 0, 0, 0);                        \
+        acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(A1, B1, acc[1][1], 0, 0, 0);                        \
+    }
+            GM_RD(0, pa0, pa1, pb0, pb1)
+#pragma unroll
+            for (int s = 0; s < GK / 2; s += 2) {
+                GM_RD(s + 1, qa0, qa1, qb0, qb1)
+                GM_MM(pa0, pa1, pb0, pb1)
+                if (s + 2 < GK / 2) GM_RD(s + 2, pa0, pa1, pb0, pb1)
+                GM_MM(qa0, qa1, qb0, qb1)
+            }
+            __builtin_amdgcn_sched_group_barrier(0x100, 4, 0);
+#pragma unroll
+            for (int s = 0; s < GK / 2; ++s) {
+                if (s + 1 < GK / 2) __builtin_amdgcn_sched_group_barrier(0x100, 4, 0);
+                __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);
+            }
+#undef GM_RD
+#undef GM_MM
+        }
+        if (ch + 1 < nchunks) {
+            st_op(As[bf ^ 1], A_KM, ra);
+            st_op(Bs[bf ^ 1], B_KM, rb);
+        }
+        __syncthreads();
+    }
+    if (g.colsum && A_KM && tn == 0) {   // (block-uniform) one column tile per row block writes the sums
+        // the two halves of each column: pairs of threads tid, tid + 128
+        __shared__ float cs2[GT];
+        if (tid >= 128) cs2[tid - 128] = csum;
+        __syncthreads();
+        if (tid < 128 && m0 + tid < g.M) g.colsum[((int64_t)split * gridDim.y + bt) * g.M + m0 + tid] = csum + cs2[tid];
+    }
+    // epilogue: acc[i][j] register v = C[wr + 32 i + 8 (v / 4) + 4 kh + v % 4][wc + 32 j + col]
+    float *C = g.c + bt * g.sc;
+    if (EPI == 3) C = g.c + ((int64_t)split * gridDim.y + bt) * (int64_t)g.M * g.N;
+    const int64_t ldc = EPI == 3 ? g.N : g.ldc;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+        const int n = n0 + wc + 32 * j + col;
+        if (n >= g.N) continue;
+        const float bv = (EPI == 1 || EPI == 2) ? g.bias[bt * g.sbias + n] : 0.0f;
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int v = 0; v < 16; ++v) {
+                const int m = m0 + wr + 32 * i + 8 * (v >> 2) + 4 * kh + (v & 3);
+                if (m >= g.M) continue;
+                float r = acc[i][j][v];
+                if (EPI == 1) r = tanhf(r + bv);
+                else if (EPI == 2) r = r + bv;
+                C[(int64_t)m * ldc + n] = r;
+            }
+    }
+}
+
+// out[b][m][n] = sum over splits s in order of part[s][b][m][n]  (+ out if accumulate)
+__global__ void gemm_reduce_kernel(const float *__restrict__ part, int splits, int64_t per, float *__restrict__ out,
+                                   int accumulate) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= per) return;
+    float s = part[i];
+    for (int k = 1; k < splits; ++k) s += part[(int64_t)k * per + i];
+    out[i] = accumulate ? out[i] + s : s;
+}
+
+template <bool A_KM, bool B_KM, bool AGRAD, int EPI>
+void launch(const GemmArgs &g, int batch, int splits, hipStream_t s) {
+    const int tiles = ((g.M + GT - 1) / GT) * ((g.N + GT - 1) / GT);
+    hipLaunchKernelGGL((gemm_f32_kernel<A_KM, B_KM, AGRAD, EPI>), dim3((unsigned)tiles, (unsigned)batch,
+                                                                        (unsigned)splits),
+                       dim3(256), 0, s, g);
+}
+
+}  // namespace
+
+extern "C" {
+
+// C = act(A_rm [M][K] @ B_rm[N][K]^T + bias): the forward Linear (+ Tanh).
+//   act: 0 none (bias may be NULL), 1 tanh.  Batched over blockIdx.y with strides.
+int vn_gemm_f32_linear(const float *a, int64_t lda, int64_t sa, const float *w, int64_t ldw, int64_t sw,
+                       const float *bias, int64_t sbias, float *c, int64_t ldc, int64_t sc, int32_t M, int32_t N,
+                       int32_t K, int32_t batch, int32_t act, void *stream) {
+    if (!a || !w || !c) return fail(VN_ERR_INVALID, "NULL argument");
+    if (M < 1 || N < 1 || K < 1 || batch < 1) return fail(VN_ERR_INVALID, "bad sizes M=%d N=%d K=%d", M, N, K);
+    if (act == 1 && !bias) return fail(VN_ERR_INVALID, "tanh epilogue needs a bias");
+    GemmArgs g{};
+    g.a = a; g.b = w; g.bias = bias; g.c = c;
+    g.lda = lda; g.ldb = ldw; g.ldc = ldc; g.sa = sa; g.sb = sw; g.sc = sc; g.sbias = sbias;
+    g.M = M; g.N = N; g.K = K; g.kper = K;
+    const hipStream_t s = (hipStream_t)stream;
+    if (act == 1) launch<false, false, false, 1>(g, batch, 1, s);
+    else if (bias) launch<false, false, false, 2>(g, batch, 1, s);
+    else launch<false, false, false, 0>(g, batch, 1, s);
+    VN_HIP(hipGetLastError());
+    return VN_OK;
+}
+
+// C = dZ [M][K] @ W [K][N], dZ = dy (1 - y^2) when y != NULL (the Tanh
+// backward fused into the load), else dZ = dy.  Batched.
+int vn_gemm_f32_dx(const float *dy, const float *y, int64_t ldd, int64_t sd, const float *w, int64_t ldw, int64_t sw,
+                   float *c, int64_t ldc, int64_t sc, int32_t M, int32_t N, int32_t K, int32_t batch, void *stream) {
+    if (!dy || !w || !c) return fail(VN_ERR_INVALID, "NULL argument");
+    if (M < 1 || N < 1 || K < 1 || batch < 1) return fail(VN_ERR_INVALID, "bad sizes M=%d N=%d K=%d", M, N, K);
+    GemmArgs g{};
+    g.a = dy; g.a2 = y; g.b = w; g.c = c;
+    g.lda = ldd; g.ldb = ldw; g.ldc = ldc; g.sa = sd; g.sb = sw; g.sc = sc;
+    g.M = M; g.N = N; g.K = K; g.kper = K;
+    const hipStream_t s = (hipStream_t)stream;
+    if (y) launch<false, true, true, 0>(g, batch, 1, s);
+    else launch<false, true, false, 0>(g, batch, 1, s);
+    VN_HIP(hipGetLastError());
+    return VN_OK;
+}
+
+// Weight gradient over a tall sample axis: C [M][N] = A^T B, A = dZ [K][M]
+// (k-major; dZ = dy (1 - y^2) when y != NULL), B [K][N] k-major; the K axis is
+// split into `splits` parts whose partials (workspace: splits * batch * M * N
+// floats) are summed in order; colsum [batch][M] (optional) receives sum_k
+// dZ[k][m] (workspace2: splits * batch * M floats).  accumulate: C += result.
+int vn_gemm_f32_tn(const float *dy, const float *y, int64_t ldd, int64_t sd, const float *b, int64_t ldb, int64_t sb,
+                   float *c, int64_t sc, float *colsum, int32_t M, int32_t N, int32_t K, int32_t batch, int32_t splits,
+                   float *workspace, float *workspace2, int32_t accumulate, void *stream) {
+    if (!dy || !b || !c || !workspace) return fail(VN_ERR_INVALID, "NULL argument");
+    if (colsum && !workspace2) return fail(VN_ERR_INVALID, "colsum needs workspace2");
+    if (M < 1 || N < 1 || K < 1 || batch < 1 || splits < 1) return fail(VN_ERR_INVALID, "bad sizes");
+    if (sc != (int64_t)M * N) return fail(VN_ERR_INVALID, "C must be contiguous [batch][M][N]");
+    int kper = (K + splits - 1) / splits;
+    kper = (kper + GK - 1) / GK * GK;
+    splits = (K + kper - 1) / kper;
+    GemmArgs g{};
+    g.a = dy; g.a2 = y; g.b = b; g.c = workspace; g.colsum = colsum ? workspace2 : nullptr;
+    g.lda = ldd; g.ldb = ldb; g.ldc = N; g.sa = sd; g.sb = sb; g.sc = 0;
+    g.M = M; g.N = N; g.K = K; g.kper = kper;
+    const hipStream_t s = (hipStream_t)stream;
+    if (y) launch<true, true, true, 3>(g, batch, splits, s);
+    else launch<true, true, false, 3>(g, batch, splits, s);
+    const int64_t per = (int64_t)batch * M * N;
+    hipLaunchKernelGGL(gemm_reduce_kernel, dim3((unsigned)((per + 255) / 256)), dim3(256), 0, s, workspace, splits,
+                       per, c, accumulate);
+    if (colsum) {
+        const int64_t pc = (int64_t)batch * M;
+        hipLaunchKernelGGL(gemm_reduce_kernel, dim3((unsigned)((pc + 255) / 256)), dim3(256), 0, s, workspace2,
+                           splits, pc, colsum, accumulate);
+    }
+    VN_HIP(hipGetLastError());
+    return VN_OK;
+}
+
+}  // extern "C"

@@ -7,6 +7,7 @@ infrastructure and is never used by the product path.)
 from __future__ import annotations
 
 import ctypes as C
+import os
 import threading
 
 from . import _build
@@ -89,12 +90,16 @@ _SIGS = {
     "vn_collect_post_step": (C.c_int, [P, P, C.c_int32, C.c_int32, P, P, P, P, P, P, P, P, C.c_int32, P, C.c_int32,
                                        P, C.c_int32, P, P, P, P, C.c_int32, P, P, P, P, C.c_int32, P]),
     "vn_episode_start": (C.c_int, [P, P, C.c_int32, P, P, P, P, C.c_int32, C.c_int32, P]),
-    "vn_lstm_seq_fwd_cell": (C.c_int, [P, C.c_int64, C.c_int64, P, C.c_int64, P, P, P, P, C.c_int64, C.c_int32,
-                                       C.c_int32, C.c_int32, P]),
-    "vn_lstm_seq_bwd_cell": (C.c_int, [P, C.c_int64, P, P, P, C.c_int64, P, P, C.c_int64, P, C.c_int64, C.c_int32,
-                                       C.c_int32, C.c_int32, P]),
-    "vn_lstm_seq_fwd": (C.c_int, [P, P, P, P, P, P, C.c_int32, C.c_int32, C.c_int32, C.c_int32, P]),
-    "vn_lstm_seq_bwd": (C.c_int, [P, P, P, P, P, P, P, C.c_int32, C.c_int32, C.c_int32, C.c_int32, C.c_int32, P]),
+    "vn_lstm_seq_pack_size": (C.c_int, [C.c_int32, C.c_int32, C.c_int32, P, P]),
+    "vn_lstm_seq_fwd_mfma": (C.c_int, [P, C.c_int32, P, P, P, P, P, P, P, C.c_int32, C.c_int32, C.c_int32, C.c_int32,
+                                       P]),
+    "vn_lstm_seq_bwd_mfma": (C.c_int, [P, P, P, P, P, P, P, P, C.c_int32, C.c_int32, C.c_int32, C.c_int32, P]),
+    "vn_gemm_f32_linear": (C.c_int, [P, C.c_int64, C.c_int64, P, C.c_int64, C.c_int64, P, C.c_int64, P, C.c_int64,
+                                     C.c_int64, C.c_int32, C.c_int32, C.c_int32, C.c_int32, C.c_int32, P]),
+    "vn_gemm_f32_dx": (C.c_int, [P, P, C.c_int64, C.c_int64, P, C.c_int64, C.c_int64, P, C.c_int64, C.c_int64,
+                                 C.c_int32, C.c_int32, C.c_int32, C.c_int32, P]),
+    "vn_gemm_f32_tn": (C.c_int, [P, P, C.c_int64, C.c_int64, P, C.c_int64, C.c_int64, P, C.c_int64, P, C.c_int32,
+                                 C.c_int32, C.c_int32, C.c_int32, C.c_int32, P, P, C.c_int32, P]),
 }
 EXPORTED_SYMBOLS = tuple(_SIGS)
 
@@ -130,7 +135,10 @@ def load(build_if_missing: bool = True):
         # torch first: its libamdhip64.so.7 then satisfies our NEEDED entry, so
         # the process has one HIP runtime.
         import torch  # noqa: F401
-        _lib = _bind(C.CDLL(str(_build.LIB)))
+        # VOXNAV_LIB: another build of the library in the product's place
+        # (A/B timing of diagnostics builds under _lib/variants only)
+        alt = os.environ.get("VOXNAV_LIB")
+        _lib = _bind(C.CDLL(str(alt if alt else _build.LIB)), strict=not alt)
         return _lib
 
 

@@ -1,0 +1,172 @@
+"""The PPO learner's matrix products on the f32 matrix cores (no library GEMM).
+
+Autograd functions over the HIP kernels of csrc/voxnav_gemm_f32.hip for the
+learner's Linear layers (SB3 ``MlpExtractor`` + ``action_net`` /
+``value_net``, reached from ``RecurrentPPO.train`` / ``PPO.train`` at
+train/Grid_Train.py:228) and the LSTM weight gradients:
+
+* ``linear_tanh_pair``: one Tanh layer of BOTH branches (pi, vf) per launch,
+  forward ``tanh(x W^T + b)``; backward ``dX = (dY (1 - Y^2)) W`` with the
+  Tanh backward formed on the operand load, ``dW = dZ^T X`` split over the
+  sample axis (per-split partials summed in order) and ``db = sum dZ`` from
+  the same staged tiles;
+* ``linear``: a Linear without activation (the heads), same backward;
+* ``mm_tn``: ``a^T b`` over a tall sample axis (+ the column sums of a).
+
+f32 throughout (the reference's dtype).  CUDA tensors only; the CPU path
+(the CPU parity tests) uses torch's own ops.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from typing import Optional, Tuple
+
+import torch
+
+from . import _native
+
+SPLIT_ROWS = 256         # minimum rows of the sample axis per split of a weight-gradient product
+
+
+def _p(t: Optional[torch.Tensor]):
+    return None if t is None else C.c_void_p(t.data_ptr())
+
+
+def _stream(dev):
+    return C.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
+
+
+def _splits(K: int, tiles: int) -> int:
+    """Split count for a K-long reduction whose output has `tiles` 128x128 tiles:
+    enough blocks to fill the chip (>= ~512), at least SPLIT_ROWS rows each."""
+    want = max(1, -(-512 // max(1, tiles)))
+    return max(1, min(want, 256, K // SPLIT_ROWS))
+
+
+def mm_tn(a: torch.Tensor, b: torch.Tensor, y: Optional[torch.Tensor] = None, colsum: bool = False,
+          out: Optional[torch.Tensor] = None) -> Tuple[torch.Tensor, Optional[torch.Tensor]]:
+    """Batched ``z^T b`` with z = a (1 - y^2) if y is given else a.
+    a, y: [batch, K, M]; b: [batch, K, N] (batch stride 0 allowed via expand);
+    returns ([batch, M, N], [batch, M] column sums of z or None)."""
+    lib = _native.load()
+    Bt, K, M = a.shape
+    N = b.shape[2]
+    dev = a.device
+    if a.stride(2) != 1 or a.stride(1) != M or b.stride(2) != 1 or b.stride(1) != N:
+        raise ValueError("mm_tn: operands must be row-contiguous [batch, K, cols]")
+    tiles = -(-M // 128) * -(-N // 128) * Bt
+    sp = _splits(K, tiles)
+    out = torch.empty((Bt, M, N), dtype=torch.float32, device=dev) if out is None else out
+    ws = torch.empty(sp * Bt * M * N, dtype=torch.float32, device=dev)
+    cs = torch.empty((Bt, M), dtype=torch.float32, device=dev) if colsum else None
+    ws2 = torch.empty(sp * Bt * M, dtype=torch.float32, device=dev) if colsum else None
+    _native.check(lib.vn_gemm_f32_tn(_p(a), _p(y), M, a.stride(0), _p(b), N, b.stride(0), _p(out), M * N, _p(cs),
+                                     M, N, K, Bt, sp, _p(ws), _p(ws2), 0, _stream(dev)), "vn_gemm_f32_tn")
+    return out, cs
+
+
+class _LinearTanhPair(torch.autograd.Function):
+    """y[br] = tanh(x[br] W[br]^T + b[br]) for br in (pi, vf): x [2, M, K]
+    (batch stride 0 when both branches read the same input), W [2, N, K], b [2, N]."""
+
+    @staticmethod
+    def forward(ctx, x, w, b, tanh: bool):
+        lib = _native.load()
+        _, M, K = x.shape
+        N = w.shape[1]
+        dev = x.device
+        y = torch.empty((2, M, N), dtype=torch.float32, device=dev)
+        _native.check(lib.vn_gemm_f32_linear(_p(x), K, x.stride(0), _p(w), K, N * K, _p(b), N, _p(y), N, M * N, M, N,
+                                             K, 2, 1 if tanh else 0, _stream(dev)), "vn_gemm_f32_linear")
+        ctx.save_for_backward(x, w, y)
+        ctx.tanh = tanh
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        lib = _native.load()
+        x, w, y = ctx.saved_tensors
+        _, M, K = x.shape
+        N = w.shape[1]
+        dev = x.device
+        st = _stream(dev)
+        dy = dy.contiguous()
+        yy = y if ctx.tanh else None
+        dx = None
+        if ctx.needs_input_grad[0]:
+            dx = torch.empty((2, M, K), dtype=torch.float32, device=dev)
+            # dX = dZ W: W [N][K] row-major is the k-major operand of this product
+            _native.check(lib.vn_gemm_f32_dx(_p(dy), _p(yy), N, M * N, _p(w), K, N * K, _p(dx), K, M * K, M, K, N, 2,
+                                             st), "vn_gemm_f32_dx")
+            # (a shared input was expanded outside: expand's backward sums the branches)
+        dw, db = mm_tn(dy, x, y=yy, colsum=True)
+        return dx, dw, db, None
+
+
+def linear_tanh_pair(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor, tanh: bool = True) -> torch.Tensor:
+    """x [2, M, K] (or [M, K], shared by both branches), w [2, N, K], b [2, N] -> [2, M, N]."""
+    if x.dim() == 2:
+        x = x.contiguous().unsqueeze(0).expand(2, *x.shape)
+    elif not x.is_contiguous():
+        x = x.contiguous()
+    return _LinearTanhPair.apply(x, w, b, tanh)
+
+
+class _Linear(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, w, b):
+        lib = _native.load()
+        M, K = x.shape
+        N = w.shape[0]
+        dev = x.device
+        y = torch.empty((M, N), dtype=torch.float32, device=dev)
+        _native.check(lib.vn_gemm_f32_linear(_p(x), K, 0, _p(w), K, 0, _p(b), 0, _p(y), N, 0, M, N, K, 1, 0,
+                                             _stream(dev)), "vn_gemm_f32_linear")
+        ctx.save_for_backward(x, w)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        lib = _native.load()
+        x, w = ctx.saved_tensors
+        M, K = x.shape
+        N = w.shape[0]
+        dev = x.device
+        dy = dy.contiguous()
+        dx = None
+        if ctx.needs_input_grad[0]:
+            dx = torch.empty((M, K), dtype=torch.float32, device=dev)
+            _native.check(lib.vn_gemm_f32_dx(_p(dy), None, N, 0, _p(w), K, 0, _p(dx), K, 0, M, K, N, 1, _stream(dev)),
+                          "vn_gemm_f32_dx")
+        dw, db = mm_tn(dy.unsqueeze(0), x.unsqueeze(0), colsum=True)
+        return dx, dw[0], db[0]
+
+
+def linear(x: torch.Tensor, module: torch.nn.Linear) -> torch.Tensor:
+    """``module(x)`` for 2-D x on the matrix-core kernels (CUDA), torch otherwise."""
+    if x.device.type != "cuda":
+        return module(x)
+    return _Linear.apply(x.contiguous(), module.weight, module.bias)
+
+
+def mlp_pair(pi_net: torch.nn.Sequential, vf_net: torch.nn.Sequential, x_pi: torch.Tensor,
+             x_vf: Optional[torch.Tensor] = None) -> Tuple[torch.Tensor, torch.Tensor]:
+    """Both SB3 MLP branches (Linear + Tanh layers of equal widths) layer by
+    layer, the two branches of a layer in one launch.  ``x_vf is None``: both
+    read ``x_pi`` (MlpPolicy's observation)."""
+    def tanh_layers(seq):   # [Linear, Tanh] * n, or None
+        mods = list(seq)
+        if len(mods) % 2 or not all(isinstance(a, torch.nn.Linear) and a.bias is not None and
+                                    isinstance(t, torch.nn.Tanh) for a, t in zip(mods[0::2], mods[1::2])):
+            return None
+        return mods[0::2]
+    lin_pi, lin_vf = tanh_layers(pi_net), tanh_layers(vf_net)
+    if (x_pi.device.type != "cuda" or lin_pi is None or lin_vf is None or len(lin_pi) != len(lin_vf) or
+            any(a.weight.shape != b.weight.shape for a, b in zip(lin_pi, lin_vf))):
+        return pi_net(x_pi), vf_net(x_pi if x_vf is None else x_vf)
+    h = x_pi if x_vf is None else torch.stack([x_pi, x_vf])
+    for a, b in zip(lin_pi, lin_vf):
+        w = torch.stack([a.weight, b.weight])
+        bb = torch.stack([a.bias, b.bias])
+        h = linear_tanh_pair(h, w, bb, tanh=True)
+    return h[0], h[1]

@@ -6,21 +6,19 @@ sb3_contrib ``RecurrentPPO.train`` re-runs the actor and the critic LSTM of
 at train/Grid_Train.py:228) and back-propagates through them.  Here both
 LSTMs run together over the padded ``[L, B]`` batch:
 
-forward   ``gx = X @ [W_ih_actor | W_ih_critic]^T`` for all steps (one GEMM);
-          then ``vn_lstm_seq_fwd``: the time loop in native code, per step
-          ``h_{t-1} @ W_hh^T`` for both LSTMs (one batched rocBLAS GEMM)
-          and the cell kernel (gates, cell, h; the activations are kept for
-          the backward pass);
-backward  ``vn_lstm_seq_bwd``: per step, in reverse, the backward cell
-          kernel (gate gradients dG_t, dc_{t-1}) and ``dh_{t-1} = dG_t @
-          W_hh`` (batched); then the weight gradients over all steps at
-          once: ``dW_hh = dG^T H_prev`` (batched), ``dW_ih = dG^T X``,
-          ``db = sum dG``.
+forward   ``vn_lstm_seq_fwd_mfma``: the time loop in native code, one
+          launch per step: ``[x_t | h_{t-1}] @ [W_ih | W_hh]^T`` for both
+          LSTMs on the f32 matrix cores with the cell update (gates, c, h;
+          the activations are kept for the backward pass) as the epilogue;
+backward  ``vn_lstm_seq_bwd_mfma``: per step, in reverse, ``dh_t +=
+          dG_{t+1} @ W_hh`` on the matrix cores with the backward cell
+          (gate gradients dG_t, dc_{t-1}) as the epilogue; then the weight
+          gradients over all steps at once: ``dW_hh = dG^T H_prev``,
+          ``dW_ih = dG^T X``, ``db = sum dG``.
 
-The GEMMs are library GEMMs (rocBLAS in the loops, hipBLASLt through torch
-outside), f32 -- the reference's dtype; the cell kernels and the loops are
-csrc/voxnav_learn.hip.  The loops are native because issued from Python
-each step's two launches cost more host time than their GPU time.
+The loop kernels are csrc/voxnav_learn_f32.hip (f32, the reference's dtype);
+the loops are native because issued from Python each step's launch costs
+more host time than its GPU time.
 Padded steps sit after each sequence's real steps and get zero output
 gradient from the masked losses, so they never influence the real ones --
 the same result as sb3's per-step masked loop (a sequence only begins with
@@ -36,7 +34,7 @@ from typing import Tuple
 
 import torch
 
-from . import _native, splitk
+from . import _native, learn_ops
 
 
 def _p(t: torch.Tensor):
@@ -58,27 +56,40 @@ class _DualLSTM(torch.autograd.Function):
         G = 4 * H
         dev = x.device
         st = _stream(dev)
-        xf = x.reshape(L * B, D).contiguous()
-        w_ih = torch.cat([w_ih_a, w_ih_c], 0)                       # [2*4H, D]
-        w_hh = torch.stack([w_hh_a, w_hh_c]).contiguous()          # [2, 4H, H]
+        xc = x.contiguous()
+        w_ih = torch.stack([w_ih_a, w_ih_c])                         # [2, 4H, D]
+        D0 = D
+        if D % 4:
+            # the kernels read x and W_ih in float4s: zero-pad the input width
+            # (e.g. simpleEnv's 6L + 7 observation) -- zero columns add nothing
+            D = (D + 3) // 4 * 4
+            xc = torch.nn.functional.pad(xc, (0, D - D0))
+            w_ih = torch.nn.functional.pad(w_ih, (0, D - D0))
+        w_ih = w_ih.contiguous()
+        w_hh = torch.stack([w_hh_a, w_hh_c]).contiguous()            # [2, 4H, H]
         bias = torch.stack([b_ih_a + b_hh_a, b_ih_c + b_hh_c]).contiguous()
-        gx = xf @ w_ih.t()                                          # [L*B, 2*4H]
+        nf, nb = C.c_int64(), C.c_int64()
+        _native.check(lib.vn_lstm_seq_pack_size(2, D, H, C.byref(nf), C.byref(nb)), "vn_lstm_seq_pack_size")
+        wpack = torch.empty(nf.value, dtype=torch.float32, device=dev)
         hs = torch.empty((2, L + 1, B, H), dtype=torch.float32, device=dev)
         cs = torch.empty_like(hs)
         hs[:, 0] = h0
         cs[:, 0] = c0
         act = torch.empty((L, 2, B, G), dtype=torch.float32, device=dev)   # step-major: act[t] contiguous
-        _native.check(lib.vn_lstm_seq_fwd(_p(gx), _p(w_hh), _p(bias), _p(hs), _p(cs), _p(act), 2, L, B, H, st),
-                      "vn_lstm_seq_fwd")
+        # [x_t | h_{t-1}] @ [W_ih | W_hh]^T and the cell, one fused launch per step
+        _native.check(lib.vn_lstm_seq_fwd_mfma(_p(xc), D, _p(w_ih), _p(w_hh), _p(bias), _p(wpack), _p(hs), _p(cs),
+                                               _p(act), 2, L, B, H, st), "vn_lstm_seq_fwd_mfma")
+        xf = xc.view(L * B, D)
         ctx.save_for_backward(xf, w_ih_a, w_ih_c, w_hh, hs, cs, act)
-        ctx.dims = (L, B, D, H)
+        ctx.dims = (L, B, D, D0, H)
+        ctx.bwd_pack = nb.value
         return hs[:, 1:]
 
     @staticmethod
     def backward(ctx, d_out):
         lib = _native.load()
         xf, w_ih_a, w_ih_c, w_hh, hs, cs, act = ctx.saved_tensors
-        L, B, D, H = ctx.dims
+        L, B, D, D0, H = ctx.dims
         G = 4 * H
         dev = xf.device
         st = _stream(dev)
@@ -87,17 +98,21 @@ class _DualLSTM(torch.autograd.Function):
         dc = torch.zeros((2, B, H), dtype=torch.float32, device=dev)
         dh = torch.empty((2, B, H), dtype=torch.float32, device=dev)
         need_h0 = ctx.needs_input_grad[1]
-        _native.check(lib.vn_lstm_seq_bwd(_p(dh_out), _p(w_hh), _p(act), _p(cs), _p(dG), _p(dc), _p(dh),
-                                          1 if need_h0 else 0, 2, L, B, H, st), "vn_lstm_seq_bwd")
+        wpack = torch.empty(ctx.bwd_pack, dtype=torch.float32, device=dev)
+        # per step (reverse): dh_t += dG_{t+1} @ W_hh and the cell backward, one fused launch
+        _native.check(lib.vn_lstm_seq_bwd_mfma(_p(dh_out), _p(w_hh), _p(wpack), _p(act), _p(cs), _p(dG), _p(dc),
+                                               _p(dh) if need_h0 else None, 2, L, B, H, st), "vn_lstm_seq_bwd_mfma")
         dGf = dG.view(2, L * B, G)
-        # dG^T H_prev, split over the samples (hs[l, :L] is a contiguous view)
-        d_w_hh = [splitk.mm_tn(dGf[k], hs[k, :L].reshape(L * B, H)) for k in range(2)]
-        d_w_ih_a = splitk.mm_tn(dGf[0], xf)
-        d_w_ih_c = splitk.mm_tn(dGf[1], xf)
-        db = dGf.sum(1)
+        # weight gradients over all steps on the matrix cores (split over the
+        # samples): dW_hh = dG^T H_prev (hs[:, :L] is a strided view), dW_ih =
+        # dG^T X, db = sum dG (the column sums of the same staged dG tiles)
+        d_w_hh, _ = learn_ops.mm_tn(dGf, hs[:, :L].reshape(2, L * B, H))
+        d_w_ih, db = learn_ops.mm_tn(dGf, xf.unsqueeze(0).expand(2, L * B, D), colsum=True)
+        d_w_ih_a, d_w_ih_c = d_w_ih[0, :, :D0], d_w_ih[1, :, :D0]
+        d_w_hh = (d_w_hh[0], d_w_hh[1])
         dx = None
         if ctx.needs_input_grad[0]:
-            dx = (dGf[0] @ w_ih_a + dGf[1] @ w_ih_c).view(L, B, D)
+            dx = (dGf[0] @ w_ih_a + dGf[1] @ w_ih_c).view(L, B, D0)
         dh0 = dh.clone() if need_h0 else None
         dc0 = dc.clone() if ctx.needs_input_grad[2] else None
         # b_ih and b_hh get the same gradient, but as separate tensors:

@@ -20,9 +20,9 @@ normalize_advantage True, Adam eps 1e-5):
 Everything stays on the device: minibatch rows are gathered straight from
 the collector's ``[T, N]``-major buffers by index arithmetic (no flattened
 copies), sequences are packed with one scatter, and both LSTMs run together
-over the padded batch (``voxnav.lstm_seq.dual_lstm``: library GEMMs and the
-per-step cell kernels of csrc/voxnav_learn.hip, forward and backward),
-which equals sb3's masked per-step loop because a sequence can only begin
+over the padded batch (``voxnav.lstm_seq.dual_lstm``: one fused
+matrix-core launch per step, csrc/voxnav_learn_f32.hip, forward and
+backward), which equals sb3's masked per-step loop because a sequence can only begin
 with an episode start.
 The one host round-trip per recurrent minibatch is the (n_seq, max_len)
 pair that sizes the padded tensor.
@@ -37,13 +37,14 @@ The minibatch order is drawn from ``numpy.random.default_rng(seed)``
 """
 from __future__ import annotations
 
+from contextlib import nullcontext as _nullctx
 from typing import Dict, List, Optional, Sequence
 
 import numpy as np
 import torch
 import torch.nn.functional as Fn
 
-from . import splitk
+from . import learn_ops
 from .lstm_seq import dual_lstm
 from .policy import ActorCriticPolicy, RecurrentActorCriticPolicy
 
@@ -92,28 +93,73 @@ class PPOLearner:
 
     def _heads(self, lat_pi, lat_vf, actions):
         pol = self.policy
-        # split-K weight gradients over the minibatch (voxnav/splitk.py)
-        logits = splitk.linear(splitk.sequential(pol.mlp_extractor.policy_net, lat_pi), pol.action_net)
-        values = splitk.linear(splitk.sequential(pol.mlp_extractor.value_net, lat_vf), pol.value_net).flatten()
+        # both MLP branches layer by layer and the heads on the f32 matrix
+        # cores (voxnav/learn_ops.py; torch's own ops on the CPU)
+        ex = pol.mlp_extractor
+        h_pi, h_vf = learn_ops.mlp_pair(ex.policy_net, ex.value_net, lat_pi, None if lat_vf is lat_pi else lat_vf)
+        logits = learn_ops.linear(h_pi, pol.action_net)
+        values = learn_ops.linear(h_vf, pol.value_net).flatten()
         logp_all = torch.log_softmax(logits, dim=-1)
         log_prob = logp_all.gather(1, actions.view(-1, 1)).flatten()
         entropy = -(logp_all.exp() * logp_all).sum(-1)
         return values, log_prob, entropy
 
-    def _evaluate_recurrent(self, buf, idx: torch.Tensor):
-        """evaluate_actions on minibatch rows ``idx`` (env-major flat ids)."""
+    def _pack_begin(self, buf, idx: torch.Tensor) -> dict:
+        """The sequence structure of minibatch rows ``idx`` (env-major flat
+        ids): sequences start at episode starts and env changes
+        (sb3_contrib create_sequencers).  Everything but the padded size
+        (n_seq, max_len) stays on the device; on CUDA the structure is
+        computed on a side stream and the size copied to pinned host memory,
+        so the one host read per minibatch can wait for it while the previous
+        minibatch's update still runs (``update_many``)."""
         T, N = buf.actions.shape
         dev = idx.device
-        env = idx // T
-        t = idx - env * T
-        src = t * N + env                                         # row in the [T, N]-major buffers
-        es = buf.episode_starts.reshape(-1)[src]
-        seq_start = (es > 0.5) | (t == 0)                         # episode start or env change
-        seq_start[0] = True
-        seq_id = torch.cumsum(seq_start.to(torch.int64), 0) - 1
-        first = torch.nonzero(seq_start, as_tuple=True)[0]       # position of each sequence start
-        pos = torch.arange(idx.numel(), device=dev) - first[seq_id]
-        n_seq, max_len = (int(v) for v in torch.stack([seq_id[-1] + 1, pos.max() + 1]).tolist())
+        side = None
+        if dev.type == "cuda":
+            if getattr(self, "_side", None) is None:
+                self._side = torch.cuda.Stream(dev)
+            side = self._side
+            side.wait_stream(torch.cuda.current_stream(dev))
+        with torch.cuda.stream(side) if side is not None else _nullctx():
+            env = idx // T
+            t = idx - env * T
+            src = t * N + env                                         # row in the [T, N]-major buffers
+            es = buf.episode_starts.reshape(-1)[src]
+            seq_start = (es > 0.5) | (t == 0)                         # episode start or env change
+            seq_start[0] = True
+            seq_id = torch.cumsum(seq_start.to(torch.int64), 0) - 1
+            ar = torch.arange(idx.numel(), device=dev)
+            # position in the sequence: distance to the last start at or before (a running max, no sync)
+            pos = ar - torch.cummax(torch.where(seq_start, ar, torch.zeros_like(ar)), 0).values
+            size = torch.stack([seq_id[-1] + 1, pos.max() + 1])
+            pk = dict(idx=idx, env=env, t=t, src=src, es=es, seq_start=seq_start, seq_id=seq_id, pos=pos)
+            if side is not None:
+                host = torch.empty(2, dtype=torch.int64, pin_memory=True)
+                host.copy_(size, non_blocking=True)
+                ev = torch.cuda.Event()
+                ev.record(side)
+                pk.update(host=host, ev=ev)
+            else:
+                pk.update(host=size)
+        if side is not None:
+            main = torch.cuda.current_stream(dev)
+            for v in pk.values():
+                if isinstance(v, torch.Tensor) and v.is_cuda:
+                    v.record_stream(main)            # made on the side stream, used on the main one
+        return pk
+
+    def _evaluate_recurrent(self, buf, pk: dict):
+        """evaluate_actions on a packed minibatch (``_pack_begin``)."""
+        T, N = buf.actions.shape
+        if "ev" in pk:
+            pk["ev"].synchronize()                                # the minibatch's size only
+            torch.cuda.current_stream(pk["idx"].device).wait_event(pk["ev"])
+        n_seq, max_len = (int(v) for v in pk["host"].tolist())
+        src, es, seq_start, seq_id, pos, t, env = (pk[k] for k in ("src", "es", "seq_start", "seq_id", "pos", "t",
+                                                                   "env"))
+        dev = src.device
+        first = (torch.nonzero_static(seq_start, size=n_seq).flatten() if dev.type == "cuda"
+                 else torch.nonzero(seq_start, as_tuple=True)[0])   # position of each sequence start
         D = buf.obs.shape[-1]
         x = torch.zeros((max_len, n_seq, D), dtype=torch.float32, device=dev)
         x[pos, seq_id] = buf.obs.reshape(T * N, D)[src]
@@ -135,12 +181,14 @@ class PPOLearner:
         acts = buf.actions.reshape(-1)[src].long()
         return self._heads(obs, obs, acts), src
 
-    def update(self, buf, idx: torch.Tensor) -> torch.Tensor:
+    def update(self, buf, idx: torch.Tensor, packed: Optional[dict] = None) -> torch.Tensor:
         """One minibatch (env-major flat ids ``idx``): losses, backward,
         (all-reduce), clip, Adam.  Returns the logged values as a device
-        tensor (no host sync)."""
-        (values, log_prob, entropy), src = (self._evaluate_recurrent(buf, idx) if self.recurrent
-                                            else self._evaluate_ff(buf, idx))
+        tensor (no host sync beyond the recurrent minibatch's size)."""
+        if self.recurrent:
+            (values, log_prob, entropy), src = self._evaluate_recurrent(buf, packed or self._pack_begin(buf, idx))
+        else:
+            (values, log_prob, entropy), src = self._evaluate_ff(buf, idx)
         adv = buf.advantages.reshape(-1)[src]
         if self.normalize_advantage and (self.recurrent or adv.numel() > 1):
             adv = (adv - adv.mean()) / (adv.std() + 1e-8)
@@ -168,6 +216,23 @@ class PPOLearner:
                                 (torch.abs(ratio - 1) > self.clip_range).double().mean(),
                                 gnorm.detach().double()])
 
+    def update_many(self, buf, idxs: Sequence[torch.Tensor]) -> torch.Tensor:
+        """``update`` over consecutive minibatches, the next minibatch's
+        sequence structure computed (side stream) while this one's update is
+        queued, so the host read of its size does not idle the GPU.
+        Returns the stacked logs [n, 7]."""
+        idxs = list(idxs)
+        if not idxs:
+            return torch.zeros((0, 7), dtype=torch.float64)
+        nxt = self._pack_begin(buf, idxs[0]) if self.recurrent else None
+        logs = []
+        for i, idx in enumerate(idxs):
+            cur = nxt
+            if self.recurrent and i + 1 < len(idxs):
+                nxt = self._pack_begin(buf, idxs[i + 1])
+            logs.append(self.update(buf, idx, packed=cur))
+        return torch.stack(logs)
+
     # ------------------------------------------------------------ train
     def train(self, buf, epoch_orders: Optional[Sequence] = None) -> Dict[str, float]:
         """One ``train()`` over a collector ``RolloutBuffer`` (n_epochs passes).
@@ -186,9 +251,9 @@ class PPOLearner:
                 perm = torch.roll(torch.arange(total, device=dev), -int(order))
             else:
                 perm = torch.as_tensor(np.asarray(order), dtype=torch.int64, device=dev)
-            for s in range(0, total, self.batch_size):
-                acc += self.update(buf, perm[s:s + self.batch_size])
-                n_mb += 1
+            logs = self.update_many(buf, [perm[s:s + self.batch_size] for s in range(0, total, self.batch_size)])
+            acc += logs.sum(0)
+            n_mb += logs.shape[0]
         m = (acc / max(1, n_mb)).tolist()
         with torch.no_grad():
             v, r = buf.values.reshape(-1), buf.returns.reshape(-1)

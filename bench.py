@@ -86,8 +86,9 @@ def parse(argv=None):
                          "BASELINE config C4) and mlp (PPO-MLP, P2_training, config C3), or none")
     ap.add_argument("--collector-T", type=int, default=128, help="rollout length (n_steps) of the collector leg")
     ap.add_argument("--collector-rollouts", type=int, default=2, help="timed rollouts of the collector leg")
-    ap.add_argument("--collector-bf16", type=int, default=1,
-                    help="also time the PPO-LSTM collector with bf16 policy GEMMs (the reference's policy is f32)")
+    ap.add_argument("--collector-bf16", type=int, default=0,
+                    help="also time the PPO-LSTM collector with bf16 policy GEMMs (an option: the reference's policy "
+                         "is f32, so it is not a default leg)")
     ap.add_argument("--learner-batch", type=int, default=65536,
                     help="PPO learner legs: minibatch size (0 = skip); run on each f32 collector's buffer")
     ap.add_argument("--learner-minibatches", type=int, default=16, help="timed learner minibatch updates")
@@ -380,21 +381,20 @@ def learner_leg(args, torch, dist, dev, world, pol, buf, kind):
     perm = torch.roll(torch.arange(T * N, device=dev), -12345 % (T * N))
     if kind == "mlp":
         perm = torch.randperm(T * N, device=dev, generator=torch.Generator(device=dev).manual_seed(0))
-    for m in range(2):
-        ln.update(buf, perm[m * B:(m + 1) * B])
+    ln.update_many(buf, [perm[m * B:(m + 1) * B] for m in range(2)])
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
     t0 = time.perf_counter()
-    for m in range(n):
-        ln.update(buf, perm[(m % ((T * N) // B)) * B:(m % ((T * N) // B) + 1) * B])
+    nb = (T * N) // B
+    ln.update_many(buf, [perm[(m % nb) * B:(m % nb + 1) * B] for m in range(n)])
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
     el, = _max_over_ranks(torch, dist, dev, world, time.perf_counter() - t0)
     sps = n * B * world / el
     fl = 3 * (lstm_flops_per_agent_step() if kind == "lstm" else mlp_flops_per_agent_step())  # fwd + bwd ~ 3x fwd
-    inc = ("sequence packing, actor+critic LSTM re-run (dual-LSTM: library GEMMs + HIP cell kernels), MLPs, "
+    inc = ("sequence packing, actor+critic LSTM re-run (fused MFMA step kernels), MLPs (MFMA GEMM kernels), "
            if kind == "lstm" else "minibatch gather, actor/critic MLPs, ")
     return {"value": round(sps, 1), "unit": "samples/s", "batch_size": B, "minibatches": n,
             "ms_per_minibatch": round(el * 1e3 / n, 3), "tflops": round(fl * sps / 1e12, 2),

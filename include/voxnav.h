@@ -387,65 +387,53 @@ int vn_collect_post_step(const uint8_t *terminated, const uint8_t *truncated, in
 /* ------------------------------------------------------------------------
  * PPO learner: the LSTM re-run of sb3_contrib RecurrentPPO.train
  * (RecurrentActorCriticPolicy.evaluate_actions -> _process_sequence, from
- * model.learn at train/Grid_Train.py:228) and its backward pass.  The
- * GEMMs are library GEMMs issued by the caller; these are the per-step
- * cell kernels in between, for n_lstm LSTMs (actor, critic) at once.
- * Gate order i, f, g, o (torch nn.LSTM).  All device f32, stream-ordered.
+ * model.learn at train/Grid_Train.py:228), its backward pass, and the
+ * Linear layers of the update -- all on the library's own f32 matrix-core
+ * kernels.  Gate order i, f, g, o (torch nn.LSTM).  All device f32,
+ * stream-ordered.
  * ---------------------------------------------------------------------- */
 
 /*
- * Forward step: pre = gx + gates + bias; i,f,g,o = sig, sig, tanh, sig;
- * c_new = f*c_prev + i*g; h_new = o*tanh(c_new); gates := (i, f, g, o).
- *   gx     element (l, b, j) at gx[b*gx_row_stride + l*gx_lstm_stride + j]
- *          (X @ [W_ih_0 | W_ih_1 ...]^T, one GEMM for all steps)
- *   gates  [n_lstm][B][4H] at lstm stride gate_lstm_stride; in: h_prev @
- *          W_hh^T, out: the activations (kept for the backward step)
- *   bias   [n_lstm][4H] (b_ih + b_hh)
- *   c_prev, c_new, h_new  [n_lstm][B][H] at lstm stride state_lstm_stride
- * H and every stride a multiple of 4.
+ * The learner's LSTM time loops on the f32 matrix cores (csrc/voxnav_learn_f32.hip;
+ * sb3_contrib RecurrentPPO.train's LSTM re-run, train/Grid_Train.py:228, SURVEY.md
+ * App. D.3): one launch per step, the whole product and the cell (or its backward)
+ * fused.  vn_lstm_seq_pack_size gives the float counts of the two weight
+ * workspaces (packed once per call).
+ *   x      [L][B][D]                 w_ih [n_lstm][4H][D]   w_hh [n_lstm][4H][H]
+ *   bias   [n_lstm][4H] = b_ih + b_hh
+ *   hs, cs [n_lstm][L+1][B][H]       (index 0: the initial state, set by the caller)
+ *   act    [L][n_lstm][B][4H]        (out: i, f, g, o after the nonlinearities)
+ * Backward: dh_out [n_lstm][L][B][H] (gradient of the outputs), dG [n_lstm][L][B][4H]
+ * (out), dc [n_lstm][B][H] (in: zeros = dL/dc_{L-1}; out: dL/dc_0), dh0 [n_lstm][B][H]
+ * (out: dL/dh_0) or NULL.  D and H must be multiples of 4.
  */
-int vn_lstm_seq_fwd_cell(const float *gx, int64_t gx_row_stride, int64_t gx_lstm_stride, float *gates,
-                         int64_t gate_lstm_stride, const float *bias, const float *c_prev, float *c_new, float *h_new,
-                         int64_t state_lstm_stride, int32_t n_lstm, int32_t B, int32_t H, void *stream);
-
-/*
- * Backward step: dh = dh_out + dh_rec (dh_rec = dG_{t+1} @ W_hh, or NULL at
- * the last step); dc [n_lstm][B][H] contiguous (in: dL/dc_t, out:
- * dL/dc_{t-1}); dG [n_lstm][B][4H] at lstm stride dG_lstm_stride, the gate
- * pre-activation gradient, from the forward's activations act (lstm stride
- * act_lstm_stride) and c_prev, c_new (lstm stride state_lstm_stride).
- *   dh_out [n_lstm][B][H] at lstm stride dh_out_lstm_stride
- */
-int vn_lstm_seq_bwd_cell(const float *dh_out, int64_t dh_out_lstm_stride, const float *dh_rec, float *dc,
-                         const float *act, int64_t act_lstm_stride, const float *c_prev, const float *c_new,
-                         int64_t state_lstm_stride, float *dG, int64_t dG_lstm_stride, int32_t n_lstm, int32_t B,
+int vn_lstm_seq_pack_size(int32_t n_lstm, int32_t D, int32_t H, int64_t *fwd_floats, int64_t *bwd_floats);
+int vn_lstm_seq_fwd_mfma(const float *x, int32_t D, const float *w_ih, const float *w_hh, const float *bias,
+                         float *wpack, float *hs, float *cs, float *act, int32_t n_lstm, int32_t L, int32_t B,
                          int32_t H, void *stream);
+int vn_lstm_seq_bwd_mfma(const float *dh_out, const float *w_hh, float *wpack, const float *act, const float *cs,
+                         float *dG, float *dc, float *dh0, int32_t n_lstm, int32_t L, int32_t B, int32_t H,
+                         void *stream);
 
 /*
- * The whole forward time loop of n_lstm LSTMs over L steps (replaces the
- * per-step Python loop of voxnav/lstm_seq.py; sb3_contrib
- * RecurrentActorCriticPolicy._process_sequence as called by
- * RecurrentPPO.train, reached from train/Grid_Train.py:228).  Per step t:
- * act[t][l] = hs[l][t] @ W_hh[l]^T (rocBLAS, both LSTMs batched), then the
- * forward cell step above (gx row stride n_lstm*4H, lstm stride 4H).
- *   gx    [L*B][n_lstm*4H]      w_hh  [n_lstm][4H][H]     bias [n_lstm][4H]
- *   hs, cs [n_lstm][L+1][B][H]  (index 0: the initial state, set by the caller)
- *   act   [L][n_lstm][B][4H]    (out: the activations)
- * rocBLAS is bound at run time (librocblas.so.5, the already-loaded copy when
- * there is one); VN_ERR_HIP when it cannot be loaded.
+ * The learner's matrix products on the f32 matrix cores (csrc/voxnav_gemm_f32.hip):
+ * every Linear of the PPO update (SB3 MlpExtractor / heads, RecurrentPPO.train) and
+ * the LSTM weight gradients -- no library GEMM in the learner.  Batched over `batch`
+ * with element strides s*.
+ *   vn_gemm_f32_linear  C = act(A [M][K] @ W [N][K]^T + bias)   act 0 none, 1 tanh
+ *   vn_gemm_f32_dx      C = dZ [M][K] @ W [K][N], dZ = dy (1 - y^2) (y != NULL) or dy
+ *   vn_gemm_f32_tn      C [M][N] = dZ^T B, dZ [K][M] (as above), B [K][N], K split in
+ *                       `splits` (workspace: splits*batch*M*N floats), colsum [batch][M]
+ *                       = sum_k dZ[k][m] (workspace2: splits*batch*M), accumulate: C +=
  */
-int vn_lstm_seq_fwd(const float *gx, const float *w_hh, const float *bias, float *hs, float *cs, float *act,
-                    int32_t n_lstm, int32_t L, int32_t B, int32_t H, void *stream);
-
-/*
- * The backward time loop: for t = L-1 .. 0 the backward cell step (dh_out
- * [n_lstm][L][B][H], dh_rec = dh from step t+1) into dG [n_lstm][L][B][4H],
- * then dh = dG[:, t] @ W_hh (skipped at t = 0 unless need_dh0).  dc
- * [n_lstm][B][H] must hold dL/dc_{L-1} (zeros) on entry and holds dL/dc0 on
- * return; dh [n_lstm][B][H] holds dL/dh0 on return when need_dh0.
- */
-int vn_lstm_seq_bwd(const float *dh_out, const float *w_hh, const float *act, const float *cs, float *dG, float *dc,
-                    float *dh, int32_t need_dh0, int32_t n_lstm, int32_t L, int32_t B, int32_t H, void *stream);
+int vn_gemm_f32_linear(const float *a, int64_t lda, int64_t sa, const float *w, int64_t ldw, int64_t sw,
+                       const float *bias, int64_t sbias, float *c, int64_t ldc, int64_t sc, int32_t M, int32_t N,
+                       int32_t K, int32_t batch, int32_t act, void *stream);
+int vn_gemm_f32_dx(const float *dy, const float *y, int64_t ldd, int64_t sd, const float *w, int64_t ldw, int64_t sw,
+                   float *c, int64_t ldc, int64_t sc, int32_t M, int32_t N, int32_t K, int32_t batch, void *stream);
+int vn_gemm_f32_tn(const float *dy, const float *y, int64_t ldd, int64_t sd, const float *b, int64_t ldb, int64_t sb,
+                   float *c, int64_t sc, float *colsum, int32_t M, int32_t N, int32_t K, int32_t batch, int32_t splits,
+                   float *workspace, float *workspace2, int32_t accumulate, void *stream);
 
 #ifdef __cplusplus
 }

@@ -1,0 +1,38 @@
+#!/bin/bash
+# One GPU session of named steps (STEPS=a,b,...), each under its own time
+# limit; a fault / abort / timeout ends the session (a test failure, exit 1,
+# does not).  Logs under gpurun_out/<TAG>_<step>.log.
+set -u
+cd "${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+TAG=${TAG:-s}
+run() {
+  local name=$1 t=$2; shift 2
+  [[ ",$STEPS," == *",$name,"* ]] || return 0
+  local t0=$(date +%s)
+  timeout -k 10 "$t" "$@" > "gpurun_out/${TAG}_$name.log" 2>&1
+  local rc=$?
+  echo "[$name] rc=$rc ($(( $(date +%s) - t0 )) s)"
+  tail -n 12 "gpurun_out/${TAG}_$name.log"
+  if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
+  return 0
+}
+EPROF="python3 scripts/env_prof.py --lib 3d-navigation-reinforcement-learning_amd/voxnav/_lib/variants/libvoxnav_eprof.so"
+run smoke 300 python3 -c "import __graft_entry__ as g; g.smoke()"
+run ltests 600 python3 -u -m pytest tests/test_learn_ops.py tests/test_ppo.py -m gpu -x -q --timeout 300 --timeout-method thread
+run tests 1100 python3 -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread ${PYTEST_ARGS:-}
+run eprof_p3 300 $EPROF --room P3_training --F 128 --steps 1024 --reps 1
+run eprof_p3f1 300 $EPROF --room P3_training --F 1 --steps 200 --reps 1
+run eprof_p2 300 $EPROF --room P2_training --F 128 --steps 1024 --reps 1
+run eprof_box 300 $EPROF --room 32x32x8 --F 20 --warmup 5 --reps 5
+run eprof_boxf1 300 $EPROF --room 32x32x8 --F 1 --steps 200 --reps 1
+run learn_lstm 400 rocprofv3 --kernel-trace --stats -d gpurun_out/${TAG}_learn_lstm -o trace --output-format csv -- python3 scripts/ppo_bench.py --agents 65536 --batch 65536 --minibatches 8 --policy lstm
+run learn_mlp 400 rocprofv3 --kernel-trace --stats -d gpurun_out/${TAG}_learn_mlp -o trace --output-format csv -- python3 scripts/ppo_bench.py --agents 65536 --batch 65536 --minibatches 8 --policy mlp
+run ab_p3 600 bash scripts/_ab_p3.sh
+run ab_ph 300 bash scripts/_ab_ph.sh
+run sq_p3 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_LDS SQ_WAIT_ANY SQ_WAVE_CYCLES -d gpurun_out/${TAG}_sq_p3 -o sq --output-format csv -- python3 bench.py --steps 20 --warmup 5 --cpu-seconds 0 --single-step-check 0 --collector none --simple 0 --fuse-check 0 --episode-window 0 --room-sets P3_training --room-set-steps 256
+run learn_lstm_gk16 300 env VOXNAV_LIB=3d-navigation-reinforcement-learning_amd/voxnav/_lib/variants/libvoxnav_gk16.so python3 scripts/ppo_bench.py --agents 65536 --batch 65536 --minibatches 8 --policy lstm
+run learn_mlp_gk16 300 env VOXNAV_LIB=3d-navigation-reinforcement-learning_amd/voxnav/_lib/variants/libvoxnav_gk16.so python3 scripts/ppo_bench.py --agents 65536 --batch 65536 --minibatches 8 --policy mlp
+run bench 600 python3 bench.py ${BENCH_ARGS:-}
+exit 0

@@ -290,6 +290,33 @@ def test_full_size_properties(voxnav):
         np.testing.assert_array_equal(ro.reward[:, g].cpu().numpy(), orc["reward"][:, 0])
 
 
+def test_full_size_p3_sampled_belief(voxnav):
+    """P3_training at the bench's agent count (65536, byte-mark kernel with
+    deferred plane marks), one 128-step launch: sampled agents replayed alone
+    through the oracle -- obs, f64 rewards, flags and the final belief map."""
+    src, N, L, K = "set:P3_training", 65536, 10, 128
+    env = make_env(voxnav, src, L, n=N, autoreset=True)
+    env.reset(seed=42)
+    ro = env.step_random(K, policy_seed=42, t0=0, reward_f64=True)
+    rng = np.random.default_rng(1)
+    picks = rng.choice(N, size=16, replace=False)
+    sel = torch.as_tensor(picks, device=env.device)
+    b = env.belief().index_select(0, sel).cpu().numpy().astype(np.int64)
+    st = env.export_state().cpu().numpy()
+    obs = ro.obs.index_select(1, sel).cpu().numpy()
+    rew = ro.reward.index_select(1, sel).cpu().numpy()
+    te = ro.terminated.index_select(1, sel).cpu().numpy()
+    rooms = env.room_set.rooms
+    for j, g in enumerate(picks):
+        orc_env = oracle_env(src, L, n_agents=1)
+        orc = orc_env.run_random([42 + int(g)], policy_seed=42, K=K, gid_base=int(g), seed_stride=N)
+        assert obs[:, j].tobytes() == orc["obs"][:, 0].tobytes(), g
+        np.testing.assert_array_equal(rew[:, j], orc["reward"][:, 0])
+        np.testing.assert_array_equal(te[:, j], orc["terminated"][:, 0])
+        W, D, H = rooms[int(st[g, 13])].shape
+        np.testing.assert_array_equal(b[j, :W, :D, :H], np.minimum(orc_env.belief(0), 63), err_msg=f"agent {g}")
+
+
 def test_gae_matches_oracle(voxnav):
     from oracle.oracle import gae as oracle_gae
     from voxnav.gae import compute_gae
@@ -325,19 +352,27 @@ def test_gridagent_facade_matches_golden(voxnav):
             si += 1
     ag.close()
 
-MIX_CASES = [("box:32x32x8", 10, 96), ("box:8x8x4", 4, 40), ("box:16x16x8", 7, 50)]
+MIX_CASES = [("box:32x32x8", 10, 96), ("box:8x8x4", 4, 40), ("box:16x16x8", 7, 50), ("set:P3_training", 10, 64),
+             ("box:100x40x8", 10, 48)]
+# belief modes: (VOXNAV_PCACHE, VOXNAV_DEFER)
+MIX_MODES = [("0", "1"), ("0", "0"), ("1", "1"), ("2", "1")]
 
 
-@pytest.mark.parametrize("pcache", ["0", "1", "2"])
+@pytest.mark.parametrize("pcache,defer", MIX_MODES, ids=[f"pc{a}-df{b}" for a, b in MIX_MODES])
 @pytest.mark.parametrize("src,L,N", MIX_CASES, ids=[c[0] for c in MIX_CASES])
-def test_launch_mix_belief_matches_oracle(voxnav, monkeypatch, pcache, src, L, N):
+def test_launch_mix_belief_matches_oracle(voxnav, monkeypatch, pcache, defer, src, L, N):
     """Launches of 16, 1, 5, 3 and 30 fused steps on one env in each belief
-    mode of the PH-8 kernel (VOXNAV_PCACHE: 0 byte marks, 1 plane sets in u64
-    LDS rows, 2 in u32 rows -- marks outside the window then live only in the
-    marked-bit planes and reach a column's bytes when it enters the window):
+    mode (VOXNAV_PCACHE: 0 byte marks, 1 plane sets in u64 LDS rows, 2 in u32
+    rows -- marks outside the window then live only in the marked-bit planes
+    and reach a column's bytes when it enters the window; VOXNAV_DEFER 1: in
+    byte-mark mode with plane rows of <= 2 words a sensing pass's plane marks
+    are applied at the start of the next step or at the launch's end):
     obs, f64 rewards, flags and every agent's exported belief map equal the
     oracle's after 120 steps with auto-resets."""
+    if pcache != "0" and src.startswith(("set:", "box:100")):
+        pytest.skip("plane-set modes need PH-8 rooms of <= 64 x 64")
     monkeypatch.setenv("VOXNAV_PCACHE", pcache)
+    monkeypatch.setenv("VOXNAV_DEFER", defer)
     env = make_env(voxnav, src, L, n=N, autoreset=True)
     env.reset(seed=42)
     ks = [16, 1, 5, 16, 3, 16, 16, 1, 16, 30]
