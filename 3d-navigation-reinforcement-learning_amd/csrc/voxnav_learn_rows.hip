@@ -1,0 +1,510 @@
+// voxnav_learn_rows.hip -- the PPO learner's LSTM re-run as ONE persistent
+// launch per direction, weights held in registers for the whole sequence
+// (sb3_contrib RecurrentPPO.train -> evaluate_actions -> _process_sequence,
+// reached from model.learn at train/Grid_Train.py:228).
+//
+// Row layout.  A minibatch of batch_size = R * T env-major samples (T the
+// rollout length) covers R whole env rollouts, the first and the last one
+// split at the same step s by the random roll: row r is env e0 + r over all T
+// steps, and row 0 holds env e0 + R for t < s.  A row restarts its LSTM state
+// wherever sb3 starts a sequence (t = 0, an episode start, the seam of row
+// 0): h, c := the buffer's stored state x (1 - episode_start) -- so a row is a
+// run of whole sb3 sequences laid end to end, and the outputs equal sb3's
+// padded per-sequence re-run without any padding.
+//
+// Work split: block (LSTM l, unit block ub of 32 units, row tile rt of 32
+// rows); the 8 unit blocks of one (l, rt) form a group that exchanges h each
+// step.  Every block of the grid (2 x 8 x R/32 <= 256, one per CU) is
+// resident for the whole launch (checked on the host), and the hand-off is
+// the agent-scope protocol of the HIP guide's Guideline 16 (R1, counter form):
+// the payload (h_t; in the backward the partial dh of step t-1) is written
+// with 16-B write-through (sc1) stores, every storing wave drains vmcnt, the
+// block synchronises, ONE lane adds to the group's counter (agent scope); a
+// consumer polls the counter with relaxed sc1 loads and reads the payload
+// with sc1 loads only.  Spins are bounded: a timeout sets *err and the launch
+// runs to its end (the host raises).
+//
+// forward   wave w = gate w: the 32 x 32 tile [x_t | h_{t-1}] @ W[gate w, 32
+//           units]^T on v_mfma_f32_32x32x2_f32, W (168 VGPRs) resident; the
+//           x part runs while the group's h_{t-1} is still being produced;
+//           the cell (i, f, g, o, c, h) as the epilogue, c carried in
+//           registers (a block owns its units' cells).
+// backward  per step in reverse: dh = dh_out + sum of the 8 partials of step
+//           t+1 (fixed order), the cell backward (dG_t, dc carried in
+//           registers), then this block's partial dh_{t-1} = dG_t[:, its 128
+//           gate columns] @ W_hh[those rows, 256 units] (W_hh slice resident,
+//           128 VGPRs); rows whose step t starts a sequence pass no gradient
+//           back (their h_{t-1}, c_{t-1} came from the buffer).
+// f32 throughout (the reference's dtype), accurate expf / tanhf.
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "vn_common.h"
+
+using vn_detail::fail;
+
+namespace {
+
+typedef __attribute__((ext_vector_type(16))) float f32x16_t;
+
+constexpr int RW = 32;      // rows per tile
+constexpr int UBK = 32;     // units per block
+constexpr int NUB = 8;      // unit blocks per LSTM (H = 256)
+constexpr uint32_t kSpinLimit = 1u << 22;   // ~0.3 s per wait at s_sleep 2
+
+__device__ __forceinline__ float sigm(float x) { return 1.0f / (1.0f + expf(-x)); }
+
+__device__ __forceinline__ f32x16_t zero16() {
+    f32x16_t z;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) z[r] = 0.0f;
+    return z;
+}
+
+__device__ __forceinline__ float4 f4(float a) { return make_float4(a, a, a, a); }
+__device__ __forceinline__ float4 operator+(float4 a, float4 b) { return make_float4(a.x + b.x, a.y + b.y, a.z + b.z, a.w + b.w); }
+__device__ __forceinline__ float4 operator*(float4 a, float4 b) { return make_float4(a.x * b.x, a.y * b.y, a.z * b.z, a.w * b.w); }
+
+__device__ __forceinline__ float4 as_f4(__attribute__((ext_vector_type(4))) float v) { return make_float4(v[0], v[1], v[2], v[3]); }
+
+// 16-B write-through (sc1) store / sc1 load through a buffer resource (aux 16 = sc1)
+__device__ __forceinline__ void st_sc1(__amdgpu_buffer_rsrc_t rs, uint32_t off, float4 v) {
+    __attribute__((ext_vector_type(4))) float w = {v.x, v.y, v.z, v.w};
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) uint32_t, w), rs, off,
+                                           0, 16);
+}
+__device__ __forceinline__ float4 ld_sc1(__amdgpu_buffer_rsrc_t rs, uint32_t off) {
+    const auto u = __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 16);
+    const auto v = __builtin_bit_cast(__attribute__((ext_vector_type(4))) float, u);
+    return as_f4(v);
+}
+
+// one lane: wait until *cnt >= target (relaxed agent-scope loads = sc1), bounded
+// (a timed-out launch sets *err; every later wait of every block then returns
+// at once, so the launch drains instead of timing out step after step)
+__device__ __forceinline__ bool wait_ge(uint32_t *cnt, uint32_t target, int32_t *err) {
+    uint32_t spins = 0;
+    while (__hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+        __builtin_amdgcn_s_sleep(2);
+        ++spins;
+        if ((spins & 1023u) == 0u && __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return false;
+        if (spins > kSpinLimit) {
+            __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            return false;
+        }
+    }
+    return true;
+}
+
+// after this block's payload stores: drain (every wave), block barrier, one add
+__device__ __forceinline__ void publish(uint32_t *cnt) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+struct RowsFwd {
+    const float *x;          // [L][B][D]
+    const float *w_ih;       // [2][4H][D]
+    const float *w_hh;       // [2][4H][H]
+    const float *bias;       // [2][4H]  (b_ih + b_hh)
+    const float *h_store;    // [T][2][N][H]  the rollout buffer's LSTM states
+    const float *c_store;
+    const int32_t *env;      // [L][B]  the row's env at each step
+    const uint8_t *start;    // [L][B]  1: a sequence starts at this step
+    const float *keep;       // [L][B]  1 - episode_start of that sample
+    float *hout;             // [2][L][B][H]  h_t (the handed-off payload)
+    float *hprev;            // [2][L][B][H]  the h_{t-1} each step used
+    float *cprev, *cnew;     // [2][L][B][H]
+    float *act;              // [2][L][B][4H] i, f, g, o
+    uint32_t *cnt;           // [2 * NT] group counters (zeroed per call)
+    int32_t *err;
+    int64_t n_env;
+    int L, B, NT;
+};
+
+template <int D, int H>
+__global__ __launch_bounds__(256, 1) void lstm_rows_fwd_kernel(RowsFwd a) {
+    constexpr int NCX = D / 8, NCH = H / 8, NC = NCX + NCH;
+    constexpr int XP = D + 4, HP = H + 4, GP = 36;
+    static_assert(D % 8 == 0 && H == NUB * UBK, "shape");
+    __shared__ __attribute__((aligned(16))) float xs[2][RW][XP];
+    __shared__ __attribute__((aligned(16))) float hsl[RW][HP];
+    __shared__ __attribute__((aligned(16))) float gts[4][RW][GP];
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);   // this wave's gate
+    const int hh = lane >> 5, cl = lane & 31;
+    const int G = 2 * a.NT;
+    const int ub = (int)blockIdx.x / G, g = (int)blockIdx.x - ub * G;   // blocks of a group: equal index mod 8 when G % 8 == 0
+    const int l = g / a.NT, rt = g - l * a.NT;
+    const int row0 = rt * RW, u0 = ub * UBK;
+    const int B = a.B, L = a.L;
+
+    // resident weights: B operand of gate wv, unit u0 + cl, k = 8 ch + 4 hh + j
+    float4 wr[NC];
+    {
+        const float *wi = a.w_ih + ((size_t)l * 4 * H + (size_t)wv * H + u0 + cl) * D;
+        const float *wh = a.w_hh + ((size_t)l * 4 * H + (size_t)wv * H + u0 + cl) * H;
+#pragma unroll
+        for (int ch = 0; ch < NC; ++ch) {
+            const int k = 8 * ch + 4 * hh;
+            wr[ch] = ch < NCX ? *reinterpret_cast<const float4 *>(wi + k)
+                              : *reinterpret_cast<const float4 *>(wh + (k - D));
+        }
+    }
+    // epilogue mapping: row er of the tile, units u0 + 4 eq .. + 3
+    const int er = tid >> 3, eq = tid & 7;
+    const int erow = row0 + er;
+    const bool elive = erow < B;
+    const int eu = u0 + 4 * eq;
+    float4 bs[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) bs[q] = *reinterpret_cast<const float4 *>(a.bias + (size_t)l * 4 * H + q * H + eu);
+    float4 cc = f4(0.0f);
+
+    const __amdgpu_buffer_rsrc_t hrs =
+        __builtin_amdgcn_make_buffer_rsrc(a.hout, 0, (int)((size_t)2 * L * B * H * 4), 0x00020000);
+    uint32_t *cnt = a.cnt + g;
+
+    // x rows of a step: RW x D floats, float4 f -> (row f / (D/4), col 4 (f % (D/4)))
+    constexpr int XF = RW * D / 4, XPT = (XF + 255) / 256;
+    auto load_x = [&](int t, float4 *r) {
+#pragma unroll
+        for (int i = 0; i < XPT; ++i) {
+            const int f = tid + 256 * i;
+            const int rr = f / (D / 4), c4 = f - rr * (D / 4);
+            r[i] = (f < XF && row0 + rr < B)
+                       ? *reinterpret_cast<const float4 *>(a.x + ((size_t)t * B + row0 + rr) * D + 4 * c4)
+                       : f4(0.0f);
+        }
+    };
+    auto store_x = [&](int buf, const float4 *r) {
+#pragma unroll
+        for (int i = 0; i < XPT; ++i) {
+            const int f = tid + 256 * i;
+            const int rr = f / (D / 4), c4 = f - rr * (D / 4);
+            if (f < XF) *reinterpret_cast<float4 *>(&xs[buf][rr][4 * c4]) = r[i];
+        }
+    };
+    {
+        float4 r[XPT];
+        load_x(0, r);
+        store_x(0, r);
+    }
+    __syncthreads();
+
+    for (int t = 0; t < L; ++t) {
+        const int xb = t & 1;
+        float4 xn[XPT];
+        if (t + 1 < L) load_x(t + 1, xn);
+        // the x part of the product (needs nothing from the group)
+        f32x16_t acc = zero16();
+#pragma unroll
+        for (int ch = 0; ch < NCX; ++ch) {
+            const float4 av = *reinterpret_cast<const float4 *>(&xs[xb][cl][8 * ch + 4 * hh]);
+            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av.x, wr[ch].x, acc, 0, 0, 0);
+            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av.y, wr[ch].y, acc, 0, 0, 0);
+            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av.z, wr[ch].z, acc, 0, 0, 0);
+            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av.w, wr[ch].w, acc, 0, 0, 0);
+        }
+        // h_{t-1} of the tile's rows: the group's output of step t-1 (sc1 loads
+        // after the counter shows all 8 blocks done), or the stored state at a
+        // sequence start
+        if (t > 0) {
+            if (tid == 0) wait_ge(cnt, (uint32_t)(NUB * t), a.err);
+            __syncthreads();
+        }
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            const int f = tid + 256 * i;
+            const int rr = f >> 6, c4 = f & 63;          // H / 4 = 64 float4 per row
+            const int row = row0 + rr;
+            float4 v = f4(0.0f);
+            if (row < B) {
+                const size_t o = (size_t)t * B + row;
+                if (t == 0 || a.start[o]) {
+                    const float k = a.keep[o];
+                    const float4 s = *reinterpret_cast<const float4 *>(
+                        a.h_store + (((size_t)t * 2 + l) * a.n_env + a.env[o]) * H + 4 * c4);
+                    v = s * f4(k);
+                } else {
+                    v = ld_sc1(hrs, (uint32_t)((((size_t)l * L + (t - 1)) * B + row) * H + 4 * c4) * 4u);
+                }
+            }
+            *reinterpret_cast<float4 *>(&hsl[rr][4 * c4]) = v;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int ch = 0; ch < NCH; ++ch) {
+            const float4 av = *reinterpret_cast<const float4 *>(&hsl[cl][8 * ch + 4 * hh]);
+            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av.x, wr[NCX + ch].x, acc, 0, 0, 0);
+            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av.y, wr[NCX + ch].y, acc, 0, 0, 0);
+            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av.z, wr[NCX + ch].z, acc, 0, 0, 0);
+            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av.w, wr[NCX + ch].w, acc, 0, 0, 0);
+        }
+        if (t + 1 < L) store_x(xb ^ 1, xn);
+        // gate tile -> LDS: register v = row 8 (v / 4) + 4 hh + v % 4, unit cl
+#pragma unroll
+        for (int v = 0; v < 16; ++v) gts[wv][8 * (v >> 2) + 4 * hh + (v & 3)][cl] = acc[v];
+        __syncthreads();
+        if (elive) {
+            const size_t o = (size_t)t * B + erow;
+            float4 pre[4];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) pre[q] = *reinterpret_cast<const float4 *>(&gts[q][er][4 * eq]) + bs[q];
+            float4 cp = cc;
+            if (t == 0 || a.start[o]) {
+                const float k = a.keep[o];
+                cp = *reinterpret_cast<const float4 *>(a.c_store + (((size_t)t * 2 + l) * a.n_env + a.env[o]) * H + eu) *
+                     f4(k);
+            }
+            float4 ig, fg, gg, og, cn, hn;
+#define VN_CELL(c)                                 \
+    ig.c = sigm(pre[0].c);                         \
+    fg.c = sigm(pre[1].c);                         \
+    gg.c = tanhf(pre[2].c);                        \
+    og.c = sigm(pre[3].c);                         \
+    {                                              \
+        const float fc_ = fg.c * cp.c, ig_ = ig.c * gg.c; \
+        cn.c = fc_ + ig_;                          \
+    }                                              \
+    hn.c = og.c * tanhf(cn.c);
+            VN_CELL(x) VN_CELL(y) VN_CELL(z) VN_CELL(w)
+#undef VN_CELL
+            cc = cn;
+            const size_t so = (((size_t)l * L + t) * B + erow) * H + eu;
+            st_sc1(hrs, (uint32_t)(so * 4u), hn);          // the payload first
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            *reinterpret_cast<float4 *>(a.cnew + so) = cn;
+            *reinterpret_cast<float4 *>(a.cprev + so) = cp;
+            *reinterpret_cast<float4 *>(a.hprev + so) = *reinterpret_cast<const float4 *>(&hsl[er][eu]);
+            float *pa = a.act + (((size_t)l * L + t) * B + erow) * 4 * H + eu;
+            *reinterpret_cast<float4 *>(pa) = ig;
+            *reinterpret_cast<float4 *>(pa + H) = fg;
+            *reinterpret_cast<float4 *>(pa + 2 * H) = gg;
+            *reinterpret_cast<float4 *>(pa + 3 * H) = og;
+        }
+        // h_t published (the payload stores were drained above; the barrier
+        // inside publish orders every wave's drain before the one add)
+        __syncthreads();
+        if (tid == 0) __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+}
+
+struct RowsBwd {
+    const float *dh_out;     // [2][L][B][H]
+    const float *w_hh;       // [2][4H][H]
+    const float *act;        // [2][L][B][4H]
+    const float *cprev, *cnew;
+    const uint8_t *start;    // [L][B]
+    float *dG;               // [2][L][B][4H] out
+    float *part;             // [2 slots][2][NT][NUB][RW][H] partial dh
+    uint32_t *cnt;           // [2 * NT]
+    int32_t *err;
+    int L, B, NT;
+};
+
+template <int H>
+__global__ __launch_bounds__(256, 1) void lstm_rows_bwd_kernel(RowsBwd a) {
+    constexpr int GC = 4 * UBK;   // this block's gate columns (K of the partial product)
+    constexpr int NCK = GC / 8;   // 16 chunks
+    constexpr int DP = GC + 4, PP = H + 4;
+    static_assert(H == NUB * UBK, "shape");
+    __shared__ __attribute__((aligned(16))) float dgs[RW][DP];
+    __shared__ __attribute__((aligned(16))) float pst[RW][PP];
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);   // output units 64 wv .. + 63
+    const int hh = lane >> 5, cl = lane & 31;
+    const int G = 2 * a.NT;
+    const int ub = (int)blockIdx.x / G, g = (int)blockIdx.x - ub * G;
+    const int l = g / a.NT, rt = g - l * a.NT;
+    const int row0 = rt * RW, u0 = ub * UBK;
+    const int B = a.B, L = a.L;
+
+    // resident W_hh slice: B operand [k = gate * 32 + unit32][n = 64 wv + 32 j + cl],
+    // k = 8 ch + 4 hh + jj
+    float4 wb[2][NCK];
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int ch = 0; ch < NCK; ++ch) {
+            float v[4];
+#pragma unroll
+            for (int jj = 0; jj < 4; ++jj) {
+                const int k = 8 * ch + 4 * hh + jj;
+                const int grow = (k >> 5) * H + u0 + (k & 31);
+                v[jj] = a.w_hh[((size_t)l * 4 * H + grow) * H + 64 * wv + 32 * j + cl];
+            }
+            wb[j][ch] = make_float4(v[0], v[1], v[2], v[3]);
+        }
+    const int er = tid >> 3, eq = tid & 7;
+    const int erow = row0 + er;
+    const bool elive = erow < B;
+    const int eu = u0 + 4 * eq;
+    float4 dc = f4(0.0f);
+    const size_t slot_f = (size_t)2 * a.NT * NUB * RW * H;     // floats per slot
+    const __amdgpu_buffer_rsrc_t prs =
+        __builtin_amdgcn_make_buffer_rsrc(a.part, 0, (int)(2 * slot_f * 4), 0x00020000);
+    uint32_t *cnt = a.cnt + g;
+    auto pofs = [&](int slot, int ubb, int row, int unit) -> uint32_t {   // byte offset in part
+        return (uint32_t)(((size_t)slot * slot_f + ((((size_t)l * a.NT + rt) * NUB + ubb) * RW + row) * H + unit) * 4u);
+    };
+
+    for (int s = 0; s < L; ++s) {
+        const int t = L - 1 - s;
+        if (s > 0) {
+            if (tid == 0) wait_ge(cnt, (uint32_t)(NUB * s), a.err);
+            __syncthreads();
+        }
+        float4 dG4[4] = {f4(0.0f), f4(0.0f), f4(0.0f), f4(0.0f)};
+        bool st = true;
+        if (elive) {
+            const size_t o = (size_t)t * B + erow;
+            st = t == 0 || a.start[o];
+            float4 dhr = f4(0.0f);
+            if (s > 0) {
+                // the 8 partials of step t+1 (sc1 loads), summed in unit-block order
+#pragma unroll
+                for (int k = 0; k < NUB; ++k) dhr = dhr + ld_sc1(prs, pofs((t + 1) & 1, k, er, eu));
+            }
+            const size_t so = (((size_t)l * L + t) * B + erow) * H + eu;
+            const float4 dh = *reinterpret_cast<const float4 *>(a.dh_out + so) + dhr;
+            const float *pa = a.act + (((size_t)l * L + t) * B + erow) * 4 * H + eu;
+            const float4 ig = *reinterpret_cast<const float4 *>(pa), fg = *reinterpret_cast<const float4 *>(pa + H);
+            const float4 gg = *reinterpret_cast<const float4 *>(pa + 2 * H);
+            const float4 og = *reinterpret_cast<const float4 *>(pa + 3 * H);
+            const float4 cp = *reinterpret_cast<const float4 *>(a.cprev + so);
+            const float4 cn = *reinterpret_cast<const float4 *>(a.cnew + so);
+#define VN_CELLB(c)                                                   \
+    {                                                                 \
+        const float tc = tanhf(cn.c);                                 \
+        const float dtc = dh.c * og.c;                                \
+        const float dcc = dc.c + dtc * (1.0f - tc * tc);              \
+        dG4[0].c = dcc * gg.c * (ig.c * (1.0f - ig.c));               \
+        dG4[1].c = dcc * cp.c * (fg.c * (1.0f - fg.c));               \
+        dG4[2].c = dcc * ig.c * (1.0f - gg.c * gg.c);                 \
+        dG4[3].c = dh.c * tc * (og.c * (1.0f - og.c));                \
+        dc.c = dcc * fg.c;                                            \
+    }
+            VN_CELLB(x) VN_CELLB(y) VN_CELLB(z) VN_CELLB(w)
+#undef VN_CELLB
+            if (st) dc = f4(0.0f);   // c_{t-1} of this row came from the buffer
+            float *pg = a.dG + (((size_t)l * L + t) * B + erow) * 4 * H + eu;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) *reinterpret_cast<float4 *>(pg + q * H) = dG4[q];
+        }
+        if (t == 0) break;                      // no dh_{-1}
+        // A operand of the partial product: dG rows, zero where the step starts a sequence
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+            *reinterpret_cast<float4 *>(&dgs[er][q * UBK + 4 * eq]) = st ? f4(0.0f) : dG4[q];
+        __syncthreads();
+        f32x16_t acc0 = zero16(), acc1 = zero16();
+#pragma unroll
+        for (int ch = 0; ch < NCK; ++ch) {
+            const float4 av = *reinterpret_cast<const float4 *>(&dgs[cl][8 * ch + 4 * hh]);
+            acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(av.x, wb[0][ch].x, acc0, 0, 0, 0);
+            acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(av.x, wb[1][ch].x, acc1, 0, 0, 0);
+            acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(av.y, wb[0][ch].y, acc0, 0, 0, 0);
+            acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(av.y, wb[1][ch].y, acc1, 0, 0, 0);
+            acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(av.z, wb[0][ch].z, acc0, 0, 0, 0);
+            acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(av.z, wb[1][ch].z, acc1, 0, 0, 0);
+            acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(av.w, wb[0][ch].w, acc0, 0, 0, 0);
+            acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(av.w, wb[1][ch].w, acc1, 0, 0, 0);
+        }
+#pragma unroll
+        for (int v = 0; v < 16; ++v) {
+            const int r = 8 * (v >> 2) + 4 * hh + (v & 3);
+            pst[r][64 * wv + cl] = acc0[v];
+            pst[r][64 * wv + 32 + cl] = acc1[v];
+        }
+        __syncthreads();
+        // the partial [RW][H] of this block: 16-B sc1 stores, then publish
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            const int f = tid + 256 * i;
+            const int rr = f >> 6, c4 = f & 63;
+            st_sc1(prs, pofs(t & 1, ub, rr, 4 * c4), *reinterpret_cast<const float4 *>(&pst[rr][4 * c4]));
+        }
+        publish(cnt);
+    }
+}
+
+int rows_supported(int D, int H) { return D == 80 && H == 256; }
+
+int rows_grid_ok(int B, int NT, int *grid) {
+    *grid = 2 * NUB * NT;
+    if (B < 1 || NT < 1 || B > NT * RW) return 0;
+    int dev = 0, ncu = 0, per_fwd = 0, per_bwd = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return 0;
+    if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_fwd, lstm_rows_fwd_kernel<80, 256>, 256, 0) != hipSuccess)
+        return 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_bwd, lstm_rows_bwd_kernel<256>, 256, 0) != hipSuccess)
+        return 0;
+    const int cap = ncu * (per_fwd < per_bwd ? per_fwd : per_bwd);
+    return *grid <= cap;
+}
+
+}  // namespace
+
+extern "C" {
+
+int vn_lstm_rows_supported(int32_t D, int32_t H, int32_t B) {
+    if (!rows_supported(D, H)) return 0;
+    int grid = 0;
+    return rows_grid_ok(B, (B + RW - 1) / RW, &grid);
+}
+
+int vn_lstm_rows_part_floats(int32_t B, int64_t *floats) {
+    if (!floats || B < 1) return fail(VN_ERR_INVALID, "bad argument");
+    const int NT = (B + RW - 1) / RW;
+    *floats = (int64_t)2 * 2 * NT * NUB * RW * 256;
+    return VN_OK;
+}
+
+int vn_lstm_rows_fwd(const float *x, int32_t D, const float *w_ih, const float *w_hh, const float *bias,
+                     const float *h_store, const float *c_store, int64_t n_env, const int32_t *env,
+                     const uint8_t *start, const float *keep, float *hout, float *hprev, float *cprev, float *cnew,
+                     float *act, uint32_t *cnt, int32_t *err, int32_t L, int32_t B, int32_t H, void *stream) {
+    if (!x || !w_ih || !w_hh || !bias || !h_store || !c_store || !env || !start || !keep || !hout || !hprev ||
+        !cprev || !cnew || !act || !cnt || !err)
+        return fail(VN_ERR_INVALID, "NULL argument");
+    if (!rows_supported(D, H)) return fail(VN_ERR_INVALID, "row-layout LSTM: D 80 and H 256 only (got %d, %d)", D, H);
+    if (L < 1) return fail(VN_ERR_INVALID, "L < 1");
+    const int NT = (B + RW - 1) / RW;
+    int grid = 0;
+    if (!rows_grid_ok(B, NT, &grid))
+        return fail(VN_ERR_INVALID, "row-layout LSTM: %d blocks are not co-resident (B = %d)", grid, B);
+    if ((size_t)2 * L * B * H * 4 >= (1ull << 31)) return fail(VN_ERR_INVALID, "row-layout LSTM: hout over 2 GB");
+    const hipStream_t st = (hipStream_t)stream;
+    VN_HIP(hipMemsetAsync(cnt, 0, (size_t)2 * NT * sizeof(uint32_t), st));
+    RowsFwd a{x, w_ih, w_hh, bias, h_store, c_store, env, start, keep, hout, hprev, cprev, cnew, act, cnt, err,
+              n_env, L, B, NT};
+    hipLaunchKernelGGL((lstm_rows_fwd_kernel<80, 256>), dim3((unsigned)grid), dim3(256), 0, st, a);
+    VN_HIP(hipGetLastError());
+    return VN_OK;
+}
+
+int vn_lstm_rows_bwd(const float *dh_out, const float *w_hh, const float *act, const float *cprev, const float *cnew,
+                     const uint8_t *start, float *dG, float *part, uint32_t *cnt, int32_t *err, int32_t L, int32_t B,
+                     int32_t H, void *stream) {
+    if (!dh_out || !w_hh || !act || !cprev || !cnew || !start || !dG || !part || !cnt || !err)
+        return fail(VN_ERR_INVALID, "NULL argument");
+    if (!rows_supported(80, H)) return fail(VN_ERR_INVALID, "row-layout LSTM: H 256 only (got %d)", H);
+    if (L < 1) return fail(VN_ERR_INVALID, "L < 1");
+    const int NT = (B + RW - 1) / RW;
+    int grid = 0;
+    if (!rows_grid_ok(B, NT, &grid))
+        return fail(VN_ERR_INVALID, "row-layout LSTM: %d blocks are not co-resident (B = %d)", grid, B);
+    const hipStream_t st = (hipStream_t)stream;
+    VN_HIP(hipMemsetAsync(cnt, 0, (size_t)2 * NT * sizeof(uint32_t), st));
+    RowsBwd a{dh_out, w_hh, act, cprev, cnew, start, dG, part, cnt, err, L, B, NT};
+    hipLaunchKernelGGL((lstm_rows_bwd_kernel<256>), dim3((unsigned)grid), dim3(256), 0, st, a);
+    VN_HIP(hipGetLastError());
+    return VN_OK;
+}
+
+}  // extern "C"

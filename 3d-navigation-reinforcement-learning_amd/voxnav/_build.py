@@ -20,7 +20,7 @@ INCLUDE = REPO / "include"
 LIBDIR = PKG / "_lib"
 LIB = LIBDIR / "libvoxnav.so"
 SOURCES = [CSRC / "voxnav_env.hip", CSRC / "voxnav_simple.hip", CSRC / "voxnav_collect.hip",
-           CSRC / "voxnav_learn_f32.hip", CSRC / "voxnav_gemm_f32.hip",
+           CSRC / "voxnav_learn_f32.hip", CSRC / "voxnav_learn_rows.hip", CSRC / "voxnav_gemm_f32.hip",
            CSRC / "voxnav_policy_f32.hip"]
 HEADERS = [INCLUDE / "voxnav.h", CSRC / "vn_common.h", CSRC / "env_core.h"]
 ARCH = os.environ.get("VOXNAV_ARCH", "gfx950")

@@ -123,6 +123,101 @@ class _DualLSTM(torch.autograd.Function):
                 db[1].clone(), db[1].clone())
 
 
+class _DualLSTMRows(torch.autograd.Function):
+    """Actor and critic LSTM over the row layout (csrc/voxnav_learn_rows.hip):
+    x [L, B, D]; a row restarts from the stored state (h_store / c_store
+    [T, 2, N, H] at (t, env[t, r])) times keep[t, r] wherever start[t, r]."""
+
+    @staticmethod
+    def forward(ctx, x, env, start, keep, h_store, c_store, w_ih_a, w_hh_a, b_ih_a, b_hh_a, w_ih_c, w_hh_c, b_ih_c,
+                b_hh_c):
+        lib = _native.load()
+        L, B, D = x.shape
+        H = w_hh_a.shape[1]
+        G = 4 * H
+        dev = x.device
+        st = _stream(dev)
+        xc = x.contiguous()
+        w_ih = torch.stack([w_ih_a, w_ih_c]).contiguous()
+        w_hh = torch.stack([w_hh_a, w_hh_c]).contiguous()
+        bias = torch.stack([b_ih_a + b_hh_a, b_ih_c + b_hh_c]).contiguous()
+        nt = -(-B // 32)
+        hout = torch.empty((2, L, B, H), dtype=torch.float32, device=dev)
+        hprev, cprev, cnew = torch.empty_like(hout), torch.empty_like(hout), torch.empty_like(hout)
+        act = torch.empty((2, L, B, G), dtype=torch.float32, device=dev)
+        cnt = torch.empty(2 * nt, dtype=torch.int32, device=dev)
+        err = _rows_err(dev)
+        _native.check(lib.vn_lstm_rows_fwd(_p(xc), D, _p(w_ih), _p(w_hh), _p(bias), _p(h_store), _p(c_store),
+                                           h_store.shape[2], _p(env), _p(start), _p(keep), _p(hout), _p(hprev),
+                                           _p(cprev), _p(cnew), _p(act), _p(cnt), _p(err), L, B, H, st),
+                      "vn_lstm_rows_fwd")
+        ctx.save_for_backward(xc, w_hh, start, hprev, cprev, cnew, act, w_ih_a, w_ih_c)
+        ctx.dims = (L, B, D, H)
+        return hout
+
+    @staticmethod
+    def backward(ctx, d_out):
+        lib = _native.load()
+        xc, w_hh, start, hprev, cprev, cnew, act, w_ih_a, w_ih_c = ctx.saved_tensors
+        L, B, D, H = ctx.dims
+        G = 4 * H
+        dev = xc.device
+        st = _stream(dev)
+        dh_out = d_out.contiguous()
+        dG = torch.empty((2, L, B, G), dtype=torch.float32, device=dev)
+        nf = C.c_int64()
+        _native.check(lib.vn_lstm_rows_part_floats(B, C.byref(nf)), "vn_lstm_rows_part_floats")
+        part = torch.empty(nf.value, dtype=torch.float32, device=dev)
+        cnt = torch.empty(2 * -(-B // 32), dtype=torch.int32, device=dev)
+        _native.check(lib.vn_lstm_rows_bwd(_p(dh_out), _p(w_hh), _p(act), _p(cprev), _p(cnew), _p(start), _p(dG),
+                                           _p(part), _p(cnt), _p(_rows_err(dev)), L, B, H, st), "vn_lstm_rows_bwd")
+        dGf = dG.view(2, L * B, G)
+        d_w_hh, _ = learn_ops.mm_tn(dGf, hprev.view(2, L * B, H))
+        d_w_ih, db = learn_ops.mm_tn(dGf, xc.view(1, L * B, D).expand(2, L * B, D), colsum=True)
+        dx = None
+        if ctx.needs_input_grad[0]:
+            dx = (dGf[0] @ w_ih_a + dGf[1] @ w_ih_c).view(L, B, D)
+        return (dx, None, None, None, None, None, d_w_ih[0], d_w_hh[0], db[0].clone(), db[0].clone(), d_w_ih[1],
+                d_w_hh[1], db[1].clone(), db[1].clone())
+
+
+_ERR = {}
+
+
+def _rows_err(dev) -> torch.Tensor:
+    """The row kernels' device error word (1: an in-launch hand-off timed out)."""
+    key = str(dev)
+    if key not in _ERR:
+        _ERR[key] = torch.zeros(1, dtype=torch.int32, device=dev)
+    return _ERR[key]
+
+
+def rows_check(dev) -> None:
+    """Raise if a row-layout launch on `dev` timed out (one host read)."""
+    e = _ERR.get(str(dev))
+    if e is not None and int(e.item()) != 0:
+        e.zero_()
+        raise _native.VoxnavError("row-layout LSTM: an in-launch hand-off timed out (blocks not co-resident?)")
+
+
+def rows_supported(policy, D: int, B: int) -> bool:
+    """Whether the row-layout kernels take this policy / minibatch on this device."""
+    la, lc = policy.lstm_actor, policy.lstm_critic
+    if la.num_layers != 1 or lc.num_layers != 1 or la.bidirectional or lc.bidirectional or not la.bias:
+        return False
+    return bool(_native.load().vn_lstm_rows_supported(D, la.hidden_size, B))
+
+
+def dual_lstm_rows(policy, x: torch.Tensor, env: torch.Tensor, start: torch.Tensor, keep: torch.Tensor,
+                   h_store: torch.Tensor, c_store: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
+    """(out_actor, out_critic), each [L, B, H], of ``policy.lstm_actor`` /
+    ``lstm_critic`` over the row layout (see ``_DualLSTMRows``)."""
+    la, lc = policy.lstm_actor, policy.lstm_critic
+    out = _DualLSTMRows.apply(x, env, start, keep, h_store, c_store, la.weight_ih_l0, la.weight_hh_l0, la.bias_ih_l0,
+                              la.bias_hh_l0, lc.weight_ih_l0, lc.weight_hh_l0, lc.bias_ih_l0, lc.bias_hh_l0)
+    return out[0], out[1]
+
+
 def dual_lstm(policy, x: torch.Tensor, h0: torch.Tensor, c0: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
     """(out_actor, out_critic), each [L, B, H], of ``policy.lstm_actor`` and
     ``policy.lstm_critic`` over x [L, B, D] from states h0, c0 [2, B, H]

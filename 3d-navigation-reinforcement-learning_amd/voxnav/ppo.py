@@ -37,6 +37,7 @@ The minibatch order is drawn from ``numpy.random.default_rng(seed)``
 """
 from __future__ import annotations
 
+import os
 from contextlib import nullcontext as _nullctx
 from typing import Dict, List, Optional, Sequence
 
@@ -44,7 +45,7 @@ import numpy as np
 import torch
 import torch.nn.functional as Fn
 
-from . import learn_ops
+from . import learn_ops, lstm_seq
 from .lstm_seq import dual_lstm
 from .policy import ActorCriticPolicy, RecurrentActorCriticPolicy
 
@@ -120,11 +121,43 @@ class PPOLearner:
                 self._side = torch.cuda.Stream(dev)
             side = self._side
             side.wait_stream(torch.cuda.current_stream(dev))
+        n = idx.numel()
+        rows = n // T if (dev.type == "cuda" and n % T == 0 and n // T <= N) else 0
+        if rows and not self._rows_ok(buf.obs.shape[-1], rows):
+            rows = 0
         with torch.cuda.stream(side) if side is not None else _nullctx():
             env = idx // T
             t = idx - env * T
             src = t * N + env                                         # row in the [T, N]-major buffers
             es = buf.episode_starts.reshape(-1)[src]
+            if rows:
+                # row layout (csrc/voxnav_learn_rows.hip): row r = env e0 + r over all T
+                # steps; the last env of a minibatch that starts mid-rollout (steps
+                # t < t0) shares row 0 with the first (steps >= t0)
+                r = torch.remainder(env - env[0], N)
+                r = torch.where(r == rows, torch.zeros_like(r), r)
+                pos = t * rows + r
+                t0 = t[0]
+                st = (t == 0) | (es > 0.5) | ((r == 0) & (t == t0) & (t0 > 0))
+                src_rows = torch.empty_like(src)
+                src_rows[pos] = src
+                grid = dict(src=src_rows,
+                            env=torch.empty(n, dtype=torch.int32, device=dev).index_put_((pos,), env.to(torch.int32)),
+                            start=torch.empty(n, dtype=torch.uint8, device=dev).index_put_((pos,), st.to(torch.uint8)),
+                            keep=torch.empty(n, dtype=torch.float32, device=dev).index_put_((pos,), 1.0 - es))
+                pk = dict(idx=idx, rows=rows, **grid)
+                if side is not None:
+                    ev = torch.cuda.Event()
+                    ev.record(side)
+                    pk["ev"] = ev
+        if rows:
+            if side is not None:
+                main = torch.cuda.current_stream(dev)
+                for v in pk.values():
+                    if isinstance(v, torch.Tensor) and v.is_cuda:
+                        v.record_stream(main)
+            return pk
+        with torch.cuda.stream(side) if side is not None else _nullctx():
             seq_start = (es > 0.5) | (t == 0)                         # episode start or env change
             seq_start[0] = True
             seq_id = torch.cumsum(seq_start.to(torch.int64), 0) - 1
@@ -148,9 +181,36 @@ class PPOLearner:
                     v.record_stream(main)            # made on the side stream, used on the main one
         return pk
 
+    def _rows_ok(self, D: int, rows: int) -> bool:
+        """The row-layout LSTM kernels take (D, rows) for this policy (cached host query)."""
+        cache = self.__dict__.setdefault("_rows_cache", {})
+        key = (D, rows)
+        if key not in cache:
+            # VOXNAV_LSTM_ROWS=0: the per-sequence packed path (A/B knob)
+            cache[key] = os.environ.get("VOXNAV_LSTM_ROWS", "1") != "0" and lstm_seq.rows_supported(self.policy, D, rows)
+        return cache[key]
+
+    def _evaluate_rows(self, buf, pk: dict):
+        """evaluate_actions in the row layout: both LSTMs over [T, rows] in one
+        persistent launch each (no host read, no padding)."""
+        T, N = buf.actions.shape
+        rows = pk["rows"]
+        if "ev" in pk:
+            torch.cuda.current_stream(pk["idx"].device).wait_event(pk["ev"])
+        src = pk["src"]
+        D = buf.obs.shape[-1]
+        x = buf.obs.reshape(T * N, D)[src].view(T, rows, D)
+        out_pi, out_vf = lstm_seq.dual_lstm_rows(self.policy, x, pk["env"], pk["start"], pk["keep"], buf.lstm_h,
+                                                 buf.lstm_c)
+        H = out_pi.shape[-1]
+        acts = buf.actions.reshape(-1)[src].long()
+        return self._heads(out_pi.reshape(T * rows, H), out_vf.reshape(T * rows, H), acts), src
+
     def _evaluate_recurrent(self, buf, pk: dict):
         """evaluate_actions on a packed minibatch (``_pack_begin``)."""
         T, N = buf.actions.shape
+        if "rows" in pk:
+            return self._evaluate_rows(buf, pk)
         if "ev" in pk:
             pk["ev"].synchronize()                                # the minibatch's size only
             torch.cuda.current_stream(pk["idx"].device).wait_event(pk["ev"])
@@ -231,6 +291,8 @@ class PPOLearner:
             if self.recurrent and i + 1 < len(idxs):
                 nxt = self._pack_begin(buf, idxs[i + 1])
             logs.append(self.update(buf, idx, packed=cur))
+        if self.recurrent and idxs[0].is_cuda:
+            lstm_seq.rows_check(idxs[0].device)      # a timed-out row-layout launch raises
         return torch.stack(logs)
 
     # ------------------------------------------------------------ train

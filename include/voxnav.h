@@ -416,6 +416,33 @@ int vn_lstm_seq_bwd_mfma(const float *dh_out, const float *w_hh, float *wpack, c
                          void *stream);
 
 /*
+ * The learner's LSTM re-run in the row layout (csrc/voxnav_learn_rows.hip; same
+ * sb3_contrib RecurrentPPO.train re-run as above, train/Grid_Train.py:228): a
+ * minibatch of R whole env rollouts as B = R rows over all L = T steps, a row's
+ * state restarted from the buffer at every sequence start; ONE persistent launch
+ * per direction with the weights resident in registers and the 8 unit blocks of
+ * each (LSTM, 32-row tile) exchanging h (forward) / partial dh (backward) through
+ * an in-launch agent-scope hand-off.  D 80, H 256, both LSTMs (actor, critic).
+ *   x [L][B][D]; h_store, c_store [T][2][n_env][H] (the rollout buffer's states);
+ *   env [L][B] int32 (the row's env), start [L][B] u8 (1: a sequence starts),
+ *   keep [L][B] (1 - episode_start); out: hout, hprev (the h_{t-1} used), cprev,
+ *   cnew [2][L][B][H], act [2][L][B][4H] (i, f, g, o); cnt: 2 * ceil(B / 32) u32
+ *   counters (zeroed by the call); err: set to 1 if a hand-off timed out.
+ * Backward: dh_out [2][L][B][H] -> dG [2][L][B][4H]; part: vn_lstm_rows_part_floats
+ * floats of workspace.  vn_lstm_rows_supported: 1 when (D, H, B) can run (every
+ * block co-resident on this device), else 0 (use vn_lstm_seq_*).
+ */
+int vn_lstm_rows_supported(int32_t D, int32_t H, int32_t B);
+int vn_lstm_rows_part_floats(int32_t B, int64_t *floats);
+int vn_lstm_rows_fwd(const float *x, int32_t D, const float *w_ih, const float *w_hh, const float *bias,
+                     const float *h_store, const float *c_store, int64_t n_env, const int32_t *env,
+                     const uint8_t *start, const float *keep, float *hout, float *hprev, float *cprev, float *cnew,
+                     float *act, uint32_t *cnt, int32_t *err, int32_t L, int32_t B, int32_t H, void *stream);
+int vn_lstm_rows_bwd(const float *dh_out, const float *w_hh, const float *act, const float *cprev, const float *cnew,
+                     const uint8_t *start, float *dG, float *part, uint32_t *cnt, int32_t *err, int32_t L, int32_t B,
+                     int32_t H, void *stream);
+
+/*
  * The learner's matrix products on the f32 matrix cores (csrc/voxnav_gemm_f32.hip):
  * every Linear of the PPO update (SB3 MlpExtractor / heads, RecurrentPPO.train) and
  * the LSTM weight gradients -- no library GEMM in the learner.  Batched over `batch`

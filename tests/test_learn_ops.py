@@ -122,3 +122,65 @@ def test_dual_lstm_matches_torch(D, H, L, B):
     ref = [p.grad for p in params] + [h0.grad, c0.grad]
     for g, r in zip(got, ref):
         _close(g, r, rel=1e-4)
+
+
+def _rows_reference(x, env, start, keep, hs, cs, lstm, l):
+    """float64 restatement of one LSTM over the row layout: at a sequence start
+    the state is the buffer's stored state x keep, else the row's previous."""
+    L, B, _ = x.shape
+    w_ih, w_hh = lstm.weight_ih_l0.double(), lstm.weight_hh_l0.double()
+    b = (lstm.bias_ih_l0 + lstm.bias_hh_l0).double()
+    h = torch.zeros((B, w_hh.shape[1]), dtype=torch.float64, device=x.device)
+    c = torch.zeros_like(h)
+    outs = []
+    for t in range(L):
+        st = start[t].bool().view(B, 1)
+        k = keep[t].double().view(B, 1)
+        h = torch.where(st, hs[t, l, env[t].long()].double() * k, h)
+        c = torch.where(st, cs[t, l, env[t].long()].double() * k, c)
+        gi, gf, gg, go = (x[t].double() @ w_ih.T + h @ w_hh.T + b).chunk(4, dim=1)
+        c = torch.sigmoid(gf) * c + torch.sigmoid(gi) * torch.tanh(gg)
+        h = torch.sigmoid(go) * torch.tanh(c)
+        outs.append(h)
+    return torch.stack(outs)
+
+
+@pytest.mark.parametrize("L,B,N,p_start", [(24, 512, 600, 0.03), (9, 37, 40, 0.2), (128, 64, 64, 0.01)])
+def test_dual_lstm_rows_matches_float64(L, B, N, p_start):
+    """The persistent row-layout LSTM (csrc/voxnav_learn_rows.hip: weights
+    resident, in-launch h / partial-dh hand-offs between the 8 unit blocks of a
+    row tile) against a float64 restatement: outputs and the weight / bias
+    gradients of both LSTMs, with sequence starts (stored states x keep) at t = 0,
+    at random steps and mid-row; full 512-row tiles, a ragged last tile, and a
+    whole 128-step rollout."""
+    from types import SimpleNamespace
+    from voxnav import lstm_seq
+    dev = "cuda:0"
+    D, H = 80, 256
+    torch.manual_seed(L * B + N)
+    la, lc = torch.nn.LSTM(D, H).to(dev), torch.nn.LSTM(D, H).to(dev)
+    pol = SimpleNamespace(lstm_actor=la, lstm_critic=lc)
+    if not lstm_seq.rows_supported(pol, D, B):
+        pytest.skip("row-layout kernels not co-resident on this device")
+    x = torch.randn((L, B, D), device=dev)
+    env = torch.randint(0, N, (L, B), device=dev, dtype=torch.int32)
+    start = (torch.rand((L, B), device=dev) < p_start).to(torch.uint8)
+    start[0] = 1
+    keep = (torch.rand((L, B), device=dev) > 0.3).float()
+    hs = 0.5 * torch.randn((L, 2, N, H), device=dev)
+    cs = 0.5 * torch.randn((L, 2, N, H), device=dev)
+    dy = torch.randn((2, L, B, H), device=dev)
+    oa, oc = lstm_seq.dual_lstm_rows(pol, x, env, start, keep, hs, cs)
+    ((oa * dy[0]).sum() + (oc * dy[1]).sum()).backward()
+    params = list(la.parameters()) + list(lc.parameters())
+    got = [p.grad.clone() for p in params]
+    lstm_seq.rows_check(torch.device(dev))
+    for p in params:
+        p.grad = None
+    ra = _rows_reference(x, env, start, keep, hs, cs, la, 0)
+    rc = _rows_reference(x, env, start, keep, hs, cs, lc, 1)
+    ((ra * dy[0].double()).sum() + (rc * dy[1].double()).sum()).backward()
+    _close(oa, ra.float())
+    _close(oc, rc.float())
+    for g, p in zip(got, params):
+        _close(g, p.grad, rel=1e-4)
