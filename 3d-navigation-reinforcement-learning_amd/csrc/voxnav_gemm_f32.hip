@@ -18,7 +18,7 @@
 // [k][col]) so every MFMA operand is one conflict-free ds_read_b32 (lane l
 // supplies A[row l%32][k l/32], B[k l/32][col l%32]); a row-major operand is
 // transposed on its way into LDS.  Split-K (gridDim.z > 1 along K) writes
-// per-split partials that gemm_reduce_kernel sums in split order (the result
+// per-split partials that gemm_reduce_kernel sums in a fixed order (the result
 // does not depend on timing).
 
 #include <hip/hip_runtime.h>
@@ -253,14 +253,36 @@ __global__ __launch_bounds__(256, 2) void gemm_f32_kernel(GemmArgs g) {
     }
 }
 
-// out[b][m][n] = sum over splits s in order of part[s][b][m][n]  (+ out if accumulate)
-__global__ void gemm_reduce_kernel(const float *__restrict__ part, int splits, int64_t per, float *__restrict__ out,
-                                   int accumulate) {
-    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= per) return;
-    float s = part[i];
-    for (int k = 1; k < splits; ++k) s += part[(int64_t)k * per + i];
-    out[i] = accumulate ? out[i] + s : s;
+// out[i] = sum over splits of part[s][i] (+ out if accumulate), deterministic:
+// a block owns 64 consecutive outputs; its 4 waves each sum one contiguous
+// quarter of the splits in order (loads 8 deep), and the quarters are added in
+// order through LDS -- so a tiny output over hundreds of splits (the heads'
+// weight gradients) is not one thread's serial chain of loads.
+__global__ __launch_bounds__(256) void gemm_reduce_kernel(const float *__restrict__ part, int splits, int64_t per,
+                                                          float *__restrict__ out, int accumulate) {
+    __shared__ float q[4][64];
+    const int o = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int64_t i = (int64_t)blockIdx.x * 64 + o;
+    const int per_q = (splits + 3) / 4;
+    const int k0 = w * per_q, k1 = min(splits, k0 + per_q);
+    float s = 0.0f;
+    if (i < per) {
+        int k = k0;
+        for (; k + 8 <= k1; k += 8) {
+            float v[8];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) v[j] = part[(int64_t)(k + j) * per + i];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) s += v[j];
+        }
+        for (; k < k1; ++k) s += part[(int64_t)k * per + i];
+    }
+    q[w][o] = s;
+    __syncthreads();
+    if (w == 0 && i < per) {
+        const float r = ((q[0][o] + q[1][o]) + q[2][o]) + q[3][o];
+        out[i] = accumulate ? out[i] + r : r;
+    }
 }
 
 template <bool A_KM, bool B_KM, bool AGRAD, int EPI>
@@ -335,11 +357,11 @@ int vn_gemm_f32_tn(const float *dy, const float *y, int64_t ldd, int64_t sd, con
     if (y) launch<true, true, true, 3>(g, batch, splits, s);
     else launch<true, true, false, 3>(g, batch, splits, s);
     const int64_t per = (int64_t)batch * M * N;
-    hipLaunchKernelGGL(gemm_reduce_kernel, dim3((unsigned)((per + 255) / 256)), dim3(256), 0, s, workspace, splits,
+    hipLaunchKernelGGL(gemm_reduce_kernel, dim3((unsigned)((per + 63) / 64)), dim3(256), 0, s, workspace, splits,
                        per, c, accumulate);
     if (colsum) {
         const int64_t pc = (int64_t)batch * M;
-        hipLaunchKernelGGL(gemm_reduce_kernel, dim3((unsigned)((pc + 255) / 256)), dim3(256), 0, s, workspace2,
+        hipLaunchKernelGGL(gemm_reduce_kernel, dim3((unsigned)((pc + 63) / 64)), dim3(256), 0, s, workspace2,
                            splits, pc, colsum, accumulate);
     }
     VN_HIP(hipGetLastError());
