@@ -66,9 +66,19 @@ __global__ __launch_bounds__(256, 2) void gemm_f32_kernel(GemmArgs g) {
     __shared__ float As[2][GK][GP];
     __shared__ float Bs[2][GK][GP];
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    // XCD-aware block order: blocks are dealt round-robin over the 8 XCDs
+    // (b and b + 8 share one), so the linear id is re-dealt to make each
+    // XCD's blocks one contiguous run of (split, batch, row tile, column
+    // tile): the column tiles of a row tile -- and for split-K every tile of
+    // a split -- then read their shared operand rows into ONE L2 (speed only;
+    // any placement gives the same result)
     const int ntn = (g.N + GT - 1) / GT;
-    const int tm = (int)blockIdx.x / ntn, tn = (int)blockIdx.x - tm * ntn;
-    const int bt = (int)blockIdx.y, split = (int)blockIdx.z;
+    const int nblk = (int)(gridDim.x * gridDim.y * gridDim.z);
+    int vb = (int)(blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z));
+    if ((nblk & 7) == 0) vb = (vb & 7) * (nblk >> 3) + (vb >> 3);
+    const int tiles = (int)gridDim.x;
+    const int tm = (vb % tiles) / ntn, tn = (vb % tiles) - tm * ntn;
+    const int bt = (vb / tiles) % (int)gridDim.y, split = vb / (tiles * (int)gridDim.y);
     const int m0 = tm * GT, n0 = tn * GT;
     const int k0 = split * g.kper;
     const int k1 = min(g.K, k0 + g.kper);

@@ -12,12 +12,10 @@
 // run of whole sb3 sequences laid end to end, and the outputs equal sb3's
 // padded per-sequence re-run without any padding.
 //
-// Work split: block (LSTM l, unit block ub of 32 units, row tile rt of 16
+// Work split: block (LSTM l, unit block ub of 32 units, row tile rt of 32
 // rows); the 8 unit blocks of one (l, rt) form a group that exchanges h each
-// step.  Every block of the grid (2 x 8 x R/16 <= 512, two per CU) is
-// resident for the whole launch (checked on the host): the two blocks on a
-// CU belong to different groups, so one runs its MFMAs while the other waits
-// for its group's hand-off.  The hand-off is
+// step.  Every block of the grid (2 x 8 x R/32 <= 256, one per CU) is
+// resident for the whole launch (checked on the host), and the hand-off is
 // the agent-scope protocol of the HIP guide's Guideline 16 (R1, counter form):
 // the payload (h_t; in the backward the partial dh of step t-1) is written
 // with 16-B write-through (sc1) stores, every storing wave drains vmcnt, the
@@ -26,9 +24,8 @@
 // with sc1 loads only.  Spins are bounded: a timeout sets *err and the launch
 // runs to its end (the host raises).
 //
-// forward   wave w = gate w: the 16 x 32 tile [x_t | h_{t-1}] @ W[gate w, 32
-//           units]^T on v_mfma_f32_16x16x4_f32 (two accumulators), W (168
-//           VGPRs) resident; the
+// forward   wave w = gate w: the 32 x 32 tile [x_t | h_{t-1}] @ W[gate w, 32
+//           units]^T on v_mfma_f32_32x32x2_f32, W (168 VGPRs) resident; the
 //           x part runs while the group's h_{t-1} is still being produced;
 //           the cell (i, f, g, o, c, h) as the epilogue, c carried in
 //           registers (a block owns its units' cells).
@@ -50,20 +47,21 @@ using vn_detail::fail;
 
 namespace {
 
-typedef __attribute__((ext_vector_type(4))) float f32x4_t;
+typedef __attribute__((ext_vector_type(16))) float f32x16_t;
 
-constexpr int RW = 16;      // rows per tile
+constexpr int RW = 32;      // rows per tile
 constexpr int UBK = 32;     // units per block
 constexpr int NUB = 8;      // unit blocks per LSTM (H = 256)
 constexpr uint32_t kSpinLimit = 1u << 22;   // ~0.3 s per wait at s_sleep 2
 
 __device__ __forceinline__ float sigm(float x) { return 1.0f / (1.0f + expf(-x)); }
 
-__device__ __forceinline__ f32x4_t zero4() {
-    f32x4_t z = {0.0f, 0.0f, 0.0f, 0.0f};
+__device__ __forceinline__ f32x16_t zero16() {
+    f32x16_t z;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) z[r] = 0.0f;
     return z;
 }
-#define VN_MM(a, b, c) c = __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0)
 
 __device__ __forceinline__ float4 f4(float a) { return make_float4(a, a, a, a); }
 __device__ __forceinline__ float4 operator+(float4 a, float4 b) { return make_float4(a.x + b.x, a.y + b.y, a.z + b.z, a.w + b.w); }
@@ -128,44 +126,42 @@ struct RowsFwd {
 };
 
 template <int D, int H>
-__global__ __launch_bounds__(256, 2) void lstm_rows_fwd_kernel(RowsFwd a) {
-    constexpr int NCX = D / 16, NCH = H / 16, NC = NCX + NCH;   // 16-k chunks
+__global__ __launch_bounds__(256, 1) void lstm_rows_fwd_kernel(RowsFwd a) {
+    constexpr int NCX = D / 8, NCH = H / 8, NC = NCX + NCH;
     constexpr int XP = D + 4, HP = H + 4, GP = 36;
-    static_assert(D % 16 == 0 && H == NUB * UBK, "shape");
-    __shared__ __attribute__((aligned(16))) float xs[RW][XP];
+    static_assert(D % 8 == 0 && H == NUB * UBK, "shape");
+    __shared__ __attribute__((aligned(16))) float xs[2][RW][XP];
     __shared__ __attribute__((aligned(16))) float hsl[RW][HP];
     __shared__ __attribute__((aligned(16))) float gts[4][RW][GP];
-    __shared__ __attribute__((aligned(16))) float bsl[4][UBK];
     const int tid = threadIdx.x, lane = tid & 63;
     const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);   // this wave's gate
-    const int kq = lane >> 4, cl = lane & 15;
+    const int hh = lane >> 5, cl = lane & 31;
     const int G = 2 * a.NT;
-    const int ub = (int)blockIdx.x / G, g = (int)blockIdx.x - ub * G;
+    const int ub = (int)blockIdx.x / G, g = (int)blockIdx.x - ub * G;   // blocks of a group: equal index mod 8 when G % 8 == 0
     const int l = g / a.NT, rt = g - l * a.NT;
     const int row0 = rt * RW, u0 = ub * UBK;
     const int B = a.B, L = a.L;
 
-    // resident weights: B operand of gate wv, units u0 + 16 j + cl (tile j),
-    // k = 16 c + 4 kq + i at k-step i of chunk c
-    float4 wr[2][NC];
+    // resident weights: B operand of gate wv, unit u0 + cl, k = 8 ch + 4 hh + j
+    float4 wr[NC];
+    {
+        const float *wi = a.w_ih + ((size_t)l * 4 * H + (size_t)wv * H + u0 + cl) * D;
+        const float *wh = a.w_hh + ((size_t)l * 4 * H + (size_t)wv * H + u0 + cl) * H;
 #pragma unroll
-    for (int j = 0; j < 2; ++j) {
-        const float *wi = a.w_ih + ((size_t)l * 4 * H + (size_t)wv * H + u0 + 16 * j + cl) * D;
-        const float *wh = a.w_hh + ((size_t)l * 4 * H + (size_t)wv * H + u0 + 16 * j + cl) * H;
-#pragma unroll
-        for (int c = 0; c < NC; ++c) {
-            const int k = 16 * c + 4 * kq;
-            wr[j][c] = c < NCX ? *reinterpret_cast<const float4 *>(wi + k)
-                               : *reinterpret_cast<const float4 *>(wh + (k - D));
+        for (int ch = 0; ch < NC; ++ch) {
+            const int k = 8 * ch + 4 * hh;
+            wr[ch] = ch < NCX ? *reinterpret_cast<const float4 *>(wi + k)
+                              : *reinterpret_cast<const float4 *>(wh + (k - D));
         }
     }
-    // epilogue mapping (threads 0..127): row er of the tile, units u0 + 4 eq .. + 3
-    const bool ethr = tid < RW * UBK / 4;
-    const int er = (tid >> 3) & (RW - 1), eq = tid & 7;
+    // epilogue mapping: row er of the tile, units u0 + 4 eq .. + 3
+    const int er = tid >> 3, eq = tid & 7;
     const int erow = row0 + er;
-    const bool elive = ethr && erow < B;
+    const bool elive = erow < B;
     const int eu = u0 + 4 * eq;
-    if (tid < 4 * UBK) bsl[tid >> 5][tid & 31] = a.bias[(size_t)l * 4 * H + (tid >> 5) * H + u0 + (tid & 31)];
+    float4 bs[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) bs[q] = *reinterpret_cast<const float4 *>(a.bias + (size_t)l * 4 * H + q * H + eu);
     float4 cc = f4(0.0f);
 
     const __amdgpu_buffer_rsrc_t hrs =
@@ -184,33 +180,34 @@ __global__ __launch_bounds__(256, 2) void lstm_rows_fwd_kernel(RowsFwd a) {
                        : f4(0.0f);
         }
     };
-    auto store_x = [&](const float4 *r) {
+    auto store_x = [&](int buf, const float4 *r) {
 #pragma unroll
         for (int i = 0; i < XPT; ++i) {
             const int f = tid + 256 * i;
             const int rr = f / (D / 4), c4 = f - rr * (D / 4);
-            if (f < XF) *reinterpret_cast<float4 *>(&xs[rr][4 * c4]) = r[i];
+            if (f < XF) *reinterpret_cast<float4 *>(&xs[buf][rr][4 * c4]) = r[i];
         }
     };
+    {
+        float4 r[XPT];
+        load_x(0, r);
+        store_x(0, r);
+    }
+    __syncthreads();
 
-    constexpr int HF = RW * H / 4, HPT = HF / 256;   // float4 of the h tile per thread
     for (int t = 0; t < L; ++t) {
-        // x_t rows to LDS (in flight while the group still produces h_{t-1}),
-        // then the x part of the product, which needs nothing from the group
-        {
-            float4 xr[XPT];
-            load_x(t, xr);
-            store_x(xr);
-        }
-        __syncthreads();
-        f32x4_t acc0 = zero4(), acc1 = zero4();
+        const int xb = t & 1;
+        float4 xn[XPT];
+        if (t + 1 < L) load_x(t + 1, xn);
+        // the x part of the product (needs nothing from the group)
+        f32x16_t acc = zero16();
 #pragma unroll
-        for (int c = 0; c < NCX; ++c) {
-            const float4 av = *reinterpret_cast<const float4 *>(&xs[cl][16 * c + 4 * kq]);
-            VN_MM(av.x, wr[0][c].x, acc0); VN_MM(av.x, wr[1][c].x, acc1);
-            VN_MM(av.y, wr[0][c].y, acc0); VN_MM(av.y, wr[1][c].y, acc1);
-            VN_MM(av.z, wr[0][c].z, acc0); VN_MM(av.z, wr[1][c].z, acc1);
-            VN_MM(av.w, wr[0][c].w, acc0); VN_MM(av.w, wr[1][c].w, acc1);
+        for (int ch = 0; ch < NCX; ++ch) {
+            const float4 av = *reinterpret_cast<const float4 *>(&xs[xb][cl][8 * ch + 4 * hh]);
+            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av.x, wr[ch].x, acc, 0, 0, 0);
+            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av.y, wr[ch].y, acc, 0, 0, 0);
+            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av.z, wr[ch].z, acc, 0, 0, 0);
+            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av.w, wr[ch].w, acc, 0, 0, 0);
         }
         // h_{t-1} of the tile's rows: the group's output of step t-1 (sc1 loads
         // after the counter shows all 8 blocks done), or the stored state at a
@@ -220,7 +217,7 @@ __global__ __launch_bounds__(256, 2) void lstm_rows_fwd_kernel(RowsFwd a) {
             __syncthreads();
         }
 #pragma unroll
-        for (int i = 0; i < HPT; ++i) {
+        for (int i = 0; i < 8; ++i) {
             const int f = tid + 256 * i;
             const int rr = f >> 6, c4 = f & 63;          // H / 4 = 64 float4 per row
             const int row = row0 + rr;
@@ -240,27 +237,23 @@ __global__ __launch_bounds__(256, 2) void lstm_rows_fwd_kernel(RowsFwd a) {
         }
         __syncthreads();
 #pragma unroll
-        for (int c = 0; c < NCH; ++c) {
-            const float4 av = *reinterpret_cast<const float4 *>(&hsl[cl][16 * c + 4 * kq]);
-            VN_MM(av.x, wr[0][NCX + c].x, acc0); VN_MM(av.x, wr[1][NCX + c].x, acc1);
-            VN_MM(av.y, wr[0][NCX + c].y, acc0); VN_MM(av.y, wr[1][NCX + c].y, acc1);
-            VN_MM(av.z, wr[0][NCX + c].z, acc0); VN_MM(av.z, wr[1][NCX + c].z, acc1);
-            VN_MM(av.w, wr[0][NCX + c].w, acc0); VN_MM(av.w, wr[1][NCX + c].w, acc1);
+        for (int ch = 0; ch < NCH; ++ch) {
+            const float4 av = *reinterpret_cast<const float4 *>(&hsl[cl][8 * ch + 4 * hh]);
+            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av.x, wr[NCX + ch].x, acc, 0, 0, 0);
+            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av.y, wr[NCX + ch].y, acc, 0, 0, 0);
+            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av.z, wr[NCX + ch].z, acc, 0, 0, 0);
+            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av.w, wr[NCX + ch].w, acc, 0, 0, 0);
         }
-        // gate tile -> LDS: register v = row 4 kq + v, unit 16 j + cl
+        if (t + 1 < L) store_x(xb ^ 1, xn);
+        // gate tile -> LDS: register v = row 8 (v / 4) + 4 hh + v % 4, unit cl
 #pragma unroll
-        for (int v = 0; v < 4; ++v) {
-            gts[wv][4 * kq + v][cl] = acc0[v];
-            gts[wv][4 * kq + v][16 + cl] = acc1[v];
-        }
+        for (int v = 0; v < 16; ++v) gts[wv][8 * (v >> 2) + 4 * hh + (v & 3)][cl] = acc[v];
         __syncthreads();
         if (elive) {
             const size_t o = (size_t)t * B + erow;
             float4 pre[4];
 #pragma unroll
-            for (int q = 0; q < 4; ++q)
-                pre[q] = *reinterpret_cast<const float4 *>(&gts[q][er][4 * eq]) +
-                         *reinterpret_cast<const float4 *>(&bsl[q][4 * eq]);
+            for (int q = 0; q < 4; ++q) pre[q] = *reinterpret_cast<const float4 *>(&gts[q][er][4 * eq]) + bs[q];
             float4 cp = cc;
             if (t == 0 || a.start[o]) {
                 const float k = a.keep[o];
@@ -293,8 +286,8 @@ __global__ __launch_bounds__(256, 2) void lstm_rows_fwd_kernel(RowsFwd a) {
             *reinterpret_cast<float4 *>(pa + 2 * H) = gg;
             *reinterpret_cast<float4 *>(pa + 3 * H) = og;
         }
-        // h_t published: the storing waves drained their payload stores above,
-        // the barrier orders every wave's drain before the one add
+        // h_t published (the payload stores were drained above; the barrier
+        // inside publish orders every wave's drain before the one add)
         __syncthreads();
         if (tid == 0) __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
@@ -313,44 +306,42 @@ struct RowsBwd {
     int L, B, NT;
 };
 
-
 template <int H>
-__global__ __launch_bounds__(256, 2) void lstm_rows_bwd_kernel(RowsBwd a) {
+__global__ __launch_bounds__(256, 1) void lstm_rows_bwd_kernel(RowsBwd a) {
     constexpr int GC = 4 * UBK;   // this block's gate columns (K of the partial product)
-    constexpr int NCK = GC / 16;  // 8 chunks of 16 k
+    constexpr int NCK = GC / 8;   // 16 chunks
     constexpr int DP = GC + 4, PP = H + 4;
     static_assert(H == NUB * UBK, "shape");
     __shared__ __attribute__((aligned(16))) float dgs[RW][DP];
     __shared__ __attribute__((aligned(16))) float pst[RW][PP];
     const int tid = threadIdx.x, lane = tid & 63;
     const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);   // output units 64 wv .. + 63
-    const int kq = lane >> 4, cl = lane & 15;
+    const int hh = lane >> 5, cl = lane & 31;
     const int G = 2 * a.NT;
     const int ub = (int)blockIdx.x / G, g = (int)blockIdx.x - ub * G;
     const int l = g / a.NT, rt = g - l * a.NT;
     const int row0 = rt * RW, u0 = ub * UBK;
     const int B = a.B, L = a.L;
 
-    // resident W_hh slice: B operand [k = gate * 32 + unit32][n = 64 wv + 16 j + cl],
-    // k = 16 c + 4 kq + i at k-step i of chunk c
-    float4 wb[4][NCK];
+    // resident W_hh slice: B operand [k = gate * 32 + unit32][n = 64 wv + 32 j + cl],
+    // k = 8 ch + 4 hh + jj
+    float4 wb[2][NCK];
 #pragma unroll
-    for (int j = 0; j < 4; ++j)
+    for (int j = 0; j < 2; ++j)
 #pragma unroll
-        for (int c = 0; c < NCK; ++c) {
+        for (int ch = 0; ch < NCK; ++ch) {
             float v[4];
 #pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                const int k = 16 * c + 4 * kq + i;
+            for (int jj = 0; jj < 4; ++jj) {
+                const int k = 8 * ch + 4 * hh + jj;
                 const int grow = (k >> 5) * H + u0 + (k & 31);
-                v[i] = a.w_hh[((size_t)l * 4 * H + grow) * H + 64 * wv + 16 * j + cl];
+                v[jj] = a.w_hh[((size_t)l * 4 * H + grow) * H + 64 * wv + 32 * j + cl];
             }
-            wb[j][c] = make_float4(v[0], v[1], v[2], v[3]);
+            wb[j][ch] = make_float4(v[0], v[1], v[2], v[3]);
         }
-    const bool ethr = tid < RW * UBK / 4;
-    const int er = (tid >> 3) & (RW - 1), eq = tid & 7;
+    const int er = tid >> 3, eq = tid & 7;
     const int erow = row0 + er;
-    const bool elive = ethr && erow < B;
+    const bool elive = erow < B;
     const int eu = u0 + 4 * eq;
     float4 dc = f4(0.0f);
     const size_t slot_f = (size_t)2 * a.NT * NUB * RW * H;     // floats per slot
@@ -360,7 +351,6 @@ __global__ __launch_bounds__(256, 2) void lstm_rows_bwd_kernel(RowsBwd a) {
     auto pofs = [&](int slot, int ubb, int row, int unit) -> uint32_t {   // byte offset in part
         return (uint32_t)(((size_t)slot * slot_f + ((((size_t)l * a.NT + rt) * NUB + ubb) * RW + row) * H + unit) * 4u);
     };
-    constexpr int PF = RW * H / 4, PPT = PF / 256;   // float4 of the partial per thread
 
     for (int s = 0; s < L; ++s) {
         const int t = L - 1 - s;
@@ -407,33 +397,33 @@ __global__ __launch_bounds__(256, 2) void lstm_rows_bwd_kernel(RowsBwd a) {
         }
         if (t == 0) break;                      // no dh_{-1}
         // A operand of the partial product: dG rows, zero where the step starts a sequence
-        if (ethr) {
 #pragma unroll
-            for (int q = 0; q < 4; ++q)
-                *reinterpret_cast<float4 *>(&dgs[er][q * UBK + 4 * eq]) = st ? f4(0.0f) : dG4[q];
-        }
+        for (int q = 0; q < 4; ++q)
+            *reinterpret_cast<float4 *>(&dgs[er][q * UBK + 4 * eq]) = st ? f4(0.0f) : dG4[q];
         __syncthreads();
-        f32x4_t acc[4] = {zero4(), zero4(), zero4(), zero4()};
+        f32x16_t acc0 = zero16(), acc1 = zero16();
 #pragma unroll
-        for (int c = 0; c < NCK; ++c) {
-            const float4 av = *reinterpret_cast<const float4 *>(&dgs[cl][16 * c + 4 * kq]);
-#pragma unroll
-            for (int j = 0; j < 4; ++j) VN_MM(av.x, wb[j][c].x, acc[j]);
-#pragma unroll
-            for (int j = 0; j < 4; ++j) VN_MM(av.y, wb[j][c].y, acc[j]);
-#pragma unroll
-            for (int j = 0; j < 4; ++j) VN_MM(av.z, wb[j][c].z, acc[j]);
-#pragma unroll
-            for (int j = 0; j < 4; ++j) VN_MM(av.w, wb[j][c].w, acc[j]);
+        for (int ch = 0; ch < NCK; ++ch) {
+            const float4 av = *reinterpret_cast<const float4 *>(&dgs[cl][8 * ch + 4 * hh]);
+            acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(av.x, wb[0][ch].x, acc0, 0, 0, 0);
+            acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(av.x, wb[1][ch].x, acc1, 0, 0, 0);
+            acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(av.y, wb[0][ch].y, acc0, 0, 0, 0);
+            acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(av.y, wb[1][ch].y, acc1, 0, 0, 0);
+            acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(av.z, wb[0][ch].z, acc0, 0, 0, 0);
+            acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(av.z, wb[1][ch].z, acc1, 0, 0, 0);
+            acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(av.w, wb[0][ch].w, acc0, 0, 0, 0);
+            acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(av.w, wb[1][ch].w, acc1, 0, 0, 0);
         }
 #pragma unroll
-        for (int j = 0; j < 4; ++j)
-#pragma unroll
-            for (int v = 0; v < 4; ++v) pst[4 * kq + v][64 * wv + 16 * j + cl] = acc[j][v];
+        for (int v = 0; v < 16; ++v) {
+            const int r = 8 * (v >> 2) + 4 * hh + (v & 3);
+            pst[r][64 * wv + cl] = acc0[v];
+            pst[r][64 * wv + 32 + cl] = acc1[v];
+        }
         __syncthreads();
         // the partial [RW][H] of this block: 16-B sc1 stores, then publish
 #pragma unroll
-        for (int i = 0; i < PPT; ++i) {
+        for (int i = 0; i < 8; ++i) {
             const int f = tid + 256 * i;
             const int rr = f >> 6, c4 = f & 63;
             st_sc1(prs, pofs(t & 1, ub, rr, 4 * c4), *reinterpret_cast<const float4 *>(&pst[rr][4 * c4]));

@@ -40,7 +40,11 @@ def _splits(K: int, tiles: int) -> int:
     """Split count for a K-long reduction whose output has `tiles` 128x128 tiles:
     enough blocks to fill the chip (>= ~512), at least SPLIT_ROWS rows each."""
     want = max(1, -(-512 // max(1, tiles)))
-    return max(1, min(want, 256, K // SPLIT_ROWS))
+    sp = max(1, min(want, 256, K // SPLIT_ROWS))
+    # a multiple of 8 when it can be: the kernel then deals whole splits to one
+    # XCD each (csrc/voxnav_gemm_f32.hip), so a split's operand rows are read
+    # into one L2
+    return sp if sp < 8 else sp // 8 * 8
 
 
 def mm_tn(a: torch.Tensor, b: torch.Tensor, y: Optional[torch.Tensor] = None, colsum: bool = False,

@@ -141,7 +141,7 @@ class _DualLSTMRows(torch.autograd.Function):
         w_ih = torch.stack([w_ih_a, w_ih_c]).contiguous()
         w_hh = torch.stack([w_hh_a, w_hh_c]).contiguous()
         bias = torch.stack([b_ih_a + b_hh_a, b_ih_c + b_hh_c]).contiguous()
-        nt = -(-B // 16)                        # row tiles of 16 (csrc/voxnav_learn_rows.hip RW)
+        nt = -(-B // 32)                        # row tiles of 32 (csrc/voxnav_learn_rows.hip RW)
         hout = torch.empty((2, L, B, H), dtype=torch.float32, device=dev)
         hprev, cprev, cnew = torch.empty_like(hout), torch.empty_like(hout), torch.empty_like(hout)
         act = torch.empty((2, L, B, G), dtype=torch.float32, device=dev)
@@ -168,7 +168,7 @@ class _DualLSTMRows(torch.autograd.Function):
         nf = C.c_int64()
         _native.check(lib.vn_lstm_rows_part_floats(B, C.byref(nf)), "vn_lstm_rows_part_floats")
         part = torch.empty(nf.value, dtype=torch.float32, device=dev)
-        cnt = torch.empty(2 * -(-B // 16), dtype=torch.int32, device=dev)
+        cnt = torch.empty(2 * -(-B // 32), dtype=torch.int32, device=dev)
         _native.check(lib.vn_lstm_rows_bwd(_p(dh_out), _p(w_hh), _p(act), _p(cprev), _p(cnew), _p(start), _p(dG),
                                            _p(part), _p(cnt), _p(_rows_err(dev)), L, B, H, st), "vn_lstm_rows_bwd")
         dGf = dG.view(2, L * B, G)

@@ -427,7 +427,7 @@ int vn_lstm_seq_bwd_mfma(const float *dh_out, const float *w_hh, float *wpack, c
  *   env [L][B] int32 (the row's env), start [L][B] u8 (1: a sequence starts),
  *   keep [L][B] (1 - episode_start); out: hout, hprev (the h_{t-1} used), cprev,
  *   cnew [2][L][B][H], act [2][L][B][4H] (i, f, g, o); cnt: 2 * ceil(B / 32) u32
- *   counters (zeroed by the call; 16-row tiles); err: set to 1 if a hand-off timed out.
+ *   counters (zeroed by the call; 32-row tiles); err: set to 1 if a hand-off timed out.
  * Backward: dh_out [2][L][B][H] -> dG [2][L][B][4H]; part: vn_lstm_rows_part_floats
  * floats of workspace.  vn_lstm_rows_supported: 1 when (D, H, B) can run (every
  * block co-resident on this device), else 0 (use vn_lstm_seq_*).
