@@ -200,13 +200,14 @@ struct Rays {
     bool wh[6];
 };
 
-// sensing mark of ray r at step s for a byte of a register column;
-// returns whether the column changed
-template <int PH>
-__device__ __forceinline__ bool mark(Col<PH> &c, int z, const Rays &ry, int r, int s) {
-    if (s <= ry.nf[r]) return col_or_chk<PH>(c, z, KNOWN);
-    if (ry.wh[r] && s == ry.nf[r] + 1) return col_or_chk<PH>(c, z, WALLB);
-    return false;
+// sensing mark of ray r at step s on byte z of a window word (its byte 2);
+// returns whether the byte changed
+__device__ __forceinline__ bool mark_w(uint32_t &w, const Rays &ry, int r, int s) {
+    const uint32_t v = s <= ry.nf[r] ? KNOWN : (ry.wh[r] && s == ry.nf[r] + 1) ? WALLB : 0u;
+    const uint32_t m = v << 16;
+    const bool ch = (w & m) != m;
+    w |= m;
+    return ch;
 }
 
 // ----------------------------------------------------------------------------
@@ -400,6 +401,27 @@ __device__ __forceinline__ void tile_write(uint64_t *tile, int slot, const Col<P
 }
 
 __device__ __forceinline__ int tslot(int x, int y) { return ((x & 3) << 2) | (y & 3); }
+
+// The window bytes [z - 2, z + 1] of a tile column as one u32 (byte 0 = z - 2,
+// zeros outside [0, PH)): two dword reads and a funnel shift, so a sensing
+// pass holds one register per window column instead of the whole column
+// (PH 16: 4 registers per column).
+template <int PH>
+__device__ __forceinline__ uint32_t tile_win(const uint64_t *tile, int slot, int z) {
+    constexpr int NW = PH / 4;
+    const uint32_t *cw = reinterpret_cast<const uint32_t *>(tile + slot * TileGeom<PH>::QW);
+    const int o = z - 2;
+    const int k0 = o >> 2;                                   // -1 for o = -2, -1
+    const uint32_t lo = cw[k0 < 0 ? 0 : k0] & (k0 >= 0 ? ~0u : 0u);
+    const uint32_t hi = cw[k0 + 1 < NW ? k0 + 1 : NW - 1] & (k0 + 1 < NW ? ~0u : 0u);
+    const int sh = (o & 3) * 8;
+    return sh ? (lo >> sh) | (hi << (32 - sh)) : lo;
+}
+
+// byte z of a tile column
+__device__ __forceinline__ void tile_put_byte(uint64_t *tile, int qw, int slot, int z, uint32_t v) {
+    reinterpret_cast<uint8_t *>(tile + slot * qw)[z] = (uint8_t)v;
+}
 
 // Exchanges inside an agent group (4 lanes = one DPP quad): a quad_perm DPP
 // move is one VALU instruction, where __shfl is an LDS permute with its
@@ -662,23 +684,33 @@ __device__ __forceinline__ int sense_observe(const Params &p, int8_t *map, uint6
     // PC: lane 0 owns the x-plane row (y, z), lane 1 the y-plane row (x, z), both in LDS
     RT *prow_lds = (PC && q < 2) ? ps + (q == 0 ? (y & 3) : 4 + (x & 3)) * 8 + z : nullptr;
 
-    // ---- this lane's 4 window columns from the tile ----
+    // ---- this lane's 4 window columns from the tile: the window word
+    //      (bytes z-2 .. z+1) of each, and the whole column dx = 0 (lane 2's
+    //      center column: visit count and z rays) ----
     const int cy = y + q - 2;
     const bool yin = cy >= 0 && cy < R.D;
-    Col<PH> col[4];
+    // FRESH: the reset copied the room image (PC: latent walls) to HBM, or
+    // cleared it; the tile takes the same columns
+    auto fresh_col = [&](int i, Col<PH> &c) {
+        col_zero<PH>(c);
+        if (PC && yin && x + i - 2 >= 0 && x + i - 2 < R.W)
+            col_load<PH>(p.wimg + (size_t)g.room * p.map_bytes + boff<PH>(x + i - 2, cy, 0, nby), c);
+    };
+    uint32_t win[4];
+    Col<PH> cen;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
         if (FRESH) {
-            col_zero<PH>(col[i]);
-            // PC: the reset copied the room image (latent walls) to HBM; the
-            // tile takes the same columns
-            if (PC && yin && x + i - 2 >= 0 && x + i - 2 < R.W)
-                col_load<PH>(p.wimg + (size_t)g.room * p.map_bytes + boff<PH>(x + i - 2, cy, 0, nby), col[i]);
+            Col<PH> c;
+            fresh_col(i, c);
+            win[i] = col_window<PH>(c, z);
+            if (i == 2) cen = c;
         } else {
-            tile_read<PH>(tile, tslot(x + i - 2, cy), col[i]);
+            win[i] = tile_win<PH>(tile, tslot(x + i - 2, cy), z);
         }
     }
-    uint32_t chg = 0;                     // bit i: col[i] changed by this pass
+    if (!FRESH) tile_read<PH>(tile, tslot(x, cy), cen);
+    uint32_t chg = 0;                     // bit i: window column i changed by this pass
 
     // ---- ray extents from the room's 8-byte record (bit7: ended at a wall) ----
     Rays ry;
@@ -737,17 +769,17 @@ __device__ __forceinline__ int sense_observe(const Params &p, int8_t *map, uint6
     // ---- in-window ray cells, z rays and the center ----
     uint32_t cold = 0;
     if (q == 2) {                       // row dy = 0: -x s=2, -x s=1, center, +x s=1
-        chg |= (uint32_t)mark<PH>(col[0], z, ry, 1, 2);
-        chg |= (uint32_t)mark<PH>(col[1], z, ry, 1, 1) << 1;
-        chg |= (uint32_t)mark<PH>(col[3], z, ry, 0, 1) << 3;
-        cold = col_byte<PH>(col[2], z);
-        col_or_range<PH>(col[2], z + 1, z + ry.nf[4], KNOWN);                    // up
-        if (ry.wh[4]) col_or<PH>(col[2], z + ry.nf[4] + 1, WALLB);
-        col_or_range<PH>(col[2], z - ry.nf[5], z - 1, KNOWN);                    // down
-        if (ry.wh[5]) col_or<PH>(col[2], z - ry.nf[5] - 1, WALLB);
+        chg |= (uint32_t)mark_w(win[0], ry, 1, 2);
+        chg |= (uint32_t)mark_w(win[1], ry, 1, 1) << 1;
+        chg |= (uint32_t)mark_w(win[3], ry, 0, 1) << 3;
+        cold = col_byte<PH>(cen, z);
+        col_or_range<PH>(cen, z + 1, z + ry.nf[4], KNOWN);                       // up
+        if (ry.wh[4]) col_or<PH>(cen, z + ry.nf[4] + 1, WALLB);
+        col_or_range<PH>(cen, z - ry.nf[5], z - 1, KNOWN);                       // down
+        if (ry.wh[5]) col_or<PH>(cen, z - ry.nf[5] - 1, WALLB);
         chg |= 4u;                                  // the center count changes every step
     } else {                            // column dx = 0: -y s=2 (q0), -y s=1 (q1), +y s=1 (q3)
-        chg |= (uint32_t)mark<PH>(col[2], z, ry, q == 3 ? 2 : 3, q == 0 ? 2 : 1) << 2;
+        chg |= (uint32_t)mark_w(win[2], ry, q == 3 ? 2 : 3, q == 0 ? 2 : 1) << 2;
     }
     cold = group_bcast<2>(cold);
     int t;
@@ -767,9 +799,13 @@ __device__ __forceinline__ int sense_observe(const Params &p, int8_t *map, uint6
         t += 1;
         if (t > 63) t = 63;
     }
-    if (q == 2) col_set<PH>(col[2], z, KNOWN | (uint32_t)t);
+    if (q == 2) {
+        col_set<PH>(cen, z, KNOWN | (uint32_t)t);
+        win[2] = col_window<PH>(cen, z);
+    }
 
     // ---- changed columns back to the tile (dirty), new plane marks to HBM ----
+    // (lane 2's center column whole; any other column changed only in byte z)
     uint32_t dm = 0;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
@@ -778,7 +814,16 @@ __device__ __forceinline__ int sense_observe(const Params &p, int8_t *map, uint6
         // column of the previous episode's window survives in the tile
         if (FRESH || (inroom && ((chg >> i) & 1u))) {
             const int s = tslot(x + i - 2, cy);
-            tile_write<PH>(tile, s, col[i]);
+            if (q == 2 && i == 2) {
+                tile_write<PH>(tile, s, cen);
+            } else if (FRESH) {
+                Col<PH> c;
+                fresh_col(i, c);
+                col_set<PH>(c, z, (win[i] >> 16) & 0xffu);
+                tile_write<PH>(tile, s, c);
+            } else {
+                tile_put_byte(tile, TileGeom<PH>::QW, s, z, win[i] >> 16);
+            }
             // PC: an x/y ray mark is also in the planes, so only the agent's own
             // column (visit count, z rays) has to reach HBM
             if (inroom && (!PC || (q == 2 && i == 2))) dm |= 1u << s;
@@ -890,7 +935,7 @@ __device__ __forceinline__ int sense_observe(const Params &p, int8_t *map, uint6
         // the row's 20 code words: window bytes in obs order, then lane q's tail word
         LdsU32 *l = (LdsU32 *)dst.stage + dst.aslot * 20;
 #pragma unroll
-        for (int i = 0; i < 4; ++i) l[4 * i + q] = col_window<PH>(col[i], z);
+        for (int i = 0; i < 4; ++i) l[4 * i + q] = win[i];
         const uint32_t w0 = TC_ZERO4 + ((TC_ONE - TC_ZERO) << (8 * g.facing));
         const uint32_t w1 = (TC_ACT + (uint32_t)g.last_action) | ((g.was_near_wall ? TC_ONE : TC_ZERO) << 8) |
                             ((g.last_bump ? TC_ONE : TC_ZERO) << 16) | ((TC_CID + (uint32_t)g.cid) << 24);
@@ -905,20 +950,13 @@ __device__ __forceinline__ int sense_observe(const Params &p, int8_t *map, uint6
         // byte-mark kernels, whose occupancy the VGPRs set
         LdsF4 *l = (LdsF4 *)dst.stage + dst.aslot * 20;
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            const uint32_t wb = col_window<PH>(col[i], z);
-            l[4 * i + q] = f4v(code_float4(wb, tab));
-        }
+        for (int i = 0; i < 4; ++i) l[4 * i + q] = f4v(code_float4(win[i], tab));
         l[16 + q] = f4v(tail);
     } else if (glb4) {
         // explicit address space: no flat stores; non-temporal like the flush
         GlbF4 *gp = (GlbF4 *)glb4;
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            const uint32_t wb = col_window<PH>(col[i], z);
-            __builtin_nontemporal_store(
-                f4v(code_float4(wb, tab)), gp + 4 * i + q);
-        }
+        for (int i = 0; i < 4; ++i) __builtin_nontemporal_store(f4v(code_float4(win[i], tab)), gp + 4 * i + q);
         __builtin_nontemporal_store(f4v(tail), gp + 16 + q);
     }
     return t;
