@@ -173,30 +173,28 @@ __global__ __launch_bounds__(256, 2) void gemm_f32_kernel(GemmArgs g) {
     const int wr = 64 * (wv & 1), wc = 64 * (wv >> 1);
     const int col = lane & 31, kh = lane >> 5;
 
-    // two chunks in flight: chunk c's global loads are issued at the start of
-    // chunk c - 2's MFMAs and land in LDS after chunk c - 1's (two register
-    // sets R0 / R1, LDS double-buffered; the loop is unrolled by two so every
-    // register set is static)
-    float4 ra1[GNF], rb1[GNF];
-    auto load = [&](int c, float4 *xa, float4 *xb) {
-        if (c < nchunks) {
-            ld_op(A, A2, g.lda, m0, g.M, A_KM, AGRAD, k0 + c * GK, xa);
-            ld_op(Bm, nullptr, g.ldb, n0, g.N, B_KM, false, k0 + c * GK, xb);
+    if (nchunks > 0) {
+        ld_op(A, A2, g.lda, m0, g.M, A_KM, AGRAD, k0, ra);
+        ld_op(Bm, nullptr, g.ldb, n0, g.N, B_KM, false, k0, rb);
+        st_op(As[0], A_KM, ra);
+        st_op(Bs[0], B_KM, rb);
+    }
+    __syncthreads();
+    for (int ch = 0; ch < nchunks; ++ch) {
+        const int bf = ch & 1;
+        if (ch + 1 < nchunks) {
+            ld_op(A, A2, g.lda, m0, g.M, A_KM, AGRAD, k0 + (ch + 1) * GK, ra);
+            ld_op(Bm, nullptr, g.ldb, n0, g.N, B_KM, false, k0 + (ch + 1) * GK, rb);
         }
-    };
-    auto store = [&](int bf, const float4 *xa, const float4 *xb) {
-        st_op(As[bf], A_KM, xa);
-        st_op(Bs[bf], B_KM, xb);
-    };
-    auto compute = [&](int bf) {
         if (g.colsum && A_KM && tn == 0) {
             const int cc = tid & 127, kb = (tid >> 7) * (GK / 2);
 #pragma unroll
             for (int k = 0; k < GK / 2; ++k) csum += As[bf][kb + k][cc];
         }
-        // k-step s + 1's operands read before k-step s's MFMAs (4 LDS reads,
-        // then 4 MFMAs, enforced on the scheduler)
-        float pa0, pa1, pb0, pb1, qa0, qa1, qb0, qb1;
+        {
+            // k-step s + 1's operands read before k-step s's MFMAs (4 LDS reads,
+            // then 4 MFMAs, enforced on the scheduler)
+            float pa0, pa1, pb0, pb1, qa0, qa1, qb0, qb1;
 #define GM_RD(s_, A0, A1, B0, B1)                                                                            \
     {                                                                                                        \
         const int kk_ = 2 * (s_) + kh;                                                                       \
@@ -212,39 +210,27 @@ __global__ __launch_bounds__(256, 2) void gemm_f32_kernel(GemmArgs g) {
         acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(A1, B0, acc[1][0], 0, 0, 0);                        \
         acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(A1, B1, acc[1][1], 0, 0, 0);                        \
     }
-        GM_RD(0, pa0, pa1, pb0, pb1)
+            GM_RD(0, pa0, pa1, pb0, pb1)
 #pragma unroll
-        for (int s = 0; s < GK / 2; s += 2) {
-            GM_RD(s + 1, qa0, qa1, qb0, qb1)
-            GM_MM(pa0, pa1, pb0, pb1)
-            if (s + 2 < GK / 2) GM_RD(s + 2, pa0, pa1, pb0, pb1)
-            GM_MM(qa0, qa1, qb0, qb1)
-        }
-        __builtin_amdgcn_sched_group_barrier(0x100, 4, 0);
+            for (int s = 0; s < GK / 2; s += 2) {
+                GM_RD(s + 1, qa0, qa1, qb0, qb1)
+                GM_MM(pa0, pa1, pb0, pb1)
+                if (s + 2 < GK / 2) GM_RD(s + 2, pa0, pa1, pb0, pb1)
+                GM_MM(qa0, qa1, qb0, qb1)
+            }
+            __builtin_amdgcn_sched_group_barrier(0x100, 4, 0);
 #pragma unroll
-        for (int s = 0; s < GK / 2; ++s) {
-            if (s + 1 < GK / 2) __builtin_amdgcn_sched_group_barrier(0x100, 4, 0);
-            __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);
-        }
+            for (int s = 0; s < GK / 2; ++s) {
+                if (s + 1 < GK / 2) __builtin_amdgcn_sched_group_barrier(0x100, 4, 0);
+                __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);
+            }
 #undef GM_RD
 #undef GM_MM
-    };
-
-    load(0, ra, rb);
-    load(1, ra1, rb1);
-    if (nchunks > 0) store(0, ra, rb);
-    __syncthreads();
-    for (int ch = 0; ch < nchunks; ch += 2) {
-        // chunk ch in LDS buffer 0, chunk ch + 1 in flight in R1
-        load(ch + 2, ra, rb);
-        compute(0);
-        if (ch + 1 < nchunks) store(1, ra1, rb1);
-        __syncthreads();
-        if (ch + 1 >= nchunks) break;
-        // chunk ch + 1 in LDS buffer 1, chunk ch + 2 in flight in R0
-        load(ch + 3, ra1, rb1);
-        compute(1);
-        if (ch + 2 < nchunks) store(0, ra, rb);
+        }
+        if (ch + 1 < nchunks) {
+            st_op(As[bf ^ 1], A_KM, ra);
+            st_op(Bs[bf ^ 1], B_KM, rb);
+        }
         __syncthreads();
     }
     if (g.colsum && A_KM && tn == 0) {   // (block-uniform) one column tile per row block writes the sums
