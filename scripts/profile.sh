@@ -13,6 +13,8 @@ BARGS="${BENCH_ARGS:-} --single-step-check 0 --collector none --simple 0 --fuse-
 DARGS="--steps 20 --warmup 5 --cpu-seconds 0 --episode-window 0 $BARGS"
 TAG=${TAG:-r02}
 PASSES=${PASSES:-dtrace,dfetch,dwrite,trace,simple,simple_fetch,simple_write,trace_f1,fetch,write,l2,sq,sqw,tcp}
+# the env-only room-set legs (P2 / P3, 1,024 steps after 32 warmup, F=128), one set per run
+SARGS="--steps 20 --warmup 5 --cpu-seconds 0 --episode-window 0 --single-step-check 0 --collector none --simple 0 --fuse-check 0 --room-set-steps 1024"
 step() {
   local name=$1 t=$2; shift 2
   [[ ",$PASSES," == *",$name,"* ]] || return 0
@@ -35,4 +37,9 @@ step l2 400 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum -d gpurun_out/${TAG}_l2 -o 
 step sq 400 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_LDS SQ_INSTS_BRANCH SQ_INSTS_SMEM -d gpurun_out/${TAG}_sq -o sq --output-format csv -- python3 bench.py --steps 5408 --warmup 32 --cpu-seconds 0 $BARGS
 step sqw 400 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU -d gpurun_out/${TAG}_sqw -o sqw --output-format csv -- python3 bench.py --steps 5408 --warmup 32 --cpu-seconds 0 $BARGS
 step tcp 400 rocprofv3 --pmc TCP_TCC_READ_REQ_sum TCP_PENDING_STALL_CYCLES_sum -d gpurun_out/${TAG}_tcp -o tcp --output-format csv -- python3 bench.py --steps 5408 --warmup 32 --cpu-seconds 0 $BARGS
+for SET in P2_training P3_training; do
+  step ${SET}_trace 400 rocprofv3 --kernel-trace --stats -d gpurun_out/${TAG}_${SET}_trace -o trace --output-format csv -- python3 bench.py $SARGS --room-sets $SET
+  step ${SET}_fetch 400 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/${TAG}_${SET}_fetch -o fetch --output-format csv -- python3 bench.py $SARGS --room-sets $SET
+  step ${SET}_write 400 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/${TAG}_${SET}_write -o write --output-format csv -- python3 bench.py $SARGS --room-sets $SET
+done
 exit 0
