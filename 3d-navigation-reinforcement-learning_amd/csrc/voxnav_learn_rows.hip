@@ -298,24 +298,42 @@ struct RowsBwd {
     const float *w_hh;       // [2][4H][H]
     const float *act;        // [2][L][B][4H]
     const float *cprev, *cnew;
+    const float *hprev;      // [2][L][B][H]  the h_{t-1} each forward step used
+    const float *x;          // [L][B][D]
     const uint8_t *start;    // [L][B]
-    float *dG;               // [2][L][B][4H] out
+    float *dG;               // [2][L][B][4H] out (may be NULL)
     float *part;             // [2 slots][2][NT][NUB][RW][H] partial dh
+    float *wpart;            // [NT][2][4H][H + D] per-row-tile [dW_hh | dW_ih]
+    float *bpart;            // [NT][2][4H] per-row-tile db
     uint32_t *cnt;           // [2 * NT]
     int32_t *err;
     int L, B, NT;
 };
 
-template <int H>
+// Backward.  Besides the recurrence, each block accumulates the weight
+// gradients of its 128 gate rows over all steps and its 32 rows: dW_hh +=
+// dG_t^T h_{t-1}, dW_ih += dG_t^T x_t, db += sum dG_t, on the matrix cores
+// with the accumulators resident (wave w: gate w's 32 rows, 8 + 3 tiles of
+// 32 x 32).  Those products do not feed the recurrence, so they are issued
+// after the step's partial is published and run while the group's next
+// hand-off is in flight.  Per-row-tile partials are summed (fixed order) by
+// rows_wsum_kernel.
+template <int D, int H>
 __global__ __launch_bounds__(256, 1) void lstm_rows_bwd_kernel(RowsBwd a) {
     constexpr int GC = 4 * UBK;   // this block's gate columns (K of the partial product)
     constexpr int NCK = GC / 8;   // 16 chunks
-    constexpr int DP = GC + 4, PP = H + 4;
-    static_assert(H == NUB * UBK, "shape");
+    constexpr int DP = GC + 4, PP = H + 4, XP = 96;   // xs padded to 3 tiles of 32 (zeros past D)
+    constexpr int NXT = (D + 31) / 32;                 // dW_ih column tiles
+    constexpr int HF = RW * H / 4 / 256;               // float4 of the h tile per thread (8)
+    constexpr int XF = RW * D / 4, XPT = (XF + 255) / 256;
+    static_assert(H == NUB * UBK && D <= XP && D % 4 == 0, "shape");
     __shared__ __attribute__((aligned(16))) float dgs[RW][DP];
     __shared__ __attribute__((aligned(16))) float pst[RW][PP];
+    __shared__ __attribute__((aligned(16))) float hsl[RW][PP];
+    __shared__ __attribute__((aligned(16))) float xsl[RW][XP];
+    __shared__ uint8_t stf[RW];
     const int tid = threadIdx.x, lane = tid & 63;
-    const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);   // output units 64 wv .. + 63
+    const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);   // output units 64 wv .. + 63; dW gate wv
     const int hh = lane >> 5, cl = lane & 31;
     const int G = 2 * a.NT;
     const int ub = (int)blockIdx.x / G, g = (int)blockIdx.x - ub * G;
@@ -344,6 +362,12 @@ __global__ __launch_bounds__(256, 1) void lstm_rows_bwd_kernel(RowsBwd a) {
     const bool elive = erow < B;
     const int eu = u0 + 4 * eq;
     float4 dc = f4(0.0f);
+    float4 dbs[4] = {f4(0.0f), f4(0.0f), f4(0.0f), f4(0.0f)};
+    f32x16_t wacc[8], xacc[NXT];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) wacc[j] = zero16();
+#pragma unroll
+    for (int j = 0; j < NXT; ++j) xacc[j] = zero16();
     const size_t slot_f = (size_t)2 * a.NT * NUB * RW * H;     // floats per slot
     const __amdgpu_buffer_rsrc_t prs =
         __builtin_amdgcn_make_buffer_rsrc(a.part, 0, (int)(2 * slot_f * 4), 0x00020000);
@@ -351,9 +375,29 @@ __global__ __launch_bounds__(256, 1) void lstm_rows_bwd_kernel(RowsBwd a) {
     auto pofs = [&](int slot, int ubb, int row, int unit) -> uint32_t {   // byte offset in part
         return (uint32_t)(((size_t)slot * slot_f + ((((size_t)l * a.NT + rt) * NUB + ubb) * RW + row) * H + unit) * 4u);
     };
+    // zero the padding columns of xs once (never written by the staging)
+#pragma unroll
+    for (int i = tid; i < RW * (XP - D); i += 256) xsl[i / (XP - D)][D + i % (XP - D)] = 0.0f;
 
     for (int s = 0; s < L; ++s) {
         const int t = L - 1 - s;
+        // the step's h_{t-1} and x_t rows (weight-gradient operands; rows past B
+        // clamped: their dG is zero), in flight across the hand-off wait
+        float4 hr[HF], xr[XPT];
+#pragma unroll
+        for (int i = 0; i < HF; ++i) {
+            const int f = tid + 256 * i;
+            const int rr = f >> 6, c4 = f & 63;
+            const int row = min(row0 + rr, B - 1);
+            hr[i] = *reinterpret_cast<const float4 *>(a.hprev + (((size_t)l * L + t) * B + row) * H + 4 * c4);
+        }
+#pragma unroll
+        for (int i = 0; i < XPT; ++i) {
+            const int f = tid + 256 * i;
+            const int rr = f / (D / 4), c4 = f - rr * (D / 4);
+            const int row = min(row0 + rr, B - 1);
+            xr[i] = f < XF ? *reinterpret_cast<const float4 *>(a.x + ((size_t)t * B + row) * D + 4 * c4) : f4(0.0f);
+        }
         if (s > 0) {
             if (tid == 0) wait_ge(cnt, (uint32_t)(NUB * s), a.err);
             __syncthreads();
@@ -391,45 +435,112 @@ __global__ __launch_bounds__(256, 1) void lstm_rows_bwd_kernel(RowsBwd a) {
             VN_CELLB(x) VN_CELLB(y) VN_CELLB(z) VN_CELLB(w)
 #undef VN_CELLB
             if (st) dc = f4(0.0f);   // c_{t-1} of this row came from the buffer
-            float *pg = a.dG + (((size_t)l * L + t) * B + erow) * 4 * H + eu;
+            if (a.dG) {
+                float *pg = a.dG + (((size_t)l * L + t) * B + erow) * 4 * H + eu;
 #pragma unroll
-            for (int q = 0; q < 4; ++q) *reinterpret_cast<float4 *>(pg + q * H) = dG4[q];
+                for (int q = 0; q < 4; ++q) *reinterpret_cast<float4 *>(pg + q * H) = dG4[q];
+            }
+#pragma unroll
+            for (int q = 0; q < 4; ++q) dbs[q] = dbs[q] + dG4[q];
         }
-        if (t == 0) break;                      // no dh_{-1}
-        // A operand of the partial product: dG rows, zero where the step starts a sequence
+        // dG (the weight-gradient and the partial product's A operand), the
+        // sequence-start flags, h_{t-1} and x_t to LDS
 #pragma unroll
-        for (int q = 0; q < 4; ++q)
-            *reinterpret_cast<float4 *>(&dgs[er][q * UBK + 4 * eq]) = st ? f4(0.0f) : dG4[q];
-        __syncthreads();
-        f32x16_t acc0 = zero16(), acc1 = zero16();
+        for (int q = 0; q < 4; ++q) *reinterpret_cast<float4 *>(&dgs[er][q * UBK + 4 * eq]) = dG4[q];
+        if (eq == 0) stf[er] = st ? 1 : 0;
 #pragma unroll
-        for (int ch = 0; ch < NCK; ++ch) {
-            const float4 av = *reinterpret_cast<const float4 *>(&dgs[cl][8 * ch + 4 * hh]);
-            acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(av.x, wb[0][ch].x, acc0, 0, 0, 0);
-            acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(av.x, wb[1][ch].x, acc1, 0, 0, 0);
-            acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(av.y, wb[0][ch].y, acc0, 0, 0, 0);
-            acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(av.y, wb[1][ch].y, acc1, 0, 0, 0);
-            acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(av.z, wb[0][ch].z, acc0, 0, 0, 0);
-            acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(av.z, wb[1][ch].z, acc1, 0, 0, 0);
-            acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(av.w, wb[0][ch].w, acc0, 0, 0, 0);
-            acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(av.w, wb[1][ch].w, acc1, 0, 0, 0);
-        }
-#pragma unroll
-        for (int v = 0; v < 16; ++v) {
-            const int r = 8 * (v >> 2) + 4 * hh + (v & 3);
-            pst[r][64 * wv + cl] = acc0[v];
-            pst[r][64 * wv + 32 + cl] = acc1[v];
-        }
-        __syncthreads();
-        // the partial [RW][H] of this block: 16-B sc1 stores, then publish
-#pragma unroll
-        for (int i = 0; i < 8; ++i) {
+        for (int i = 0; i < HF; ++i) {
             const int f = tid + 256 * i;
-            const int rr = f >> 6, c4 = f & 63;
-            st_sc1(prs, pofs(t & 1, ub, rr, 4 * c4), *reinterpret_cast<const float4 *>(&pst[rr][4 * c4]));
+            *reinterpret_cast<float4 *>(&hsl[f >> 6][4 * (f & 63)]) = hr[i];
         }
-        publish(cnt);
+#pragma unroll
+        for (int i = 0; i < XPT; ++i) {
+            const int f = tid + 256 * i;
+            const int rr = f / (D / 4), c4 = f - rr * (D / 4);
+            if (f < XF) *reinterpret_cast<float4 *>(&xsl[rr][4 * c4]) = xr[i];
+        }
+        __syncthreads();
+        if (t > 0) {
+            f32x16_t acc0 = zero16(), acc1 = zero16();
+#pragma unroll
+            for (int ch = 0; ch < NCK; ++ch) {
+                const float4 av = *reinterpret_cast<const float4 *>(&dgs[cl][8 * ch + 4 * hh]);
+                acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(av.x, wb[0][ch].x, acc0, 0, 0, 0);
+                acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(av.x, wb[1][ch].x, acc1, 0, 0, 0);
+                acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(av.y, wb[0][ch].y, acc0, 0, 0, 0);
+                acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(av.y, wb[1][ch].y, acc1, 0, 0, 0);
+                acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(av.z, wb[0][ch].z, acc0, 0, 0, 0);
+                acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(av.z, wb[1][ch].z, acc1, 0, 0, 0);
+                acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(av.w, wb[0][ch].w, acc0, 0, 0, 0);
+                acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(av.w, wb[1][ch].w, acc1, 0, 0, 0);
+            }
+            // rows whose step t starts a sequence pass no gradient back
+#pragma unroll
+            for (int v = 0; v < 16; ++v) {
+                const int r = 8 * (v >> 2) + 4 * hh + (v & 3);
+                const bool cut = stf[r] != 0;
+                pst[r][64 * wv + cl] = cut ? 0.0f : acc0[v];
+                pst[r][64 * wv + 32 + cl] = cut ? 0.0f : acc1[v];
+            }
+            __syncthreads();
+            // the partial [RW][H] of this block: 16-B sc1 stores, then publish
+#pragma unroll
+            for (int i = 0; i < 8; ++i) {
+                const int f = tid + 256 * i;
+                const int rr = f >> 6, c4 = f & 63;
+                st_sc1(prs, pofs(t & 1, ub, rr, 4 * c4), *reinterpret_cast<const float4 *>(&pst[rr][4 * c4]));
+            }
+            publish(cnt);
+        }
+        // weight gradients of gate wv's 32 rows (while the next hand-off is in flight):
+        // A = dG^T [gate unit][row], B = h_{t-1} / x_t [row][col], K = the 32 rows
+#pragma unroll
+        for (int ks = 0; ks < RW / 2; ++ks) {
+            const int r = 2 * ks + hh;
+            const float av = dgs[r][wv * UBK + cl];
+#pragma unroll
+            for (int j = 0; j < 8; ++j)
+                wacc[j] = __builtin_amdgcn_mfma_f32_32x32x2f32(av, hsl[r][32 * j + cl], wacc[j], 0, 0, 0);
+#pragma unroll
+            for (int j = 0; j < NXT; ++j)
+                xacc[j] = __builtin_amdgcn_mfma_f32_32x32x2f32(av, xsl[r][32 * j + cl], xacc[j], 0, 0, 0);
+        }
+        // (the next step's LDS writes come after its wait barrier, which every
+        // wave reaches only after these reads)
+        if (t == 0) break;
     }
+    // per-row-tile weight-gradient partials: register v of a tile = gate row
+    // 8 (v / 4) + 4 hh + v % 4 of gate wv's 32, column 32 j + cl
+    float *wp = a.wpart + (((size_t)rt * 2 + l) * 4 * H) * (H + D);
+#pragma unroll
+    for (int v = 0; v < 16; ++v) {
+        const int grow = wv * H + u0 + 8 * (v >> 2) + 4 * hh + (v & 3);
+        float *prow = wp + (size_t)grow * (H + D);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) prow[32 * j + cl] = wacc[j][v];
+#pragma unroll
+        for (int j = 0; j < NXT; ++j)
+            if (32 * j + cl < D) prow[H + 32 * j + cl] = xacc[j][v];
+    }
+    // db: the 32 rows' sums (threads of one eq hold a row each), reduced through LDS
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < 4; ++q) *reinterpret_cast<float4 *>(&pst[er][q * UBK + 4 * eq]) = dbs[q];
+    __syncthreads();
+    if (tid < 4 * UBK) {
+        float sum = 0.0f;
+        for (int r = 0; r < RW; ++r) sum += pst[r][tid];
+        a.bpart[((size_t)rt * 2 + l) * 4 * H + (tid >> 5) * H + u0 + (tid & 31)] = sum;
+    }
+}
+
+// out[i] = sum over row tiles (in order) of part[rt][i]
+__global__ void rows_wsum_kernel(const float *__restrict__ part, int nt, int64_t per, float *__restrict__ out) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= per) return;
+    float s = part[i];
+    for (int k = 1; k < nt; ++k) s += part[(int64_t)k * per + i];
+    out[i] = s;
 }
 
 int rows_supported(int D, int H) { return D == 80 && H == 256; }
@@ -442,7 +553,7 @@ int rows_grid_ok(int B, int NT, int *grid) {
     if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return 0;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_fwd, lstm_rows_fwd_kernel<80, 256>, 256, 0) != hipSuccess)
         return 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_bwd, lstm_rows_bwd_kernel<256>, 256, 0) != hipSuccess)
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_bwd, lstm_rows_bwd_kernel<80, 256>, 256, 0) != hipSuccess)
         return 0;
     const int cap = ncu * (per_fwd < per_bwd ? per_fwd : per_bwd);
     return *grid <= cap;
@@ -461,7 +572,8 @@ int vn_lstm_rows_supported(int32_t D, int32_t H, int32_t B) {
 int vn_lstm_rows_part_floats(int32_t B, int64_t *floats) {
     if (!floats || B < 1) return fail(VN_ERR_INVALID, "bad argument");
     const int NT = (B + RW - 1) / RW;
-    *floats = (int64_t)2 * 2 * NT * NUB * RW * 256;
+    // the two partial-dh slots, the per-row-tile [dW_hh | dW_ih] and db partials
+    *floats = (int64_t)2 * 2 * NT * NUB * RW * 256 + (int64_t)NT * 2 * 1024 * (256 + 80) + (int64_t)NT * 2 * 1024;
     return VN_OK;
 }
 
@@ -489,9 +601,9 @@ int vn_lstm_rows_fwd(const float *x, int32_t D, const float *w_ih, const float *
 }
 
 int vn_lstm_rows_bwd(const float *dh_out, const float *w_hh, const float *act, const float *cprev, const float *cnew,
-                     const uint8_t *start, float *dG, float *part, uint32_t *cnt, int32_t *err, int32_t L, int32_t B,
-                     int32_t H, void *stream) {
-    if (!dh_out || !w_hh || !act || !cprev || !cnew || !start || !dG || !part || !cnt || !err)
+                     const float *hprev, const float *x, const uint8_t *start, float *dG, float *dw, float *db,
+                     float *part, uint32_t *cnt, int32_t *err, int32_t L, int32_t B, int32_t H, void *stream) {
+    if (!dh_out || !w_hh || !act || !cprev || !cnew || !hprev || !x || !start || !dw || !db || !part || !cnt || !err)
         return fail(VN_ERR_INVALID, "NULL argument");
     if (!rows_supported(80, H)) return fail(VN_ERR_INVALID, "row-layout LSTM: H 256 only (got %d)", H);
     if (L < 1) return fail(VN_ERR_INVALID, "L < 1");
@@ -500,9 +612,16 @@ int vn_lstm_rows_bwd(const float *dh_out, const float *w_hh, const float *act, c
     if (!rows_grid_ok(B, NT, &grid))
         return fail(VN_ERR_INVALID, "row-layout LSTM: %d blocks are not co-resident (B = %d)", grid, B);
     const hipStream_t st = (hipStream_t)stream;
+    constexpr int D = 80;
+    const size_t slot_f = (size_t)2 * NT * NUB * RW * H;
+    float *wpart = part + 2 * slot_f;
+    float *bpart = wpart + (size_t)NT * 2 * 4 * H * (H + D);
     VN_HIP(hipMemsetAsync(cnt, 0, (size_t)2 * NT * sizeof(uint32_t), st));
-    RowsBwd a{dh_out, w_hh, act, cprev, cnew, start, dG, part, cnt, err, L, B, NT};
-    hipLaunchKernelGGL((lstm_rows_bwd_kernel<256>), dim3((unsigned)grid), dim3(256), 0, st, a);
+    RowsBwd a{dh_out, w_hh, act, cprev, cnew, hprev, x, start, dG, part, wpart, bpart, cnt, err, L, B, NT};
+    hipLaunchKernelGGL((lstm_rows_bwd_kernel<80, 256>), dim3((unsigned)grid), dim3(256), 0, st, a);
+    const int64_t pw = (int64_t)2 * 4 * H * (H + D), pb = (int64_t)2 * 4 * H;
+    hipLaunchKernelGGL(rows_wsum_kernel, dim3((unsigned)((pw + 255) / 256)), dim3(256), 0, st, wpart, NT, pw, dw);
+    hipLaunchKernelGGL(rows_wsum_kernel, dim3((unsigned)((pb + 255) / 256)), dim3(256), 0, st, bpart, NT, pb, db);
     VN_HIP(hipGetLastError());
     return VN_OK;
 }

@@ -93,7 +93,11 @@ def save_checkpoint(path: Union[str, Path], policy, optimizer: Optional[torch.op
         z.writestr("data", json.dumps(data, indent=2))
         z.writestr("policy.pth", blob(sd))
         if optimizer is not None:
-            z.writestr("policy.optimizer.pth", blob(optimizer.state_dict()))
+            osd = optimizer.state_dict()
+            # the learner's fused-kernel flag is an execution choice of this build,
+            # not part of sb3's Adam: saved as torch's default
+            osd["param_groups"] = [{**g, "fused": None} if "fused" in g else g for g in osd["param_groups"]]
+            z.writestr("policy.optimizer.pth", blob(osd))
         z.writestr("pytorch_variables.pth", blob({}))
         z.writestr("_stable_baselines3_version", FORMAT_VERSION)
     return path

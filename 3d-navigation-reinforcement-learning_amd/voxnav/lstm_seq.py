@@ -164,18 +164,23 @@ class _DualLSTMRows(torch.autograd.Function):
         dev = xc.device
         st = _stream(dev)
         dh_out = d_out.contiguous()
-        dG = torch.empty((2, L, B, G), dtype=torch.float32, device=dev)
+        # dG itself only for an input gradient (the learner's x never needs one)
+        need_dx = ctx.needs_input_grad[0]
+        dG = torch.empty((2, L, B, G), dtype=torch.float32, device=dev) if need_dx else None
         nf = C.c_int64()
         _native.check(lib.vn_lstm_rows_part_floats(B, C.byref(nf)), "vn_lstm_rows_part_floats")
         part = torch.empty(nf.value, dtype=torch.float32, device=dev)
         cnt = torch.empty(2 * -(-B // 32), dtype=torch.int32, device=dev)
-        _native.check(lib.vn_lstm_rows_bwd(_p(dh_out), _p(w_hh), _p(act), _p(cprev), _p(cnew), _p(start), _p(dG),
-                                           _p(part), _p(cnt), _p(_rows_err(dev)), L, B, H, st), "vn_lstm_rows_bwd")
-        dGf = dG.view(2, L * B, G)
-        d_w_hh, _ = learn_ops.mm_tn(dGf, hprev.view(2, L * B, H))
-        d_w_ih, db = learn_ops.mm_tn(dGf, xc.view(1, L * B, D).expand(2, L * B, D), colsum=True)
+        # dG and, inside the same persistent launch, [dW_hh | dW_ih] and db
+        dw = torch.empty((2, G, H + D), dtype=torch.float32, device=dev)
+        db = torch.empty((2, G), dtype=torch.float32, device=dev)
+        _native.check(lib.vn_lstm_rows_bwd(_p(dh_out), _p(w_hh), _p(act), _p(cprev), _p(cnew), _p(hprev), _p(xc),
+                                           _p(start), _p(dG), _p(dw), _p(db), _p(part), _p(cnt), _p(_rows_err(dev)),
+                                           L, B, H, st), "vn_lstm_rows_bwd")
+        d_w_hh, d_w_ih = dw[:, :, :H].contiguous(), dw[:, :, H:].contiguous()
         dx = None
-        if ctx.needs_input_grad[0]:
+        if need_dx:
+            dGf = dG.view(2, L * B, G)
             dx = (dGf[0] @ w_ih_a + dGf[1] @ w_ih_c).view(L, B, D)
         return (dx, None, None, None, None, None, d_w_ih[0], d_w_hh[0], db[0].clone(), db[0].clone(), d_w_ih[1],
                 d_w_hh[1], db[1].clone(), db[1].clone())

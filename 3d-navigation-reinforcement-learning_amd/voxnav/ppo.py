@@ -71,7 +71,10 @@ class PPOLearner:
         self.rng = np.random.default_rng(seed)
         self.group = process_group
         self.params = [p for p in policy.parameters() if p.requires_grad]
-        self.optimizer = torch.optim.Adam(self.params, lr=self.lr, eps=1e-5)
+        # on the GPU one fused Adam kernel over all parameters (sb3's Adam, same
+        # update; torch's per-tensor foreach path costs ~9 launches per step)
+        fused = bool(self.params) and all(p.is_cuda for p in self.params)
+        self.optimizer = torch.optim.Adam(self.params, lr=self.lr, eps=1e-5, fused=fused or None)
         self.n_updates = 0
 
     # ------------------------------------------------------------ helpers

@@ -428,8 +428,10 @@ int vn_lstm_seq_bwd_mfma(const float *dh_out, const float *w_hh, float *wpack, c
  *   keep [L][B] (1 - episode_start); out: hout, hprev (the h_{t-1} used), cprev,
  *   cnew [2][L][B][H], act [2][L][B][4H] (i, f, g, o); cnt: 2 * ceil(B / 32) u32
  *   counters (zeroed by the call; 32-row tiles); err: set to 1 if a hand-off timed out.
- * Backward: dh_out [2][L][B][H] -> dG [2][L][B][4H]; part: vn_lstm_rows_part_floats
- * floats of workspace.  vn_lstm_rows_supported: 1 when (D, H, B) can run (every
+ * Backward: dh_out [2][L][B][H] (+ the forward's hprev, cprev, cnew, act and x) ->
+ * dG [2][L][B][4H] (may be NULL) and, accumulated inside the same launch, the weight gradients
+ * dw [2][4H][H + D] = [dW_hh | dW_ih] and db [2][4H] (= d b_ih = d b_hh); part:
+ * vn_lstm_rows_part_floats floats of workspace.  vn_lstm_rows_supported: 1 when (D, H, B) can run (every
  * block co-resident on this device), else 0 (use vn_lstm_seq_*).
  */
 int vn_lstm_rows_supported(int32_t D, int32_t H, int32_t B);
@@ -439,8 +441,8 @@ int vn_lstm_rows_fwd(const float *x, int32_t D, const float *w_ih, const float *
                      const uint8_t *start, const float *keep, float *hout, float *hprev, float *cprev, float *cnew,
                      float *act, uint32_t *cnt, int32_t *err, int32_t L, int32_t B, int32_t H, void *stream);
 int vn_lstm_rows_bwd(const float *dh_out, const float *w_hh, const float *act, const float *cprev, const float *cnew,
-                     const uint8_t *start, float *dG, float *part, uint32_t *cnt, int32_t *err, int32_t L, int32_t B,
-                     int32_t H, void *stream);
+                     const float *hprev, const float *x, const uint8_t *start, float *dG, float *dw, float *db,
+                     float *part, uint32_t *cnt, int32_t *err, int32_t L, int32_t B, int32_t H, void *stream);
 
 /*
  * The learner's matrix products on the f32 matrix cores (csrc/voxnav_gemm_f32.hip):
