@@ -37,8 +37,8 @@ import torch
 from . import _native, learn_ops
 
 
-def _p(t: torch.Tensor):
-    return C.c_void_p(t.data_ptr())
+def _p(t):
+    return None if t is None else C.c_void_p(t.data_ptr())
 
 
 def _stream(dev):
