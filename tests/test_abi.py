@@ -51,3 +51,15 @@ def test_errors_cross_the_boundary_as_codes():
     bad = _native.VnConfig(4, 1, 1, 7, -2.0, 0.84, 0, 0)  # unknown variant
     rc = lib.vn_create(ctypes.byref(rs), 4, ctypes.byref(bad), 0, ctypes.byref(h))
     assert rc == -1 and b"variant" in lib.vn_last_error()
+
+
+def test_bindings_match_header_arity():
+    """Every ctypes binding (voxnav/_native.py) takes as many arguments as
+    its include/voxnav.h declaration (a stale binding passes garbage)."""
+    from voxnav import _native
+    text = re.sub(r"/\*.*?\*/", "", HEADER.read_text(), flags=re.S)
+    for name, (_, args) in _native._SIGS.items():
+        m = re.search(r"\b" + name + r"\s*\(([^)]*)\)\s*;", text)
+        assert m, name
+        params = [p for p in m.group(1).split(",") if p.strip() and p.strip() != "void"]
+        assert len(params) == len(args), (name, len(params), len(args))
