@@ -195,8 +195,10 @@ __global__ __launch_bounds__(256, 1) void lstm_rows_fwd_kernel(RowsFwd a) {
     }
     __syncthreads();
 
+    __shared__ uint8_t stf[RW];       // the tile's sequence-start flags of the step
     for (int t = 0; t < L; ++t) {
         const int xb = t & 1;
+        if (tid < RW) stf[tid] = (row0 + tid < B && (t == 0 || a.start[(size_t)t * B + row0 + tid])) ? 1 : 0;
         float4 xn[XPT];
         if (t + 1 < L) load_x(t + 1, xn);
         // the x part of the product (needs nothing from the group)
@@ -216,24 +218,37 @@ __global__ __launch_bounds__(256, 1) void lstm_rows_fwd_kernel(RowsFwd a) {
             if (tid == 0) wait_ge(cnt, (uint32_t)(NUB * t), a.err);
             __syncthreads();
         }
+        // every row's h_{t-1} from the group's output, all 8 loads in flight at
+        // once (rows past B read row B - 1; a step-0 tile reads nothing) ...
+        float4 hv[8];
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
             const int f = tid + 256 * i;
             const int rr = f >> 6, c4 = f & 63;          // H / 4 = 64 float4 per row
+            const int row = min(row0 + rr, B - 1);
+            hv[i] = t > 0 ? ld_sc1(hrs, (uint32_t)((((size_t)l * L + (t - 1)) * B + row) * H + 4 * c4) * 4u)
+                          : f4(0.0f);
+        }
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            const int f = tid + 256 * i;
+            *reinterpret_cast<float4 *>(&hsl[f >> 6][4 * (f & 63)]) = hv[i];
+        }
+        __syncthreads();
+        // ... then the rows that start a sequence at t (all of them at t = 0)
+        // take the buffer's stored state x keep: one row per 64 threads
+#pragma unroll
+        for (int i = 0; i < RW / 4; ++i) {
+            const int rr = (tid >> 6) + 4 * i, c4 = tid & 63;
             const int row = row0 + rr;
-            float4 v = f4(0.0f);
-            if (row < B) {
+            if (stf[rr]) {
                 const size_t o = (size_t)t * B + row;
-                if (t == 0 || a.start[o]) {
-                    const float k = a.keep[o];
-                    const float4 s = *reinterpret_cast<const float4 *>(
-                        a.h_store + (((size_t)t * 2 + l) * a.n_env + a.env[o]) * H + 4 * c4);
-                    v = s * f4(k);
-                } else {
-                    v = ld_sc1(hrs, (uint32_t)((((size_t)l * L + (t - 1)) * B + row) * H + 4 * c4) * 4u);
-                }
+                const float4 sv = *reinterpret_cast<const float4 *>(
+                    a.h_store + (((size_t)t * 2 + l) * a.n_env + a.env[o]) * H + 4 * c4);
+                *reinterpret_cast<float4 *>(&hsl[rr][4 * c4]) = sv * f4(a.keep[o]);
+            } else if (row >= B) {
+                *reinterpret_cast<float4 *>(&hsl[rr][4 * c4]) = f4(0.0f);
             }
-            *reinterpret_cast<float4 *>(&hsl[rr][4 * c4]) = v;
         }
         __syncthreads();
 #pragma unroll
@@ -255,7 +270,7 @@ __global__ __launch_bounds__(256, 1) void lstm_rows_fwd_kernel(RowsFwd a) {
 #pragma unroll
             for (int q = 0; q < 4; ++q) pre[q] = *reinterpret_cast<const float4 *>(&gts[q][er][4 * eq]) + bs[q];
             float4 cp = cc;
-            if (t == 0 || a.start[o]) {
+            if (stf[er]) {
                 const float k = a.keep[o];
                 cp = *reinterpret_cast<const float4 *>(a.c_store + (((size_t)t * 2 + l) * a.n_env + a.env[o]) * H + eu) *
                      f4(k);
