@@ -339,9 +339,7 @@ __global__ __launch_bounds__(256, 1) void lstm_rows_bwd_kernel(RowsBwd a) {
     constexpr int NCK = GC / 8;   // 16 chunks
     constexpr int DP = GC + 4, PP = H + 4, XP = 96;   // xs padded to 3 tiles of 32 (zeros past D)
     constexpr int NXT = (D + 31) / 32;                 // dW_ih column tiles
-    constexpr int HF = RW * H / 4 / 256;               // float4 of the h tile per thread (8)
-    constexpr int XF = RW * D / 4, XPT = (XF + 255) / 256;
-    static_assert(H == NUB * UBK && D <= XP && D % 4 == 0, "shape");
+    static_assert(H == NUB * UBK && D <= XP && D % 4 == 0 && H == 256 && D / 4 <= 64, "shape: a row per wave load");
     __shared__ __attribute__((aligned(16))) float dgs[RW][DP];
     __shared__ __attribute__((aligned(16))) float pst[RW][PP];
     __shared__ __attribute__((aligned(16))) float hsl[RW][PP];
@@ -396,23 +394,8 @@ __global__ __launch_bounds__(256, 1) void lstm_rows_bwd_kernel(RowsBwd a) {
 
     for (int s = 0; s < L; ++s) {
         const int t = L - 1 - s;
-        // the step's h_{t-1} and x_t rows (weight-gradient operands; rows past B
-        // clamped: their dG is zero), in flight across the hand-off wait
-        float4 hr[HF], xr[XPT];
-#pragma unroll
-        for (int i = 0; i < HF; ++i) {
-            const int f = tid + 256 * i;
-            const int rr = f >> 6, c4 = f & 63;
-            const int row = min(row0 + rr, B - 1);
-            hr[i] = *reinterpret_cast<const float4 *>(a.hprev + (((size_t)l * L + t) * B + row) * H + 4 * c4);
-        }
-#pragma unroll
-        for (int i = 0; i < XPT; ++i) {
-            const int f = tid + 256 * i;
-            const int rr = f / (D / 4), c4 = f - rr * (D / 4);
-            const int row = min(row0 + rr, B - 1);
-            xr[i] = f < XF ? *reinterpret_cast<const float4 *>(a.x + ((size_t)t * B + row) * D + 4 * c4) : f4(0.0f);
-        }
+        // the step's sequence-start flag, loaded ahead of the hand-off wait
+        const bool st_ld = !elive || t == 0 || a.start[(size_t)t * B + erow];
         if (s > 0) {
             if (tid == 0) wait_ge(cnt, (uint32_t)(NUB * s), a.err);
             __syncthreads();
@@ -420,8 +403,7 @@ __global__ __launch_bounds__(256, 1) void lstm_rows_bwd_kernel(RowsBwd a) {
         float4 dG4[4] = {f4(0.0f), f4(0.0f), f4(0.0f), f4(0.0f)};
         bool st = true;
         if (elive) {
-            const size_t o = (size_t)t * B + erow;
-            st = t == 0 || a.start[o];
+            st = st_ld;
             float4 dhr = f4(0.0f);
             if (s > 0) {
                 // the 8 partials of step t+1 (sc1 loads), summed in unit-block order
@@ -458,22 +440,11 @@ __global__ __launch_bounds__(256, 1) void lstm_rows_bwd_kernel(RowsBwd a) {
 #pragma unroll
             for (int q = 0; q < 4; ++q) dbs[q] = dbs[q] + dG4[q];
         }
-        // dG (the weight-gradient and the partial product's A operand), the
-        // sequence-start flags, h_{t-1} and x_t to LDS
+        // dG (the partial product's and the weight gradients' A operand) and
+        // the sequence-start flags to LDS
 #pragma unroll
         for (int q = 0; q < 4; ++q) *reinterpret_cast<float4 *>(&dgs[er][q * UBK + 4 * eq]) = dG4[q];
         if (eq == 0) stf[er] = st ? 1 : 0;
-#pragma unroll
-        for (int i = 0; i < HF; ++i) {
-            const int f = tid + 256 * i;
-            *reinterpret_cast<float4 *>(&hsl[f >> 6][4 * (f & 63)]) = hr[i];
-        }
-#pragma unroll
-        for (int i = 0; i < XPT; ++i) {
-            const int f = tid + 256 * i;
-            const int rr = f / (D / 4), c4 = f - rr * (D / 4);
-            if (f < XF) *reinterpret_cast<float4 *>(&xsl[rr][4 * c4]) = xr[i];
-        }
         __syncthreads();
         if (t > 0) {
             f32x16_t acc0 = zero16(), acc1 = zero16();
@@ -507,6 +478,25 @@ __global__ __launch_bounds__(256, 1) void lstm_rows_bwd_kernel(RowsBwd a) {
             }
             publish(cnt);
         }
+        // the step's h_{t-1} and x_t rows (the weight gradients' B operands; rows
+        // past B clamped: their dG is zero), copied global -> LDS directly (no
+        // registers: the kernel sits at the VGPR cap, and register staging made
+        // the compiler serialise the loads), after the publish -- off the
+        // recurrence's critical path.  One wave instruction = one row.
+#pragma unroll
+        for (int i = 0; i < RW / 4; ++i) {
+            const int rr = (RW / 4) * wv + i;
+            const int row = min(row0 + rr, B - 1);
+            __builtin_amdgcn_global_load_lds(
+                (const __attribute__((address_space(1))) void *)(a.hprev + (((size_t)l * L + t) * B + row) * H + 4 * lane),
+                (__attribute__((address_space(3))) void *)&hsl[rr][0], 16, 0, 0);
+            if (lane < D / 4)
+                __builtin_amdgcn_global_load_lds(
+                    (const __attribute__((address_space(1))) void *)(a.x + ((size_t)t * B + row) * D + 4 * lane),
+                    (__attribute__((address_space(3))) void *)&xsl[rr][0], 16, 0, 0);
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
         // weight gradients of gate wv's 32 rows (while the next hand-off is in flight):
         // A = dG^T [gate unit][row], B = h_{t-1} / x_t [row][col], K = the 32 rows
 #pragma unroll
