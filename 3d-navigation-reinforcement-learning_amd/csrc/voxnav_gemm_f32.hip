@@ -34,12 +34,10 @@ namespace {
 typedef __attribute__((ext_vector_type(16))) float f32x16_t;
 
 constexpr int GT = 128;        // tile rows / cols
-#ifndef VN_GEMM_GK
-#define VN_GEMM_GK 32
-#endif
-constexpr int GK = VN_GEMM_GK;  // K per chunk (A/B knob: 16 or 32)
-constexpr int GNF = GK * GT / 4 / 256;   // float4 of one operand chunk per thread
-constexpr int GKQ = GK / 4;               // float4 per row of a row-major chunk
+// K per chunk: 16 for the Linear forward and dX products (K = 80 .. 256:
+// half the LDS, 4 waves per SIMD; measured 10-38 % faster than 32), 32 for the
+// split-K weight gradients (long K per split; 16 measured no faster there)
+constexpr int GK_LIN = 16, GK_TN = 32;
 constexpr int GP = GT + 4;     // LDS pitch
 
 __device__ __forceinline__ f32x16_t zero16() {
@@ -57,12 +55,14 @@ struct GemmArgs {
     float *colsum;         // optional (AGRAD, A k-major): split partials of sum_k A[k][m], [splits][M]
     int64_t lda, ldb, ldc;
     int64_t sa, sb, sc, sbias;   // batch strides (blockIdx.y = batch)
-    int M, N, K, kper;     // kper: K per split (multiple of GK, except the last split)
+    int M, N, K, kper;     // kper: K per split (multiple of GK_TN, except the last split)
 };
 
 // EPI: 0 store, 1 tanh(acc + bias), 2 acc + bias, 3 split partial (c + split * M * N)
-template <bool A_KM, bool B_KM, bool AGRAD, int EPI>
+template <int GK, bool A_KM, bool B_KM, bool AGRAD, int EPI>
 __global__ __launch_bounds__(256, 2) void gemm_f32_kernel(GemmArgs g) {
+    constexpr int GNF = GK * GT / 4 / 256;   // float4 of one operand chunk per thread
+    constexpr int GKQ = GK / 4;              // float4 per row of a row-major chunk
     __shared__ float As[2][GK][GP];
     __shared__ float Bs[2][GK][GP];
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
@@ -298,7 +298,7 @@ __global__ __launch_bounds__(256) void gemm_reduce_kernel(const float *__restric
 template <bool A_KM, bool B_KM, bool AGRAD, int EPI>
 void launch(const GemmArgs &g, int batch, int splits, hipStream_t s) {
     const int tiles = ((g.M + GT - 1) / GT) * ((g.N + GT - 1) / GT);
-    hipLaunchKernelGGL((gemm_f32_kernel<A_KM, B_KM, AGRAD, EPI>), dim3((unsigned)tiles, (unsigned)batch,
+    hipLaunchKernelGGL((gemm_f32_kernel<EPI == 3 ? GK_TN : GK_LIN, A_KM, B_KM, AGRAD, EPI>), dim3((unsigned)tiles, (unsigned)batch,
                                                                         (unsigned)splits),
                        dim3(256), 0, s, g);
 }
@@ -357,7 +357,7 @@ int vn_gemm_f32_tn(const float *dy, const float *y, int64_t ldd, int64_t sd, con
     if (M < 1 || N < 1 || K < 1 || batch < 1 || splits < 1) return fail(VN_ERR_INVALID, "bad sizes");
     if (sc != (int64_t)M * N) return fail(VN_ERR_INVALID, "C must be contiguous [batch][M][N]");
     int kper = (K + splits - 1) / splits;
-    kper = (kper + GK - 1) / GK * GK;
+    kper = (kper + GK_TN - 1) / GK_TN * GK_TN;
     splits = (K + kper - 1) / kper;
     GemmArgs g{};
     g.a = dy; g.a2 = y; g.b = b; g.c = workspace; g.colsum = colsum ? workspace2 : nullptr;
