@@ -154,10 +154,13 @@ def linear(x: torch.Tensor, module: torch.nn.Linear) -> torch.Tensor:
 
 
 def mlp_pair(pi_net: torch.nn.Sequential, vf_net: torch.nn.Sequential, x_pi: torch.Tensor,
-             x_vf: Optional[torch.Tensor] = None) -> Tuple[torch.Tensor, torch.Tensor]:
+             x_vf: Optional[torch.Tensor] = None, x_pair: Optional[torch.Tensor] = None
+             ) -> Tuple[torch.Tensor, torch.Tensor]:
     """Both SB3 MLP branches (Linear + Tanh layers of equal widths) layer by
     layer, the two branches of a layer in one launch.  ``x_vf is None``: both
-    read ``x_pi`` (MlpPolicy's observation)."""
+    read ``x_pi`` (MlpPolicy's observation).  ``x_pair`` [2, M, K]: the two
+    branches' inputs already stacked (the row-layout LSTM's output), used
+    as is -- no stacking copy forward, no gradient accumulation backward."""
     def tanh_layers(seq):   # [Linear, Tanh] * n, or None
         mods = list(seq)
         if len(mods) % 2 or not all(isinstance(a, torch.nn.Linear) and a.bias is not None and
@@ -165,10 +168,12 @@ def mlp_pair(pi_net: torch.nn.Sequential, vf_net: torch.nn.Sequential, x_pi: tor
             return None
         return mods[0::2]
     lin_pi, lin_vf = tanh_layers(pi_net), tanh_layers(vf_net)
+    if x_pair is not None:
+        x_pi, x_vf = x_pair[0], x_pair[1]
     if (x_pi.device.type != "cuda" or lin_pi is None or lin_vf is None or len(lin_pi) != len(lin_vf) or
             any(a.weight.shape != b.weight.shape for a, b in zip(lin_pi, lin_vf))):
         return pi_net(x_pi), vf_net(x_pi if x_vf is None else x_vf)
-    h = x_pi if x_vf is None else torch.stack([x_pi, x_vf])
+    h = x_pair if x_pair is not None else (x_pi if x_vf is None else torch.stack([x_pi, x_vf]))
     for a, b in zip(lin_pi, lin_vf):
         w = torch.stack([a.weight, b.weight])
         bb = torch.stack([a.bias, b.bias])

@@ -213,6 +213,14 @@ def rows_supported(policy, D: int, B: int) -> bool:
     return bool(_native.load().vn_lstm_rows_supported(D, la.hidden_size, B))
 
 
+def dual_lstm_rows_pair(policy, x: torch.Tensor, env: torch.Tensor, start: torch.Tensor, keep: torch.Tensor,
+                        h_store: torch.Tensor, c_store: torch.Tensor) -> torch.Tensor:
+    """``dual_lstm_rows`` as one stacked [2, L, B, H] tensor (actor, critic)."""
+    la, lc = policy.lstm_actor, policy.lstm_critic
+    return _DualLSTMRows.apply(x, env, start, keep, h_store, c_store, la.weight_ih_l0, la.weight_hh_l0, la.bias_ih_l0,
+                               la.bias_hh_l0, lc.weight_ih_l0, lc.weight_hh_l0, lc.bias_ih_l0, lc.bias_hh_l0)
+
+
 def dual_lstm_rows(policy, x: torch.Tensor, env: torch.Tensor, start: torch.Tensor, keep: torch.Tensor,
                    h_store: torch.Tensor, c_store: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
     """(out_actor, out_critic), each [L, B, H], of ``policy.lstm_actor`` /

@@ -95,12 +95,13 @@ class PPOLearner:
             g.copy_(flat[o:o + n].view_as(g))
             o += n
 
-    def _heads(self, lat_pi, lat_vf, actions):
+    def _heads(self, lat_pi, lat_vf, actions, lat_pair=None):
         pol = self.policy
         # both MLP branches layer by layer and the heads on the f32 matrix
         # cores (voxnav/learn_ops.py; torch's own ops on the CPU)
         ex = pol.mlp_extractor
-        h_pi, h_vf = learn_ops.mlp_pair(ex.policy_net, ex.value_net, lat_pi, None if lat_vf is lat_pi else lat_vf)
+        h_pi, h_vf = learn_ops.mlp_pair(ex.policy_net, ex.value_net, lat_pi, None if lat_vf is lat_pi else lat_vf,
+                                        x_pair=lat_pair)
         logits = learn_ops.linear(h_pi, pol.action_net)
         values = learn_ops.linear(h_vf, pol.value_net).flatten()
         logp_all = torch.log_softmax(logits, dim=-1)
@@ -203,11 +204,12 @@ class PPOLearner:
         src = pk["src"]
         D = buf.obs.shape[-1]
         x = buf.obs.reshape(T * N, D)[src].view(T, rows, D)
-        out_pi, out_vf = lstm_seq.dual_lstm_rows(self.policy, x, pk["env"], pk["start"], pk["keep"], buf.lstm_h,
-                                                 buf.lstm_c)
-        H = out_pi.shape[-1]
+        out = lstm_seq.dual_lstm_rows_pair(self.policy, x, pk["env"], pk["start"], pk["keep"], buf.lstm_h,
+                                           buf.lstm_c)                       # [2, T, rows, H]: actor, critic
+        H = out.shape[-1]
+        lat = out.view(2, T * rows, H)
         acts = buf.actions.reshape(-1)[src].long()
-        return self._heads(out_pi.reshape(T * rows, H), out_vf.reshape(T * rows, H), acts), src
+        return self._heads(lat[0], lat[1], acts, lat_pair=lat), src
 
     def _evaluate_recurrent(self, buf, pk: dict):
         """evaluate_actions on a packed minibatch (``_pack_begin``)."""
