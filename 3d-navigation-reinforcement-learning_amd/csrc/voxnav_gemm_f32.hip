@@ -24,6 +24,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <cstdlib>
 
 #include "vn_common.h"
 
@@ -295,12 +296,216 @@ __global__ __launch_bounds__(256) void gemm_reduce_kernel(const float *__restric
     }
 }
 
+// ----------------------------------------------------------------------------
+// Direct-load variant (the aligned shapes of the learner: K per split a
+// multiple of GKD, 16-B aligned rows, 4-aligned k-major column counts).  Same
+// 128 x 128 block tile and 2 x 2 32x32x2 accumulators per wave, but the
+// operand chunks go global -> LDS with global_load_lds (16 B per lane, no
+// register staging, no LDS store instructions, no per-chunk address
+// arithmetic beyond one add), double-buffered.  LDS layouts (16-B units):
+//   row-major operand  [row][GKD/4 units] with the unit index XOR-swizzled
+//     by the row (u ^ (row / (16 / NU)) % NU), so a fragment read -- 32 rows,
+//     one unit each, ds_read_b128 -- hits 16 distinct bank groups per 16 lanes;
+//     one read carries 4 k-steps of the lane's row;
+//   k-major operand    [k][32 units] with the unit XOR-swizzled by 8 on every
+//     other group of 4 k (the two lane halves of a b32 read then hit disjoint
+//     banks).
+// The k order inside a chunk is permuted identically for both operands (lane
+// half kh at k-step s takes k = 4 (kh + 2 (s / 4)) + s % 4), which is a
+// reordering of the dot product's terms only.  With AGRAD the Y tile is
+// staged beside dY and dZ = dY (1 - Y^2) is formed on the fragment read.
+template <int GKD, bool A_KM, bool B_KM, bool AGRAD, int EPI>
+__global__ __launch_bounds__(256, 2) void gemm_dl_kernel(GemmArgs g) {
+    constexpr int NU = GKD / 4;              // units per row of a row-major chunk
+    constexpr int UNITS = GT * NU;           // 16-B units per operand chunk
+    constexpr int PER = UNITS / 256;         // units per thread per operand
+    constexpr int RPB = 16 / NU;             // rows per 16-unit bank cycle
+    __shared__ float4 sA[2][UNITS], sB[2][UNITS];
+    __shared__ float4 sY[AGRAD ? 2 : 1][AGRAD ? UNITS : 1];
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const int ntn = (g.N + GT - 1) / GT;
+    const int nblk = (int)(gridDim.x * gridDim.y * gridDim.z);
+    int vb = (int)(blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z));
+    if ((nblk & 7) == 0) vb = (vb & 7) * (nblk >> 3) + (vb >> 3);
+    const int tiles = (int)gridDim.x;
+    const int tm = (vb % tiles) / ntn, tn = (vb % tiles) - tm * ntn;
+    const int bt = (vb / tiles) % (int)gridDim.y, split = vb / (tiles * (int)gridDim.y);
+    const int m0 = tm * GT, n0 = tn * GT;
+    const int k0 = split * g.kper;
+    const int k1 = min(g.K, k0 + g.kper);
+    const int nchunks = (k1 - k0) / GKD;
+    const float *A = g.a + bt * g.sa;
+    const float *Y = AGRAD ? g.a2 + bt * g.sa : nullptr;
+    const float *Bm = g.b + bt * g.sb;
+
+    // this thread's source offsets (floats, at chunk k = k0) for its PER units of each operand
+    int64_t oa[PER], ob[PER];
+    auto src_off = [&](bool km, int p, int base, int lim, int64_t ld) -> int64_t {
+        if (km) {            // [k][cols]: p = k * 32 + swizzled unit
+            const int k = p >> 5, u = (p & 31) ^ (8 * ((k >> 2) & 1));
+            const int c = min(base + 4 * u, lim - 4);
+            return (int64_t)(k0 + k) * ld + c;
+        }
+        const int r = p / NU, u = (p % NU) ^ ((r / RPB) % NU);
+        const int rr = min(base + r, lim - 1);
+        return (int64_t)rr * ld + k0 + 4 * u;
+    };
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+        const int p = (i * 4 + wv) * 64 + lane;
+        oa[i] = src_off(A_KM, p, m0, g.M, g.lda);
+        ob[i] = src_off(B_KM, p, n0, g.N, g.ldb);
+    }
+    const int64_t stepA = A_KM ? (int64_t)GKD * g.lda : GKD, stepB = B_KM ? (int64_t)GKD * g.ldb : GKD;
+    auto issue = [&](int ch, int st) {
+#pragma unroll
+        for (int i = 0; i < PER; ++i) {
+            const int w0 = (i * 4 + wv) * 64;
+            __builtin_amdgcn_global_load_lds(
+                (const __attribute__((address_space(1))) void *)(A + oa[i] + ch * stepA),
+                (__attribute__((address_space(3))) void *)&sA[st][w0], 16, 0, 0);
+            if (AGRAD)
+                __builtin_amdgcn_global_load_lds(
+                    (const __attribute__((address_space(1))) void *)(Y + oa[i] + ch * stepA),
+                    (__attribute__((address_space(3))) void *)&sY[st][w0], 16, 0, 0);
+            __builtin_amdgcn_global_load_lds(
+                (const __attribute__((address_space(1))) void *)(Bm + ob[i] + ch * stepB),
+                (__attribute__((address_space(3))) void *)&sB[st][w0], 16, 0, 0);
+        }
+    };
+
+    f32x16_t acc[2][2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[i][j] = zero16();
+    const int wr = 64 * (wv & 1), wc = 64 * (wv >> 1);
+    const int col = lane & 31, kh = lane >> 5;
+    // column sums of dZ (k-major A; the bias gradient of dW): waves with wc == 0
+    // cover every A column of the tile once, each lane half its k's
+    float csum[2] = {0.0f, 0.0f};
+    const bool do_cs = g.colsum && A_KM && tn == 0 && wc == 0;
+
+    if (nchunks > 0) issue(0, 0);
+    for (int ch = 0; ch < nchunks; ++ch) {
+        const int st = ch & 1;
+        if (ch + 1 < nchunks) {
+            __syncthreads();               // every wave is done reading stage st ^ 1 (chunk ch - 1)
+            issue(ch + 1, st ^ 1);
+            if (AGRAD) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(3 * PER) : "memory");
+            else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * PER) : "memory");
+        } else {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        __syncthreads();                   // chunk ch is in LDS for every wave
+        const float *fA = reinterpret_cast<const float *>(sA[st]);
+        const float *fB = reinterpret_cast<const float *>(sB[st]);
+        const float *fY = AGRAD ? reinterpret_cast<const float *>(sY[st]) : nullptr;
+        // operand value of fragment f (rows / cols base + 32 f + col) at k-step s
+        auto rm_unit = [&](const float4 *T, int r, int u) { return T[r * NU + (u ^ ((r / RPB) % NU))]; };
+        auto km_val = [&](const float *T, int c, int s) {
+            const int k = 4 * (kh + 2 * (s >> 2)) + (s & 3);
+            return T[(k * 32 + ((c >> 2) ^ (8 * kh))) * 4 + (c & 3)];
+        };
+#pragma unroll
+        for (int sq = 0; sq < GKD / 8; ++sq) {      // 4 k-steps per pass (one row-major unit)
+            float av[2][4], bv[2][4];
+#pragma unroll
+            for (int f = 0; f < 2; ++f) {
+                if (!A_KM) {
+                    const int r = wr + 32 * f + col;
+                    float4 v = rm_unit(sA[st], r, kh + 2 * sq);
+                    if (AGRAD) {
+                        const float4 y = rm_unit(sY[st], r, kh + 2 * sq);
+                        v.x = v.x * (1.0f - y.x * y.x);
+                        v.y = v.y * (1.0f - y.y * y.y);
+                        v.z = v.z * (1.0f - y.z * y.z);
+                        v.w = v.w * (1.0f - y.w * y.w);
+                    }
+                    av[f][0] = v.x; av[f][1] = v.y; av[f][2] = v.z; av[f][3] = v.w;
+                } else {
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) {
+                        float v = km_val(fA, wr + 32 * f + col, 4 * sq + e);
+                        if (AGRAD) {
+                            const float y = km_val(fY, wr + 32 * f + col, 4 * sq + e);
+                            v = v * (1.0f - y * y);
+                        }
+                        av[f][e] = v;
+                        if (do_cs) csum[f] += v;
+                    }
+                }
+                if (!B_KM) {
+                    const float4 v = rm_unit(sB[st], wc + 32 * f + col, kh + 2 * sq);
+                    bv[f][0] = v.x; bv[f][1] = v.y; bv[f][2] = v.z; bv[f][3] = v.w;
+                } else {
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) bv[f][e] = km_val(fB, wc + 32 * f + col, 4 * sq + e);
+                }
+            }
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[0][e], bv[0][e], acc[0][0], 0, 0, 0);
+                acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[0][e], bv[1][e], acc[0][1], 0, 0, 0);
+                acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[1][e], bv[0][e], acc[1][0], 0, 0, 0);
+                acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[1][e], bv[1][e], acc[1][1], 0, 0, 0);
+            }
+        }
+        (void)fA; (void)fB; (void)fY;
+    }
+    if (g.colsum && A_KM && tn == 0) {   // (block-uniform) lanes l, l ^ 32 hold the two k halves of column wr + 32 f + l % 32
+        if (do_cs) {
+#pragma unroll
+            for (int f = 0; f < 2; ++f) {
+                const float t = csum[f] + __shfl_xor(csum[f], 32, 64);
+                const int m = m0 + wr + 32 * f + col;
+                if (kh == 0 && m < g.M) g.colsum[((int64_t)split * gridDim.y + bt) * g.M + m] = t;
+            }
+        }
+    }
+    float *C = g.c + bt * g.sc;
+    if (EPI == 3) C = g.c + ((int64_t)split * gridDim.y + bt) * (int64_t)g.M * g.N;
+    const int64_t ldc = EPI == 3 ? g.N : g.ldc;
+    const bool full = m0 + GT <= g.M && n0 + GT <= g.N;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+        const int n = n0 + wc + 32 * j + col;
+        if (!full && n >= g.N) continue;
+        const float bv = (EPI == 1 || EPI == 2) ? g.bias[bt * g.sbias + n] : 0.0f;
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int v = 0; v < 16; ++v) {
+                const int m = m0 + wr + 32 * i + 8 * (v >> 2) + 4 * kh + (v & 3);
+                if (!full && m >= g.M) continue;
+                float r = acc[i][j][v];
+                if (EPI == 1) r = tanhf(r + bv);
+                else if (EPI == 2) r = r + bv;
+                C[(int64_t)m * ldc + n] = r;
+            }
+    }
+}
+
 template <bool A_KM, bool B_KM, bool AGRAD, int EPI>
 void launch(const GemmArgs &g, int batch, int splits, hipStream_t s) {
     const int tiles = ((g.M + GT - 1) / GT) * ((g.N + GT - 1) / GT);
-    hipLaunchKernelGGL((gemm_f32_kernel<EPI == 3 ? GK_TN : GK_LIN, A_KM, B_KM, AGRAD, EPI>), dim3((unsigned)tiles, (unsigned)batch,
-                                                                        (unsigned)splits),
-                       dim3(256), 0, s, g);
+    const dim3 grid((unsigned)tiles, (unsigned)batch, (unsigned)splits);
+    // the direct-load kernel takes 16-B aligned operands whose K per split is
+    // a whole number of chunks (VN_GEMM_DL=0: the register-staged kernel, A/B knob)
+    constexpr int GKD = 16;
+    auto al = [](const void *p) { return ((uintptr_t)p & 15) == 0; };
+    static const bool dl_on = [] {
+        const char *e = getenv("VN_GEMM_DL");
+        return !(e && e[0] == '0');
+    }();
+    const bool dl = dl_on && g.K % GKD == 0 && g.kper % GKD == 0 && g.lda % 4 == 0 && g.ldb % 4 == 0 &&
+                    g.sa % 4 == 0 && g.sb % 4 == 0 && al(g.a) && al(g.b) && (!AGRAD || al(g.a2)) &&
+                    (!A_KM || g.M % 4 == 0) && (!B_KM || g.N % 4 == 0);
+    if (dl)
+        hipLaunchKernelGGL((gemm_dl_kernel<GKD, A_KM, B_KM, AGRAD, EPI>), grid, dim3(256), 0, s, g);
+    else
+        hipLaunchKernelGGL((gemm_f32_kernel<EPI == 3 ? GK_TN : GK_LIN, A_KM, B_KM, AGRAD, EPI>), grid, dim3(256), 0,
+                           s, g);
 }
 
 }  // namespace

@@ -21,7 +21,7 @@ LIBDIR = PKG / "_lib"
 LIB = LIBDIR / "libvoxnav.so"
 SOURCES = [CSRC / "voxnav_env.hip", CSRC / "voxnav_simple.hip", CSRC / "voxnav_collect.hip",
            CSRC / "voxnav_learn_f32.hip", CSRC / "voxnav_learn_rows.hip", CSRC / "voxnav_gemm_f32.hip",
-           CSRC / "voxnav_policy_f32.hip"]
+           CSRC / "voxnav_policy_f32.hip", CSRC / "voxnav_ppo_loss.hip"]
 HEADERS = [INCLUDE / "voxnav.h", CSRC / "vn_common.h", CSRC / "env_core.h"]
 ARCH = os.environ.get("VOXNAV_ARCH", "gfx950")
 
@@ -70,10 +70,12 @@ def _compile_link(out: Path, defines=(), verbose: bool = False) -> Path:
 
 
 def build_variant(name: str, defines=(), verbose: bool = False) -> Path:
-    """A differently-configured build (-D flags) under _lib/variants/ for A/B timing."""
+    """A differently-configured build (-D flags) under _lib/variants/ for A/B
+    timing: the diagnostics build (VN_DIAG), the only one whose compile-time
+    knobs may differ from the product's defaults (csrc/vn_common.h)."""
     out = LIBDIR / "variants" / f"libvoxnav_{name}.so"
     out.parent.mkdir(parents=True, exist_ok=True)
-    return _compile_link(out, defines, verbose)
+    return _compile_link(out, ("VN_DIAG", *defines), verbose)
 
 
 def build(force: bool = False, verbose: bool = False) -> Path:

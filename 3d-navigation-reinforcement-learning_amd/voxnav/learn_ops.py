@@ -69,29 +69,42 @@ def mm_tn(a: torch.Tensor, b: torch.Tensor, y: Optional[torch.Tensor] = None, co
     return out, cs
 
 
+def _pair_stride(a: torch.Tensor, b: torch.Tensor) -> int:
+    """Element offset from tensor a to tensor b (same shape, contiguous f32):
+    the kernels' batch stride, so the two branches' parameters are read in
+    place instead of stacked into a [2, ...] copy every minibatch."""
+    d = b.data_ptr() - a.data_ptr()
+    if d % 4 or a.shape != b.shape or not (a.is_contiguous() and b.is_contiguous()):
+        raise ValueError("pair operands must be contiguous f32 tensors of one shape")
+    return d // 4
+
+
 class _LinearTanhPair(torch.autograd.Function):
     """y[br] = tanh(x[br] W[br]^T + b[br]) for br in (pi, vf): x [2, M, K]
-    (batch stride 0 when both branches read the same input), W [2, N, K], b [2, N]."""
+    (batch stride 0 when both branches read the same input), W_pi, W_vf
+    [N, K], b_pi, b_vf [N] (read in place: the batch stride is the distance
+    between the two tensors)."""
 
     @staticmethod
-    def forward(ctx, x, w, b, tanh: bool):
+    def forward(ctx, x, wa, wb, ba, bb, tanh: bool):
         lib = _native.load()
         _, M, K = x.shape
-        N = w.shape[1]
+        N = wa.shape[0]
         dev = x.device
         y = torch.empty((2, M, N), dtype=torch.float32, device=dev)
-        _native.check(lib.vn_gemm_f32_linear(_p(x), K, x.stride(0), _p(w), K, N * K, _p(b), N, _p(y), N, M * N, M, N,
+        sw, sb = _pair_stride(wa, wb), _pair_stride(ba, bb)
+        _native.check(lib.vn_gemm_f32_linear(_p(x), K, x.stride(0), _p(wa), K, sw, _p(ba), sb, _p(y), N, M * N, M, N,
                                              K, 2, 1 if tanh else 0, _stream(dev)), "vn_gemm_f32_linear")
-        ctx.save_for_backward(x, w, y)
+        ctx.save_for_backward(x, wa, wb, y)
         ctx.tanh = tanh
         return y
 
     @staticmethod
     def backward(ctx, dy):
         lib = _native.load()
-        x, w, y = ctx.saved_tensors
+        x, wa, wb, y = ctx.saved_tensors
         _, M, K = x.shape
-        N = w.shape[1]
+        N = wa.shape[0]
         dev = x.device
         st = _stream(dev)
         dy = dy.contiguous()
@@ -100,20 +113,25 @@ class _LinearTanhPair(torch.autograd.Function):
         if ctx.needs_input_grad[0]:
             dx = torch.empty((2, M, K), dtype=torch.float32, device=dev)
             # dX = dZ W: W [N][K] row-major is the k-major operand of this product
-            _native.check(lib.vn_gemm_f32_dx(_p(dy), _p(yy), N, M * N, _p(w), K, N * K, _p(dx), K, M * K, M, K, N, 2,
-                                             st), "vn_gemm_f32_dx")
+            _native.check(lib.vn_gemm_f32_dx(_p(dy), _p(yy), N, M * N, _p(wa), K, _pair_stride(wa, wb), _p(dx), K,
+                                             M * K, M, K, N, 2, st), "vn_gemm_f32_dx")
             # (a shared input was expanded outside: expand's backward sums the branches)
         dw, db = mm_tn(dy, x, y=yy, colsum=True)
-        return dx, dw, db, None
+        return dx, dw[0], dw[1], db[0], db[1], None
 
 
-def linear_tanh_pair(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor, tanh: bool = True) -> torch.Tensor:
-    """x [2, M, K] (or [M, K], shared by both branches), w [2, N, K], b [2, N] -> [2, M, N]."""
+def linear_tanh_pair(x: torch.Tensor, w, b, tanh: bool = True) -> torch.Tensor:
+    """x [2, M, K] (or [M, K], shared by both branches); w = (W_pi, W_vf) [N, K]
+    each (or one stacked [2, N, K]), b = (b_pi, b_vf) [N] (or [2, N]) -> [2, M, N]."""
     if x.dim() == 2:
         x = x.contiguous().unsqueeze(0).expand(2, *x.shape)
     elif not x.is_contiguous():
         x = x.contiguous()
-    return _LinearTanhPair.apply(x, w, b, tanh)
+    if isinstance(w, torch.Tensor):
+        w = (w[0], w[1])
+    if isinstance(b, torch.Tensor):
+        b = (b[0], b[1])
+    return _LinearTanhPair.apply(x, w[0], w[1], b[0], b[1], tanh)
 
 
 class _Linear(torch.autograd.Function):
@@ -154,13 +172,14 @@ def linear(x: torch.Tensor, module: torch.nn.Linear) -> torch.Tensor:
 
 
 def mlp_pair(pi_net: torch.nn.Sequential, vf_net: torch.nn.Sequential, x_pi: torch.Tensor,
-             x_vf: Optional[torch.Tensor] = None, x_pair: Optional[torch.Tensor] = None
-             ) -> Tuple[torch.Tensor, torch.Tensor]:
+             x_vf: Optional[torch.Tensor] = None, x_pair: Optional[torch.Tensor] = None, stacked: bool = False):
     """Both SB3 MLP branches (Linear + Tanh layers of equal widths) layer by
     layer, the two branches of a layer in one launch.  ``x_vf is None``: both
     read ``x_pi`` (MlpPolicy's observation).  ``x_pair`` [2, M, K]: the two
     branches' inputs already stacked (the row-layout LSTM's output), used
-    as is -- no stacking copy forward, no gradient accumulation backward."""
+    as is -- no stacking copy forward, no gradient accumulation backward.
+    Returns (h_pi, h_vf); with ``stacked`` the [2, M, F] pair itself, or None
+    when the branches do not take the paired kernels."""
     def tanh_layers(seq):   # [Linear, Tanh] * n, or None
         mods = list(seq)
         if len(mods) % 2 or not all(isinstance(a, torch.nn.Linear) and a.bias is not None and
@@ -172,10 +191,61 @@ def mlp_pair(pi_net: torch.nn.Sequential, vf_net: torch.nn.Sequential, x_pi: tor
         x_pi, x_vf = x_pair[0], x_pair[1]
     if (x_pi.device.type != "cuda" or lin_pi is None or lin_vf is None or len(lin_pi) != len(lin_vf) or
             any(a.weight.shape != b.weight.shape for a, b in zip(lin_pi, lin_vf))):
+        if stacked:
+            return None
         return pi_net(x_pi), vf_net(x_pi if x_vf is None else x_vf)
     h = x_pair if x_pair is not None else (x_pi if x_vf is None else torch.stack([x_pi, x_vf]))
     for a, b in zip(lin_pi, lin_vf):
-        w = torch.stack([a.weight, b.weight])
-        bb = torch.stack([a.bias, b.bias])
-        h = linear_tanh_pair(h, w, bb, tanh=True)
-    return h[0], h[1]
+        h = linear_tanh_pair(h, (a.weight, b.weight), (a.bias, b.bias), tanh=True)
+    return h if stacked else (h[0], h[1])
+
+
+def ppo_loss_supported(action_net: torch.nn.Linear, value_net: torch.nn.Linear, F: int) -> bool:
+    """The fused loss kernel takes these heads (F = latent width)."""
+    return (F % 64 == 0 and 64 <= F <= 256 and action_net.in_features == F and value_net.in_features == F and
+            value_net.out_features == 1 and 1 <= action_net.out_features <= 8 and action_net.bias is not None and
+            value_net.bias is not None)
+
+
+def ppo_loss(h: torch.Tensor, action_net: torch.nn.Linear, value_net: torch.nn.Linear, src: Optional[torch.Tensor],
+             actions: torch.Tensor, advantages: torch.Tensor, old_log_prob: torch.Tensor, returns: torch.Tensor,
+             clip_range: float, ent_coef: float, vf_coef: float, normalize_advantage: bool):
+    """The PPO minibatch loss and its gradient (csrc/voxnav_ppo_loss.hip): the
+    heads, the advantage normalisation, the clipped surrogate, value MSE and
+    entropy bonus of sb3 (Recurrent)PPO.train, in three launches.
+
+    h [2, M, F]: the (actor, critic) latents; src [M] int64 (or None): the
+    samples' rows in the flat rollout buffers ``actions`` (int32),
+    ``advantages``, ``old_log_prob``, ``returns``.  Returns (dh [2, M, F],
+    (d action_net.weight, d action_net.bias, d value_net.weight,
+    d value_net.bias), stats f64 [6]: policy loss, value loss, entropy loss,
+    loss, approx kl, clip fraction).  Nothing is differentiated here: the
+    caller backpropagates dh from h and assigns the head gradients."""
+    lib = _native.load()
+    _, M, F = h.shape
+    A = action_net.out_features
+    dev = h.device
+    if h.stride(2) != 1 or h.stride(1) != F:
+        raise ValueError("ppo_loss: latents must be row-contiguous [2, M, F]")
+    for t, dt in ((actions, torch.int32), (advantages, torch.float32), (old_log_prob, torch.float32),
+                  (returns, torch.float32)):
+        if t.dtype != dt or not t.is_contiguous() or t.device != dev:
+            raise ValueError("ppo_loss: buffers must be contiguous int32 actions / f32 values on the latents' device")
+    if src is not None and (src.dtype != torch.int64 or src.numel() != M or not src.is_contiguous()):
+        raise ValueError("ppo_loss: src must be [M] contiguous int64")
+    npart, nspart = C.c_int64(), C.c_int64()
+    _native.check(lib.vn_ppo_loss_part_floats(M, F, A, C.byref(npart), C.byref(nspart)), "vn_ppo_loss_part_floats")
+    dh = torch.empty((2, M, F), dtype=torch.float32, device=dev)
+    gh = torch.empty(A * F + A + F + 1, dtype=torch.float32, device=dev)
+    dbl = torch.empty(6 + 128 + nspart.value, dtype=torch.float64, device=dev)
+    part = torch.empty(npart.value, dtype=torch.float32, device=dev)
+    stats = dbl[:6]
+    wa, ba = action_net.weight.detach(), action_net.bias.detach()
+    wv, bv = value_net.weight.detach(), value_net.bias.detach()
+    _native.check(lib.vn_ppo_loss(_p(h[0]), _p(h[1]), F, _p(wa.contiguous()), _p(ba), _p(wv.contiguous()), _p(bv),
+                                  _p(src), _p(actions), _p(advantages), _p(old_log_prob), _p(returns), M, F, A,
+                                  float(clip_range), float(ent_coef), float(vf_coef), int(bool(normalize_advantage)),
+                                  _p(dh[0]), _p(dh[1]), _p(gh), _p(stats), _p(dbl[6:134]), _p(part), _p(dbl[134:]),
+                                  _stream(dev)), "vn_ppo_loss")
+    grads = (gh[:A * F].view(A, F), gh[A * F:A * F + A], gh[A * F + A:A * F + A + F].view(1, F), gh[-1:])
+    return dh, grads, stats

@@ -25,7 +25,11 @@ matrix-core launch per step, csrc/voxnav_learn_f32.hip, forward and
 backward), which equals sb3's masked per-step loop because a sequence can only begin
 with an episode start.
 The one host round-trip per recurrent minibatch is the (n_seq, max_len)
-pair that sizes the padded tensor.
+pair that sizes the padded tensor (none in the row layout,
+``voxnav.lstm_seq.dual_lstm_rows``).  From the MLP latents on, the heads,
+the advantage normalisation, the three losses and their gradient run in the
+fused loss kernel (``learn_ops.ppo_loss``, csrc/voxnav_ppo_loss.hip); the
+latents' gradient is backpropagated through the MLP and LSTM kernels.
 
 With ``process_group`` set, gradients are averaged over the ranks (one
 flattened all-reduce per minibatch, RCCL over xGMI with the nccl backend)
@@ -76,6 +80,9 @@ class PPOLearner:
         fused = bool(self.params) and all(p.is_cuda for p in self.params)
         self.optimizer = torch.optim.Adam(self.params, lr=self.lr, eps=1e-5, fused=fused or None)
         self.n_updates = 0
+        # heads + losses + their gradient in one fused kernel family on the GPU
+        # (learn_ops.ppo_loss); VOXNAV_FUSED_LOSS=0: torch's ops and autograd (A/B knob)
+        self.fused_loss = os.environ.get("VOXNAV_FUSED_LOSS", "1") != "0"
 
     # ------------------------------------------------------------ helpers
     def _orders(self, total: int) -> List:
@@ -208,8 +215,7 @@ class PPOLearner:
                                            buf.lstm_c)                       # [2, T, rows, H]: actor, critic
         H = out.shape[-1]
         lat = out.view(2, T * rows, H)
-        acts = buf.actions.reshape(-1)[src].long()
-        return self._heads(lat[0], lat[1], acts, lat_pair=lat), src
+        return (lat[0], lat[1], lat), src
 
     def _evaluate_recurrent(self, buf, pk: dict):
         """evaluate_actions on a packed minibatch (``_pack_begin``)."""
@@ -235,27 +241,36 @@ class PPOLearner:
         out_pi, out_vf = dual_lstm(self.policy, x, h0, c0)
         lat_pi = out_pi[pos, seq_id]
         lat_vf = out_vf[pos, seq_id]
-        acts = buf.actions.reshape(-1)[src].long()
-        return self._heads(lat_pi, lat_vf, acts), src
+        return (lat_pi, lat_vf, None), src
 
     def _evaluate_ff(self, buf, idx: torch.Tensor):
         T, N = buf.actions.shape
         env = idx // T
         src = (idx - env * T) * N + env
         obs = buf.obs.reshape(T * N, -1)[src]
-        acts = buf.actions.reshape(-1)[src].long()
-        return self._heads(obs, obs, acts), src
+        return (obs, obs, None), src
 
     def update(self, buf, idx: torch.Tensor, packed: Optional[dict] = None) -> torch.Tensor:
         """One minibatch (env-major flat ids ``idx``): losses, backward,
         (all-reduce), clip, Adam.  Returns the logged values as a device
         tensor (no host sync beyond the recurrent minibatch's size)."""
         if self.recurrent:
-            (values, log_prob, entropy), src = self._evaluate_recurrent(buf, packed or self._pack_begin(buf, idx))
+            (lat_pi, lat_vf, lat_pair), src = self._evaluate_recurrent(buf, packed or self._pack_begin(buf, idx))
         else:
-            (values, log_prob, entropy), src = self._evaluate_ff(buf, idx)
+            (lat_pi, lat_vf, lat_pair), src = self._evaluate_ff(buf, idx)
+        norm = self.normalize_advantage and (self.recurrent or src.numel() > 1)
+        if lat_pi.is_cuda and self.fused_loss:
+            pol = self.policy
+            ex = pol.mlp_extractor
+            F = ex.latent_dim_pi
+            if F == ex.latent_dim_vf and learn_ops.ppo_loss_supported(pol.action_net, pol.value_net, F):
+                h = learn_ops.mlp_pair(ex.policy_net, ex.value_net, lat_pi, None if lat_vf is lat_pi else lat_vf,
+                                       x_pair=lat_pair, stacked=True)
+                if h is not None:
+                    return self._update_fused(buf, h, src, norm)
+        values, log_prob, entropy = self._heads(lat_pi, lat_vf, buf.actions.reshape(-1)[src].long(), lat_pair)
         adv = buf.advantages.reshape(-1)[src]
-        if self.normalize_advantage and (self.recurrent or adv.numel() > 1):
+        if norm:
             adv = (adv - adv.mean()) / (adv.std() + 1e-8)
         old_lp = buf.log_probs.reshape(-1)[src]
         ret = buf.returns.reshape(-1)[src]
@@ -280,6 +295,29 @@ class PPOLearner:
                                 ((torch.exp(log_ratio) - 1) - log_ratio).mean().double(),
                                 (torch.abs(ratio - 1) > self.clip_range).double().mean(),
                                 gnorm.detach().double()])
+
+    def _update_fused(self, buf, h: torch.Tensor, src: torch.Tensor, norm: bool) -> torch.Tensor:
+        """``update`` from the MLP latents h [2, M, F] on: the heads, losses and
+        their gradient in the fused loss kernel (learn_ops.ppo_loss), the
+        latents' gradient backpropagated through the MLP and LSTM kernels,
+        the head gradients assigned; then (all-reduce), clip, Adam."""
+        pol = self.policy
+        dh, grads, stats = learn_ops.ppo_loss(h, pol.action_net, pol.value_net, src, buf.actions.reshape(-1),
+                                              buf.advantages.reshape(-1), buf.log_probs.reshape(-1),
+                                              buf.returns.reshape(-1), self.clip_range, self.ent_coef, self.vf_coef,
+                                              norm)
+        self.optimizer.zero_grad(set_to_none=True)
+        h.backward(dh)
+        for prm, g in zip((pol.action_net.weight, pol.action_net.bias, pol.value_net.weight, pol.value_net.bias),
+                          grads):
+            if prm.requires_grad:
+                prm.grad = g
+        if self.group is not None:
+            self._allreduce_grads()
+        gnorm = torch.nn.utils.clip_grad_norm_(self.params, self.max_grad_norm)
+        self.optimizer.step()
+        self.n_updates += 1
+        return torch.cat([stats, gnorm.detach().double().view(1)])
 
     def update_many(self, buf, idxs: Sequence[torch.Tensor]) -> torch.Tensor:
         """``update`` over consecutive minibatches, the next minibatch's

@@ -464,6 +464,27 @@ int vn_gemm_f32_tn(const float *dy, const float *y, int64_t ldd, int64_t sd, con
                    float *c, int64_t sc, float *colsum, int32_t M, int32_t N, int32_t K, int32_t batch, int32_t splits,
                    float *workspace, float *workspace2, int32_t accumulate, void *stream);
 
+/* PPO minibatch loss + its gradient to the MLP latents (csrc/voxnav_ppo_loss.hip).
+ * Replaces, per minibatch, the heads and loss block of sb3 RecurrentPPO.train /
+ * PPO.train (sb3_contrib ppo_recurrent.py train(): evaluate_actions -> ratio ->
+ * clipped surrogate / value MSE / entropy -> loss.backward() down to the
+ * latents), reached from train/Grid_Train.py:228 (model.learn).
+ *   hp, hv [M][F] (row stride ldh): the actor / critic latents (F = 64..256, % 64)
+ *   wa [A][F], ba [A] (action_net, A <= 8); wv [F], bv [1] (value_net)
+ *   src [M] (NULL: identity): the buffer rows of the samples; actions int32,
+ *   advantages, old_log_prob, returns: the rollout buffer, indexed by src
+ *   -> dhp, dhv [M][F] contiguous: dloss/dlatent; grad_heads [A F + A + F + 1]:
+ *      d action_net.weight, d action_net.bias, d value_net.weight, d value_net.bias;
+ *      stats [6] f64: policy loss, value loss, entropy loss, loss, approx kl,
+ *      clip fraction.  adv_sums [128] f64 scratch; part / spart: workspaces of
+ *      the sizes vn_ppo_loss_part_floats returns (floats / doubles). */
+int vn_ppo_loss_part_floats(int32_t M, int32_t F, int32_t A, int64_t *n_part, int64_t *n_spart);
+int vn_ppo_loss(const float *hp, const float *hv, int64_t ldh, const float *wa, const float *ba, const float *wv,
+                const float *bv, const int64_t *src, const int32_t *actions, const float *advantages,
+                const float *old_log_prob, const float *returns, int32_t M, int32_t F, int32_t A, float clip_range,
+                float ent_coef, float vf_coef, int32_t normalize_advantage, float *dhp, float *dhv, float *grad_heads,
+                double *stats, double *adv_sums, float *part, double *spart, void *stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -31,7 +31,7 @@ def main():
     pol = (RecurrentActorCriticPolicy() if a.policy == "lstm" else ActorCriticPolicy()).to(dev)
     env = BatchedGridEnv(num_agents=a.agents, rooms=load_archive_set("P3_training"), local_map_length=10,
                          autoreset=True, device=dev)
-    col = RolloutCollector(env, pol, n_steps=a.T, policy_dtype="bf16")
+    col = RolloutCollector(env, pol, n_steps=a.T)
     buf = col.collect()
     torch.cuda.synchronize()
     from bench import lstm_flops_per_agent_step, mlp_flops_per_agent_step

@@ -317,6 +317,59 @@ def test_full_size_p3_sampled_belief(voxnav):
         np.testing.assert_array_equal(b[j, :W, :D, :H], np.minimum(orc_env.belief(0), 63), err_msg=f"agent {g}")
 
 
+@pytest.mark.parametrize("src", ["set:P3_training", "set:P2_training"])
+def test_full_batch_room_set_sampled_blocks_through_autoreset(voxnav, src):
+    """The room-set bench workload as the bench runs it: 65,536 agents, f32
+    reward into a caller-owned rollout, five 128-step launches (640 steps).
+    One agent from every 64-agent block (position within the block varied)
+    is replayed through the oracle launch by launch -- obs bytes, reward,
+    terminated / truncated -- across at least one auto-reset (an episode
+    ends on a crash, so under the random policy most sampled agents reset,
+    some several times, each reset drawing a new room of the set).  Belief
+    maps of every 8th sampled agent are compared after the first and the
+    last launch."""
+    from voxnav.env import Rollout
+    N, L, F, K_TOTAL = 65536, 10, 128, 640
+    env = make_env(voxnav, src, L, n=N, autoreset=True)
+    dev = env.device
+    blocks = np.arange(N // 64, dtype=np.int64)
+    sample = blocks * 64 + (blocks * 41 + 17) % 64
+    dump = sample[::8]
+    idx = torch.as_tensor(sample, device=dev)
+    orc_env = oracle_env(src, L, n_agents=len(sample))
+    out = Rollout(torch.empty((F, N, 80), dtype=torch.float32, device=dev),
+                  torch.empty((F, N), dtype=torch.float32, device=dev),
+                  torch.empty((F, N), dtype=torch.uint8, device=dev),
+                  torch.empty((F, N), dtype=torch.uint8, device=dev), None)
+    env.reset(seed=42)
+    rooms = env.room_set.rooms
+    resets = np.zeros(len(sample), dtype=np.int64)
+    for t in range(0, K_TOTAL, F):
+        env.step_random(F, policy_seed=42, t0=t, out=out)
+        orc = orc_env.run_random(42 + sample, policy_seed=42, K=F, t0=t, seed_stride=N, initial_reset=(t == 0),
+                                 gids=sample, threads=8)
+        obs = out.obs.index_select(1, idx).cpu().numpy()
+        if obs.tobytes() != orc["obs"].tobytes():
+            bad = np.argwhere((obs.view(np.uint32) != orc["obs"].view(np.uint32)).any(-1))
+            raise AssertionError(f"{src}: obs mismatch at (step, sampled agent) {(bad[:5] + [t, 0]).tolist()}")
+        np.testing.assert_array_equal(out.reward.index_select(1, idx).cpu().numpy(),
+                                      orc["reward"].astype(np.float32), err_msg=f"{src} reward, steps {t}..{t + F}")
+        te = out.terminated.index_select(1, idx).cpu().numpy()
+        tr = out.truncated.index_select(1, idx).cpu().numpy()
+        np.testing.assert_array_equal(te, orc["terminated"], err_msg=f"{src} terminated, steps {t}..{t + F}")
+        np.testing.assert_array_equal(tr, orc["truncated"], err_msg=f"{src} truncated, steps {t}..{t + F}")
+        resets += (te | tr).sum(0).astype(np.int64)
+        if t == 0 or t + F == K_TOTAL:
+            st = env.export_state().cpu().numpy()
+            b = env.belief().index_select(0, torch.as_tensor(dump, device=dev)).cpu().numpy().astype(np.int64)
+            for j, g in enumerate(dump):
+                W, D, H = rooms[int(st[g, 13])].shape
+                np.testing.assert_array_equal(b[j, :W, :D, :H], np.minimum(orc_env.belief(8 * j), 63),
+                                              err_msg=f"{src}: belief of agent {g} after step {t + F}")
+    assert (resets > 0).sum() >= len(sample) // 2, f"{src}: only {(resets > 0).sum()} sampled agents reset"
+    env.close()
+
+
 def test_gae_matches_oracle(voxnav):
     from oracle.oracle import gae as oracle_gae
     from voxnav.gae import compute_gae

@@ -184,3 +184,65 @@ def test_dual_lstm_rows_matches_float64(L, B, N, p_start):
     _close(oc, rc.float())
     for g, p in zip(got, params):
         _close(g, p.grad, rel=1e-4)
+
+
+def _ppo_loss_reference(h, wa, ba, wv, bv, act, adv, olp, ret, clip, ent_coef, vf_coef, norm):
+    """sb3's heads + losses in float64 with autograd (RecurrentPPO.train /
+    PPO.train, the block after evaluate_actions)."""
+    h = h.double().requires_grad_(True)
+    P = [t.double().requires_grad_(True) for t in (wa, ba, wv, bv)]
+    logits = h[0] @ P[0].T + P[1]
+    values = (h[1] @ P[2].T + P[3]).flatten()
+    lp_all = torch.log_softmax(logits, -1)
+    lp = lp_all.gather(1, act.long().view(-1, 1)).flatten()
+    ent = -(lp_all.exp() * lp_all).sum(-1)
+    adv = adv.double()
+    if norm:
+        adv = (adv - adv.mean()) / (adv.std() + 1e-8)
+    ratio = torch.exp(lp - olp.double())
+    pl = -torch.min(adv * ratio, adv * torch.clamp(ratio, 1 - clip, 1 + clip)).mean()
+    vl = torch.nn.functional.mse_loss(ret.double(), values)
+    el = -ent.mean()
+    loss = pl + ent_coef * el + vf_coef * vl
+    loss.backward()
+    lr = lp - olp.double()
+    stats = torch.stack([pl, vl, el, loss, ((torch.exp(lr) - 1) - lr).mean(),
+                         ((ratio - 1).abs() > clip).double().mean()]).detach()
+    return h.grad, [p.grad for p in P], stats
+
+
+@pytest.mark.parametrize("M,F,A,gather,norm", [(65536, 128, 6, True, True), (77, 64, 3, False, True),
+                                               (4099, 256, 8, True, False), (1, 128, 6, False, False)])
+def test_ppo_loss_matches_float64(M, F, A, gather, norm):
+    """The fused loss kernel (heads, advantage normalisation, clipped
+    surrogate, value MSE, entropy; gradient to the latents and the head
+    weights) against the same block in float64 autograd.  Old log-probs are
+    spread so the ratio falls on both sides of the clip range and inside it
+    (the min's tie, where torch splits the gradient)."""
+    from voxnav.learn_ops import ppo_loss
+    dev = "cuda:0"
+    torch.manual_seed(M + F + A)
+    an, vn = torch.nn.Linear(F, A).to(dev), torch.nn.Linear(F, 1).to(dev)
+    h = torch.tanh(torch.randn((2, M, F), device=dev))
+    R = M + 1000 if gather else M
+    src = torch.randperm(R, device=dev)[:M].contiguous() if gather else None
+    act = torch.randint(0, A, (R,), device=dev, dtype=torch.int32)
+    adv = torch.randn(R, device=dev) * 3 + 0.5
+    ret = torch.randn(R, device=dev)
+    with torch.no_grad():
+        lp_true = torch.log_softmax(h[0] @ an.weight.T + an.bias, -1)
+    sel = src if gather else torch.arange(M, device=dev)
+    olp = torch.randn(R, device=dev) - 1.5
+    olp[sel] = lp_true.gather(1, act[sel].long().view(-1, 1)).flatten() + 0.3 * torch.randn(M, device=dev)
+    clip, ent, vf = 0.2, 0.01, 0.5
+    dh, grads, stats = ppo_loss(h, an, vn, src, act, adv, olp, ret, clip, ent, vf, norm)
+    g = lambda t: t if src is None else t[src]  # noqa: E731
+    rdh, rgrads, rstats = _ppo_loss_reference(h, an.weight, an.bias, vn.weight, vn.bias, g(act), g(adv), g(olp),
+                                              g(ret), clip, ent, vf, norm)
+    if M == 1 and norm:
+        return
+    _close(dh.double(), rdh, rel=2e-5, floor=1e-9)
+    for a, b in zip(grads, rgrads):
+        assert a.shape == b.shape
+        _close(a.double(), b, rel=1e-4, floor=1e-9)
+    _close(stats, rstats, rel=1e-5, floor=1e-7)
