@@ -1334,7 +1334,9 @@ __global__ __launch_bounds__((PCM == 1 || PCM == 2) ? VN_PC_BLOCK : BLOCK,
         const uint64_t tt = tb + (uint64_t)j;
         if (active) {
             // DM: the previous step's plane marks, before this step's tile shift reads the entering column
-            if constexpr (DM) pend_apply<PH>(p, map, pc_, pend, q);
+            if constexpr (DM) {
+                if (!(VN_ABLATE & 1048576u)) pend_apply<PH>(p, map, pc_, pend, q);   // diagnostics: skipped
+            }
             const int a = EXT ? p.actions[row] : (int)((acts >> (8 * (uint32_t)(tt & 3u))) & 0xffu);
             if (!FAST && p.actions_out && q == 0) p.actions_out[row] = a;
 

@@ -365,6 +365,61 @@ __global__ __launch_bounds__(256) void ppo_loss_reduce_kernel(const float *__res
     if (w == 0 && i < PG) gout[i] = ((q[0][o] + q[1][o]) + q[2][o]) + q[3][o];
 }
 
+
+// ---- gradient clipping (torch.nn.utils.clip_grad_norm_, sb3 max_grad_norm) ----
+// The total 2-norm over every parameter gradient (f64 sums: per-block
+// partials over all tensors, then one block in a fixed order) and the
+// divisor the fused Adam step applies to the gradients (its grad_scale):
+// max(1, (norm + 1e-6) / max_norm) = 1 / clip_grad_norm_'s clamped coefficient.
+constexpr int kMaxGradTensors = 64;
+constexpr int kNormBlocks = 256;
+
+struct GradList {
+    const float *p[kMaxGradTensors];
+    int64_t n[kMaxGradTensors];
+    int count;
+};
+
+__global__ __launch_bounds__(256) void grad_sq_kernel(GradList gl, double *__restrict__ part) {
+    __shared__ double sr[256];
+    const int t = threadIdx.x;
+    double acc = 0.0;
+    for (int k = 0; k < gl.count; ++k) {
+        const float *g = gl.p[k];
+        const int64_t n = gl.n[k];
+        const int64_t n4 = ((((uintptr_t)g) & 15) == 0) ? n / 4 : 0;
+        for (int64_t i = (int64_t)blockIdx.x * 256 + t; i < n4; i += (int64_t)gridDim.x * 256) {
+            const float4 v = reinterpret_cast<const float4 *>(g)[i];
+            acc += (double)v.x * v.x + (double)v.y * v.y + (double)v.z * v.z + (double)v.w * v.w;
+        }
+        for (int64_t i = 4 * n4 + (int64_t)blockIdx.x * 256 + t; i < n; i += (int64_t)gridDim.x * 256)
+            acc += (double)g[i] * g[i];
+    }
+    sr[t] = acc;
+    __syncthreads();
+    for (int h = 128; h >= 1; h >>= 1) {
+        if (t < h) sr[t] += sr[t + h];
+        __syncthreads();
+    }
+    if (t == 0) part[blockIdx.x] = sr[0];
+}
+
+__global__ __launch_bounds__(256) void grad_norm_kernel(const double *__restrict__ part, float max_norm,
+                                                        float *__restrict__ norm, float *__restrict__ scale) {
+    __shared__ double sr[256];
+    const int t = threadIdx.x;
+    sr[t] = part[t];
+    __syncthreads();
+    for (int h = 128; h >= 1; h >>= 1) {
+        if (t < h) sr[t] += sr[t + h];
+        __syncthreads();
+    }
+    if (t == 0) {
+        const float nv = (float)sqrt(sr[0]);
+        norm[0] = nv;
+        scale[0] = fmaxf(1.0f, (nv + 1e-6f) / max_norm);
+    }
+}
 }  // namespace
 
 extern "C" {
@@ -416,6 +471,26 @@ int vn_ppo_loss(const float *hp, const float *hv, int64_t ldh, const float *wa, 
 #undef VN_LOSS_Q
     hipLaunchKernelGGL(ppo_loss_reduce_kernel, dim3((unsigned)((PG + 63) / 64 + 1)), dim3(256), 0, s, part, spart, nb,
                        PG, M, ent_coef, vf_coef, grad_heads, stats);
+    VN_HIP(hipGetLastError());
+    return VN_OK;
+}
+
+int vn_grad_norm(const float *const *grads, const int64_t *sizes, int32_t count, float max_norm, float *norm,
+                 float *scale, double *work, void *stream) {
+    if (!grads || !sizes || !norm || !scale || !work) return fail(VN_ERR_INVALID, "NULL argument");
+    if (count < 1 || count > kMaxGradTensors)
+        return fail(VN_ERR_INVALID, "gradient count %d outside 1..%d", count, kMaxGradTensors);
+    if (!(max_norm > 0.0f)) return fail(VN_ERR_INVALID, "max_norm must be > 0");
+    GradList gl{};
+    gl.count = count;
+    for (int k = 0; k < count; ++k) {
+        if (!grads[k] || sizes[k] < 0) return fail(VN_ERR_INVALID, "gradient %d: NULL or negative size", k);
+        gl.p[k] = grads[k];
+        gl.n[k] = sizes[k];
+    }
+    const hipStream_t s = (hipStream_t)stream;
+    hipLaunchKernelGGL(grad_sq_kernel, dim3(kNormBlocks), dim3(256), 0, s, gl, work);
+    hipLaunchKernelGGL(grad_norm_kernel, dim3(1), dim3(256), 0, s, work, max_norm, norm, scale);
     VN_HIP(hipGetLastError());
     return VN_OK;
 }

@@ -249,3 +249,27 @@ def ppo_loss(h: torch.Tensor, action_net: torch.nn.Linear, value_net: torch.nn.L
                                   _stream(dev)), "vn_ppo_loss")
     grads = (gh[:A * F].view(A, F), gh[A * F:A * F + A], gh[A * F + A:A * F + A + F].view(1, F), gh[-1:])
     return dh, grads, stats
+
+
+def grad_norm_scale(params, max_norm: float, work: Optional[torch.Tensor] = None):
+    """The total 2-norm of the parameters' gradients and the divisor that
+    clips them to ``max_norm`` (csrc/voxnav_ppo_loss.hip vn_grad_norm): two
+    launches, device scalars (norm, scale) -- handed to the fused Adam step as
+    its grad_scale instead of rescaling every gradient in place
+    (torch.nn.utils.clip_grad_norm_'s update, folded into the step)."""
+    lib = _native.load()
+    grads = [p.grad for p in params if p.grad is not None]
+    if not grads:
+        raise ValueError("grad_norm_scale: no gradients")
+    dev = grads[0].device
+    for g in grads:
+        if g.dtype != torch.float32 or not g.is_contiguous() or g.device != dev:
+            raise ValueError("grad_norm_scale: gradients must be contiguous f32 on one device")
+    n = len(grads)
+    ptrs = (C.c_void_p * n)(*[g.data_ptr() for g in grads])
+    sizes = (C.c_int64 * n)(*[g.numel() for g in grads])
+    out = torch.empty(2, dtype=torch.float32, device=dev)
+    work = torch.empty(256, dtype=torch.float64, device=dev) if work is None else work
+    _native.check(lib.vn_grad_norm(ptrs, sizes, n, float(max_norm), _p(out[0:1]), _p(out[1:2]), _p(work),
+                                   _stream(dev)), "vn_grad_norm")
+    return out[0], out[1]

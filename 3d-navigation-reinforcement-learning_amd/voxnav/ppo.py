@@ -285,9 +285,7 @@ class PPOLearner:
         loss.backward()
         if self.group is not None:
             self._allreduce_grads()
-        gnorm = torch.nn.utils.clip_grad_norm_(self.params, self.max_grad_norm)
-        self.optimizer.step()
-        self.n_updates += 1
+        gnorm = self._clip_step()
         with torch.no_grad():
             log_ratio = log_prob - old_lp
             return torch.stack([policy_loss.detach().double(), value_loss.detach().double(),
@@ -314,10 +312,26 @@ class PPOLearner:
                 prm.grad = g
         if self.group is not None:
             self._allreduce_grads()
-        gnorm = torch.nn.utils.clip_grad_norm_(self.params, self.max_grad_norm)
-        self.optimizer.step()
-        self.n_updates += 1
+        gnorm = self._clip_step()
         return torch.cat([stats, gnorm.detach().double().view(1)])
+
+    def _clip_step(self) -> torch.Tensor:
+        """clip_grad_norm_ + Adam step.  On the GPU with the fused Adam: the
+        norm in two launches (learn_ops.grad_norm_scale) and the clip applied
+        by the step itself as its grad_scale divisor; else torch's clip."""
+        fused = self.optimizer.param_groups[0].get("fused")
+        if fused and self.params[0].is_cuda:
+            gnorm, scale = learn_ops.grad_norm_scale(self.params, self.max_grad_norm)
+            self.optimizer.grad_scale = scale
+            try:
+                self.optimizer.step()
+            finally:
+                self.optimizer.grad_scale = None
+        else:
+            gnorm = torch.nn.utils.clip_grad_norm_(self.params, self.max_grad_norm)
+            self.optimizer.step()
+        self.n_updates += 1
+        return gnorm
 
     def update_many(self, buf, idxs: Sequence[torch.Tensor]) -> torch.Tensor:
         """``update`` over consecutive minibatches, the next minibatch's

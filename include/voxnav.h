@@ -485,6 +485,14 @@ int vn_ppo_loss(const float *hp, const float *hv, int64_t ldh, const float *wa, 
                 float ent_coef, float vf_coef, int32_t normalize_advantage, float *dhp, float *dhv, float *grad_heads,
                 double *stats, double *adv_sums, float *part, double *spart, void *stream);
 
+/* The total 2-norm of the parameter gradients (count <= 64 f32 tensors; device
+ * pointers and element counts passed by host arrays) and the divisor the
+ * fused Adam step applies to them: max(1, (norm + 1e-6) / max_norm), i.e.
+ * 1 / torch.nn.utils.clip_grad_norm_'s clamped coefficient (sb3
+ * max_grad_norm, sb3_contrib ppo_recurrent.py train()).  work: 256 doubles. */
+int vn_grad_norm(const float *const *grads, const int64_t *sizes, int32_t count, float max_norm, float *norm,
+                 float *scale, double *work, void *stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -246,3 +246,33 @@ def test_ppo_loss_matches_float64(M, F, A, gather, norm):
         assert a.shape == b.shape
         _close(a.double(), b, rel=1e-4, floor=1e-9)
     _close(stats, rstats, rel=1e-5, floor=1e-7)
+
+
+def test_grad_norm_scale_matches_clip_grad_norm():
+    """The two-launch gradient norm (and the Adam grad_scale divisor) against
+    torch.nn.utils.clip_grad_norm_ over tensors of ragged sizes and offsets;
+    and the fused Adam step with that divisor against clip + step."""
+    from voxnav.learn_ops import grad_norm_scale
+    dev = "cuda:0"
+    torch.manual_seed(3)
+    shapes = [(1024, 256), (1024, 80), (1024,), (6, 128), (6,), (1, 128), (1,), (333, 7)]
+    ps = [torch.nn.Parameter(torch.randn(s, device=dev)) for s in shapes]
+    for p in ps:
+        p.grad = torch.randn_like(p) * 0.05
+    ref_ps = [torch.nn.Parameter(p.detach().clone()) for p in ps]
+    for r, p in zip(ref_ps, ps):
+        r.grad = p.grad.clone()
+    for max_norm in (0.5, 1e3):
+        norm, scale = grad_norm_scale(ps, max_norm)
+        ref = torch.linalg.vector_norm(torch.stack([torch.linalg.vector_norm(p.grad.double()) for p in ps])).float()
+        _close(norm, ref, rel=1e-6)
+        assert abs(scale.item() - max(1.0, (ref.item() + 1e-6) / max_norm)) <= 1e-6 * scale.item()
+    opt = torch.optim.Adam(ps, lr=3e-4, eps=1e-5, fused=True)
+    ref_opt = torch.optim.Adam(ref_ps, lr=3e-4, eps=1e-5, fused=True)
+    norm, scale = grad_norm_scale(ps, 0.5)
+    opt.grad_scale = scale
+    opt.step()
+    torch.nn.utils.clip_grad_norm_(ref_ps, 0.5)
+    ref_opt.step()
+    for p, r in zip(ps, ref_ps):
+        _close(p.detach(), r.detach(), rel=1e-6, floor=1e-7)
