@@ -617,12 +617,12 @@ __device__ __forceinline__ void pend_apply(const Params &p, int8_t *map, PlaneCa
             const uint64_t nv = pn0 | pend.pm0;
             if (pofs == 0) pc_.w[0] = nv;
             else pc_.w[1] = nv;
-            if (!(VN_ABLATE & 32u)) prow[pend.pw0] = nv;
+            if (!(VN_ABLATE & 2097184u)) prow[pend.pw0] = nv;   // 32 | 2097152: diagnostics
         }
         if (nwd1) {
             const uint64_t nv = pn1 | pend.pm1;
             if (pofs == 0) pc_.w[1] = nv;
-            if (!(VN_ABLATE & 32u)) prow[pend.pw0 + 1] = nv;
+            if (!(VN_ABLATE & 2097184u)) prow[pend.pw0 + 1] = nv;
         }
         const int sh = pend.pa - pend.pw0 * 64;   // 0..63
         rel = sh == 0 ? nwd0 : (nwd0 >> sh) | (nwd1 << (64 - sh));

@@ -323,9 +323,8 @@ def test_full_batch_room_set_sampled_blocks_through_autoreset(voxnav, src):
     reward into a caller-owned rollout, five 128-step launches (640 steps).
     One agent from every 64-agent block (position within the block varied)
     is replayed through the oracle launch by launch -- obs bytes, reward,
-    terminated / truncated -- across at least one auto-reset (an episode
-    ends on a crash, so under the random policy most sampled agents reset,
-    some several times, each reset drawing a new room of the set).  Belief
+    terminated / truncated -- across auto-resets (the sampled agents whose
+    episode ends in the window restart in a newly drawn room of the set).  Belief
     maps of every 8th sampled agent are compared after the first and the
     last launch."""
     from voxnav.env import Rollout
@@ -366,7 +365,8 @@ def test_full_batch_room_set_sampled_blocks_through_autoreset(voxnav, src):
                 W, D, H = rooms[int(st[g, 13])].shape
                 np.testing.assert_array_equal(b[j, :W, :D, :H], np.minimum(orc_env.belief(8 * j), 63),
                                               err_msg=f"{src}: belief of agent {g} after step {t + F}")
-    assert (resets > 0).sum() >= len(sample) // 2, f"{src}: only {(resets > 0).sum()} sampled agents reset"
+    # (P3 in the first 640 steps: ~6 % of the sampled agents end an episode, 57 of 1,024 measured)
+    assert (resets > 0).sum() >= 8, f"{src}: only {(resets > 0).sum()} sampled agents reset"
     env.close()
 
 

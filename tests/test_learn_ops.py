@@ -189,8 +189,8 @@ def test_dual_lstm_rows_matches_float64(L, B, N, p_start):
 def _ppo_loss_reference(h, wa, ba, wv, bv, act, adv, olp, ret, clip, ent_coef, vf_coef, norm):
     """sb3's heads + losses in float64 with autograd (RecurrentPPO.train /
     PPO.train, the block after evaluate_actions)."""
-    h = h.double().requires_grad_(True)
-    P = [t.double().requires_grad_(True) for t in (wa, ba, wv, bv)]
+    h = h.detach().double().requires_grad_(True)
+    P = [t.detach().double().requires_grad_(True) for t in (wa, ba, wv, bv)]
     logits = h[0] @ P[0].T + P[1]
     values = (h[1] @ P[2].T + P[3]).flatten()
     lp_all = torch.log_softmax(logits, -1)
