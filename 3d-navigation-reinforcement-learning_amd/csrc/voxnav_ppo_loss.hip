@@ -420,6 +420,59 @@ __global__ __launch_bounds__(256) void grad_norm_kernel(const double *__restrict
         scale[0] = fmaxf(1.0f, (nv + 1e-6f) / max_norm);
     }
 }
+
+// ---- Adam step (torch.optim.Adam, the update sb3's policy optimizer runs) ----
+// One launch over every parameter (pointers by value): with the clip divisor
+// s (vn_grad_norm; 1 when NULL) and the step's bias corrections from the host,
+// per element, in torch's fused-Adam order:
+//   g = grad / s;  m = b1 m + (1 - b1) g;  v = b2 v + (1 - b2) g g
+//   p -= (lr / bc1) m / (sqrt(v) / sqrt(bc2) + eps)
+// The gradients are read, not rewritten (the learner drops them after the step).
+struct AdamList {
+    float *p[kMaxGradTensors];
+    const float *g[kMaxGradTensors];
+    float *m[kMaxGradTensors];
+    float *v[kMaxGradTensors];
+    float *step[kMaxGradTensors];   // torch's per-parameter step counters (device f32 scalars)
+    int64_t n[kMaxGradTensors];
+    int count;
+};
+
+__global__ __launch_bounds__(256) void adam_kernel(AdamList al, const float *__restrict__ scale, float lr, float b1,
+                                                   float b2, float eps, float bc1, float bc2_sqrt, float step_value) {
+    const bool div = scale != nullptr;
+    const float s = scale ? scale[0] : 1.0f;
+    const float step_size = lr / bc1;
+    const int64_t gid = (int64_t)blockIdx.x * 256 + threadIdx.x, stride = (int64_t)gridDim.x * 256;
+    if (gid < al.count && al.step[gid]) al.step[gid][0] = step_value;
+    auto upd = [&](float &pp, float g, float &mm, float &vv) {
+        if (div) g = g / s;
+        mm = b1 * mm + (1.0f - b1) * g;
+        vv = b2 * vv + (1.0f - b2) * g * g;
+        const float denom = sqrtf(vv) / bc2_sqrt + eps;
+        pp = pp - step_size * (mm / denom);
+    };
+    for (int k = 0; k < al.count; ++k) {
+        const int64_t n = al.n[k];
+        float *P = al.p[k], *M = al.m[k], *V = al.v[k];
+        const float *G = al.g[k];
+        const bool vec = ((((uintptr_t)P) | ((uintptr_t)G) | ((uintptr_t)M) | ((uintptr_t)V)) & 15) == 0;
+        const int64_t n4 = vec ? n / 4 : 0;
+        for (int64_t i = gid; i < n4; i += stride) {
+            float4 pp = reinterpret_cast<float4 *>(P)[i], mm = reinterpret_cast<float4 *>(M)[i],
+                   vv = reinterpret_cast<float4 *>(V)[i];
+            const float4 gg = reinterpret_cast<const float4 *>(G)[i];
+            upd(pp.x, gg.x, mm.x, vv.x);
+            upd(pp.y, gg.y, mm.y, vv.y);
+            upd(pp.z, gg.z, mm.z, vv.z);
+            upd(pp.w, gg.w, mm.w, vv.w);
+            reinterpret_cast<float4 *>(P)[i] = pp;
+            reinterpret_cast<float4 *>(M)[i] = mm;
+            reinterpret_cast<float4 *>(V)[i] = vv;
+        }
+        for (int64_t i = 4 * n4 + gid; i < n; i += stride) upd(P[i], G[i], M[i], V[i]);
+    }
+}
 }  // namespace
 
 extern "C" {
@@ -491,6 +544,36 @@ int vn_grad_norm(const float *const *grads, const int64_t *sizes, int32_t count,
     const hipStream_t s = (hipStream_t)stream;
     hipLaunchKernelGGL(grad_sq_kernel, dim3(kNormBlocks), dim3(256), 0, s, gl, work);
     hipLaunchKernelGGL(grad_norm_kernel, dim3(1), dim3(256), 0, s, work, max_norm, norm, scale);
+    VN_HIP(hipGetLastError());
+    return VN_OK;
+}
+
+int vn_adam_step(float *const *params, const float *const *grads, float *const *exp_avg, float *const *exp_avg_sq,
+                 float *const *steps, const int64_t *sizes, int32_t count, const float *clip_scale, float lr,
+                 float beta1, float beta2, float eps, int64_t step, void *stream) {
+    if (!params || !grads || !exp_avg || !exp_avg_sq || !sizes) return fail(VN_ERR_INVALID, "NULL argument");
+    if (count < 1 || count > kMaxGradTensors)
+        return fail(VN_ERR_INVALID, "parameter count %d outside 1..%d", count, kMaxGradTensors);
+    if (step < 1) return fail(VN_ERR_INVALID, "step must be >= 1");
+    AdamList al{};
+    al.count = count;
+    int64_t total = 0;
+    for (int k = 0; k < count; ++k) {
+        if (!params[k] || !grads[k] || !exp_avg[k] || !exp_avg_sq[k] || sizes[k] < 0)
+            return fail(VN_ERR_INVALID, "parameter %d: NULL or negative size", k);
+        al.p[k] = params[k];
+        al.g[k] = grads[k];
+        al.m[k] = exp_avg[k];
+        al.v[k] = exp_avg_sq[k];
+        al.step[k] = steps ? steps[k] : nullptr;
+        al.n[k] = sizes[k];
+        total += sizes[k];
+    }
+    const double bc1 = 1.0 - pow((double)beta1, (double)step), bc2 = 1.0 - pow((double)beta2, (double)step);
+    int blocks = (int)((total / 4 + 255) / 256);
+    blocks = blocks < 1 ? 1 : (blocks > 2048 ? 2048 : blocks);
+    hipLaunchKernelGGL(adam_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, al, clip_scale, lr, beta1, beta2,
+                       eps, (float)bc1, (float)sqrt(bc2), (float)step);
     VN_HIP(hipGetLastError());
     return VN_OK;
 }

@@ -273,3 +273,56 @@ def grad_norm_scale(params, max_norm: float, work: Optional[torch.Tensor] = None
     _native.check(lib.vn_grad_norm(ptrs, sizes, n, float(max_norm), _p(out[0:1]), _p(out[1:2]), _p(work),
                                    _stream(dev)), "vn_grad_norm")
     return out[0], out[1]
+
+
+def adam_step(optimizer: torch.optim.Adam, clip_scale: Optional[torch.Tensor] = None) -> None:
+    """``optimizer.step()`` for a single-group ``torch.optim.Adam`` (no
+    amsgrad / weight decay / maximize) on the library's kernel
+    (csrc/voxnav_ppo_loss.hip vn_adam_step): one launch over every parameter,
+    the gradients divided by ``clip_scale`` (``grad_norm_scale``'s divisor) on
+    the way.  The optimizer's own state tensors are updated in place
+    (``exp_avg``, ``exp_avg_sq``, ``step``), so ``state_dict()`` / checkpoints
+    are torch's."""
+    lib = _native.load()
+    if len(optimizer.param_groups) != 1:
+        raise ValueError("adam_step: one parameter group")
+    grp = optimizer.param_groups[0]
+    if grp.get("amsgrad") or grp.get("weight_decay") or grp.get("maximize"):
+        raise ValueError("adam_step: plain Adam only (no amsgrad, weight decay or maximize)")
+    params = [p for p in grp["params"] if p.grad is not None]
+    if not params:
+        return
+    dev = params[0].device
+    steps = []
+    for p in params:
+        st = optimizer.state[p]
+        if not st:
+            st["step"] = torch.zeros((), dtype=torch.float32, device=dev)
+            st["exp_avg"] = torch.zeros_like(p, memory_format=torch.preserve_format)
+            st["exp_avg_sq"] = torch.zeros_like(p, memory_format=torch.preserve_format)
+        steps.append(st["step"])
+        for t in (p, p.grad, st["exp_avg"], st["exp_avg_sq"]):
+            if t.dtype != torch.float32 or not t.is_contiguous() or t.device != dev:
+                raise ValueError("adam_step: contiguous f32 parameters, gradients and moments on one device")
+    # the step count, kept on the host (read back once after a fresh state or a load_state_dict)
+    cache = getattr(optimizer, "_vn_adam_t", None)
+    if cache is None or cache[0] is not steps[0]:
+        t = int(round(float(steps[0].item())))
+    else:
+        t = cache[1]
+    t += 1
+    optimizer._vn_adam_t = (steps[0], t)
+    n = len(params)
+    arr = lambda ts: (C.c_void_p * n)(*[x.data_ptr() for x in ts])  # noqa: E731
+    st_ptrs = [s if (s.device == dev and s.dtype == torch.float32) else None for s in steps]
+    steps_arr = (C.c_void_p * n)(*[(x.data_ptr() if x is not None else None) for x in st_ptrs])
+    sizes = (C.c_int64 * n)(*[p.numel() for p in params])
+    b1, b2 = grp["betas"]
+    _native.check(lib.vn_adam_step(arr(params), arr([p.grad for p in params]),
+                                   arr([optimizer.state[p]["exp_avg"] for p in params]),
+                                   arr([optimizer.state[p]["exp_avg_sq"] for p in params]), steps_arr, sizes, n,
+                                   _p(clip_scale), float(grp["lr"]), float(b1), float(b2), float(grp["eps"]), t,
+                                   _stream(dev)), "vn_adam_step")
+    for s, x in zip(steps, st_ptrs):
+        if x is None:                       # a CPU / other-dtype step counter (a loaded state): set on the host
+            s.fill_(float(t))

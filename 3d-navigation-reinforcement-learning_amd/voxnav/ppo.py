@@ -83,6 +83,9 @@ class PPOLearner:
         # heads + losses + their gradient in one fused kernel family on the GPU
         # (learn_ops.ppo_loss); VOXNAV_FUSED_LOSS=0: torch's ops and autograd (A/B knob)
         self.fused_loss = os.environ.get("VOXNAV_FUSED_LOSS", "1") != "0"
+        # the Adam step on the library's kernel (learn_ops.adam_step, the optimizer's
+        # own state tensors); VOXNAV_NATIVE_ADAM=0: torch's fused Adam
+        self.native_adam = os.environ.get("VOXNAV_NATIVE_ADAM", "1") != "0"
 
     # ------------------------------------------------------------ helpers
     def _orders(self, total: int) -> List:
@@ -316,17 +319,21 @@ class PPOLearner:
         return torch.cat([stats, gnorm.detach().double().view(1)])
 
     def _clip_step(self) -> torch.Tensor:
-        """clip_grad_norm_ + Adam step.  On the GPU with the fused Adam: the
-        norm in two launches (learn_ops.grad_norm_scale) and the clip applied
-        by the step itself as its grad_scale divisor; else torch's clip."""
+        """clip_grad_norm_ + Adam step.  On the GPU: the norm in two launches
+        (learn_ops.grad_norm_scale) and the step in one (learn_ops.adam_step),
+        the clip applied by the step as its divisor of the gradients; else
+        torch's clip and step."""
         fused = self.optimizer.param_groups[0].get("fused")
         if fused and self.params[0].is_cuda:
             gnorm, scale = learn_ops.grad_norm_scale(self.params, self.max_grad_norm)
-            self.optimizer.grad_scale = scale
-            try:
-                self.optimizer.step()
-            finally:
-                self.optimizer.grad_scale = None
+            if self.native_adam:
+                learn_ops.adam_step(self.optimizer, scale)
+            else:
+                self.optimizer.grad_scale = scale
+                try:
+                    self.optimizer.step()
+                finally:
+                    self.optimizer.grad_scale = None
         else:
             gnorm = torch.nn.utils.clip_grad_norm_(self.params, self.max_grad_norm)
             self.optimizer.step()

@@ -493,6 +493,16 @@ int vn_ppo_loss(const float *hp, const float *hv, int64_t ldh, const float *wa, 
 int vn_grad_norm(const float *const *grads, const int64_t *sizes, int32_t count, float max_norm, float *norm,
                  float *scale, double *work, void *stream);
 
+/* One Adam step over up to 64 f32 parameter tensors (torch.optim.Adam(eps,
+ * betas), the optimizer sb3 builds for the policy; train/Grid_Train.py:84-86
+ * lr 3e-4): the gradients divided by *clip_scale (vn_grad_norm's divisor; NULL:
+ * 1), then torch's fused-Adam update with the bias corrections of `step`
+ * (1-based); `steps` (nullable) receive the step count (torch's per-parameter
+ * state["step"] scalars).  The gradients are not rewritten. */
+int vn_adam_step(float *const *params, const float *const *grads, float *const *exp_avg, float *const *exp_avg_sq,
+                 float *const *steps, const int64_t *sizes, int32_t count, const float *clip_scale, float lr,
+                 float beta1, float beta2, float eps, int64_t step, void *stream);
+
 #ifdef __cplusplus
 }
 #endif

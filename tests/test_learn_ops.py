@@ -276,3 +276,33 @@ def test_grad_norm_scale_matches_clip_grad_norm():
     ref_opt.step()
     for p, r in zip(ps, ref_ps):
         _close(p.detach(), r.detach(), rel=1e-6, floor=1e-7)
+
+
+
+def test_adam_step_matches_torch_fused_adam():
+    """The library's Adam step (clip divisor applied on the way) against
+    torch's fused Adam with the same grad_scale, over three steps from a
+    fresh state, including a tensor whose size is not a multiple of 4; the
+    optimizer state (step, moments) is torch's own."""
+    from voxnav.learn_ops import adam_step, grad_norm_scale
+    dev = "cuda:0"
+    torch.manual_seed(5)
+    shapes = [(1024, 336), (6, 128), (6,), (333, 7), (1,)]
+    ps = [torch.nn.Parameter(torch.randn(s, device=dev)) for s in shapes]
+    rs = [torch.nn.Parameter(p.detach().clone()) for p in ps]
+    opt = torch.optim.Adam(ps, lr=3e-4, eps=1e-5, fused=True)
+    ref = torch.optim.Adam(rs, lr=3e-4, eps=1e-5, fused=True)
+    for it in range(3):
+        for p, r in zip(ps, rs):
+            g = torch.randn_like(p) * 0.3
+            p.grad, r.grad = g.clone(), g.clone()
+        _, scale = grad_norm_scale(ps, 0.5)
+        adam_step(opt, scale)
+        ref.grad_scale = scale.clone()
+        ref.step()
+        ref.grad_scale = None
+        for p, r in zip(ps, rs):
+            _close(p.detach(), r.detach(), rel=1e-6, floor=1e-7)
+            for k in ("exp_avg", "exp_avg_sq"):
+                _close(opt.state[p][k], ref.state[r][k], rel=1e-5, floor=1e-12)
+            assert float(opt.state[p]["step"]) == float(ref.state[r]["step"]) == it + 1
