@@ -498,10 +498,17 @@ void launch(const GemmArgs &g, int batch, int splits, hipStream_t s) {
         const char *e = getenv("VN_GEMM_DL");
         return !(e && e[0] == '0');
     }();
+    // VN_GEMM_GKD=32: 32-deep chunks where K allows (A/B knob; half the barriers, twice the LDS)
+    static const bool gk32 = [] {
+        const char *e = getenv("VN_GEMM_GKD");
+        return e && e[0] == '3';
+    }();
     const bool dl = dl_on && g.K % GKD == 0 && g.kper % GKD == 0 && g.lda % 4 == 0 && g.ldb % 4 == 0 &&
                     g.sa % 4 == 0 && g.sb % 4 == 0 && al(g.a) && al(g.b) && (!AGRAD || al(g.a2)) &&
                     (!A_KM || g.M % 4 == 0) && (!B_KM || g.N % 4 == 0);
-    if (dl)
+    if (dl && gk32 && g.K % 32 == 0 && g.kper % 32 == 0)
+        hipLaunchKernelGGL((gemm_dl_kernel<32, A_KM, B_KM, AGRAD, EPI>), grid, dim3(256), 0, s, g);
+    else if (dl)
         hipLaunchKernelGGL((gemm_dl_kernel<GKD, A_KM, B_KM, AGRAD, EPI>), grid, dim3(256), 0, s, g);
     else
         hipLaunchKernelGGL((gemm_f32_kernel<EPI == 3 ? GK_TN : GK_LIN, A_KM, B_KM, AGRAD, EPI>), grid, dim3(256), 0,

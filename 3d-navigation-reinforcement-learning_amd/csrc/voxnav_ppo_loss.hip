@@ -473,6 +473,25 @@ __global__ __launch_bounds__(256) void adam_kernel(AdamList al, const float *__r
         for (int64_t i = 4 * n4 + gid; i < n; i += stride) upd(P[i], G[i], M[i], V[i]);
     }
 }
+
+// ---- minibatch gather (PPO.train: rollout_buffer.get(batch_size) on the
+// swap_and_flatten'ed, env-major buffer) ----
+// sample i of the minibatch is env-major flat id idx[i] = env * T + t; its row
+// in the collector's [T, N]-major buffers is t * N + env.  One block per 16
+// samples: the rows (src) and the observation rows copied, 16 B per lane.
+__global__ __launch_bounds__(256) void minibatch_rows_kernel(const int64_t *__restrict__ idx, int M, int T, int N,
+                                                             const float *__restrict__ obs, int D,
+                                                             float *__restrict__ out, int64_t *__restrict__ src) {
+    const int lane = threadIdx.x & 15, s = blockIdx.x * 16 + (threadIdx.x >> 4);
+    if (s >= M) return;
+    const int64_t id = idx[s];
+    const int64_t env = id / T, t = id - env * T;
+    const int64_t r = t * N + env;
+    if (lane == 0) src[s] = r;
+    const float4 *in = reinterpret_cast<const float4 *>(obs + r * D);
+    float4 *o = reinterpret_cast<float4 *>(out + (int64_t)s * D);
+    for (int c = lane; c < D / 4; c += 16) o[c] = in[c];
+}
 }  // namespace
 
 extern "C" {
@@ -574,6 +593,17 @@ int vn_adam_step(float *const *params, const float *const *grads, float *const *
     blocks = blocks < 1 ? 1 : (blocks > 2048 ? 2048 : blocks);
     hipLaunchKernelGGL(adam_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, al, clip_scale, lr, beta1, beta2,
                        eps, (float)bc1, (float)sqrt(bc2), (float)step);
+    VN_HIP(hipGetLastError());
+    return VN_OK;
+}
+
+int vn_minibatch_rows(const int64_t *idx, int32_t M, int32_t T, int32_t N, const float *obs, int32_t D, float *out,
+                      int64_t *src, void *stream) {
+    if (!idx || !obs || !out || !src) return fail(VN_ERR_INVALID, "NULL argument");
+    if (M < 1 || T < 1 || N < 1 || D < 4 || D % 4) return fail(VN_ERR_INVALID, "bad sizes M=%d T=%d N=%d D=%d", M, T, N, D);
+    if ((((uintptr_t)obs) | ((uintptr_t)out)) & 15) return fail(VN_ERR_INVALID, "obs / out must be 16-B aligned");
+    hipLaunchKernelGGL(minibatch_rows_kernel, dim3((unsigned)((M + 15) / 16)), dim3(256), 0, (hipStream_t)stream, idx,
+                       M, T, N, obs, D, out, src);
     VN_HIP(hipGetLastError());
     return VN_OK;
 }

@@ -326,3 +326,20 @@ def adam_step(optimizer: torch.optim.Adam, clip_scale: Optional[torch.Tensor] = 
     for s, x in zip(steps, st_ptrs):
         if x is None:                       # a CPU / other-dtype step counter (a loaded state): set on the host
             s.fill_(float(t))
+
+
+def minibatch_rows(idx: torch.Tensor, T: int, N: int, obs: torch.Tensor):
+    """(src, obs rows) of a feed-forward PPO minibatch in one launch
+    (vn_minibatch_rows): idx [M] env-major flat ids (int64), obs [T, N, D]
+    -> src [M] int64 rows of the [T, N]-major buffers, [M, D] observations."""
+    lib = _native.load()
+    M = idx.numel()
+    D = obs.shape[-1]
+    dev = idx.device
+    if idx.dtype != torch.int64 or not idx.is_contiguous() or not obs.is_contiguous() or obs.dtype != torch.float32:
+        raise ValueError("minibatch_rows: contiguous int64 ids and f32 observations")
+    out = torch.empty((M, D), dtype=torch.float32, device=dev)
+    src = torch.empty(M, dtype=torch.int64, device=dev)
+    _native.check(lib.vn_minibatch_rows(_p(idx), M, T, N, _p(obs), D, _p(out), _p(src), _stream(dev)),
+                  "vn_minibatch_rows")
+    return src, out

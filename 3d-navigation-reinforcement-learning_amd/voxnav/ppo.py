@@ -248,6 +248,9 @@ class PPOLearner:
 
     def _evaluate_ff(self, buf, idx: torch.Tensor):
         T, N = buf.actions.shape
+        if idx.is_cuda and buf.obs.shape[-1] % 4 == 0 and buf.obs.is_contiguous():
+            src, obs = learn_ops.minibatch_rows(idx.contiguous(), T, N, buf.obs)   # one launch
+            return (obs, obs, None), src
         env = idx // T
         src = (idx - env * T) * N + env
         obs = buf.obs.reshape(T * N, -1)[src]

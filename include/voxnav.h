@@ -503,6 +503,13 @@ int vn_adam_step(float *const *params, const float *const *grads, float *const *
                  float *const *steps, const int64_t *sizes, int32_t count, const float *clip_scale, float lr,
                  float beta1, float beta2, float eps, int64_t step, void *stream);
 
+/* A PPO minibatch's rows (sb3 PPO.train over the env-major flattened rollout
+ * buffer): sample i has env-major id idx[i] = env * T + t; src[i] receives its
+ * row t * N + env of the [T, N]-major buffers and out[i] its observation
+ * row (D floats, D % 4 == 0). */
+int vn_minibatch_rows(const int64_t *idx, int32_t M, int32_t T, int32_t N, const float *obs, int32_t D, float *out,
+                      int64_t *src, void *stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -40,6 +40,9 @@ run sq_p3 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_VMEM
 run learn_lstm_gk16 300 env VOXNAV_LIB=3d-navigation-reinforcement-learning_amd/voxnav/_lib/variants/libvoxnav_gk16.so python3 scripts/ppo_bench.py --agents 65536 --batch 65536 --minibatches 8 --policy lstm
 run learn_mlp_gk16 300 env VOXNAV_LIB=3d-navigation-reinforcement-learning_amd/voxnav/_lib/variants/libvoxnav_gk16.so python3 scripts/ppo_bench.py --agents 65536 --batch 65536 --minibatches 8 --policy mlp
 run gemm 200 python3 scripts/gemm_bench.py 20
+run gemm_k32 200 env VN_GEMM_GKD=32 python3 scripts/gemm_bench.py 20
+run learn_mlp_k32 300 env VN_GEMM_GKD=32 python3 scripts/ppo_bench.py --agents 65536 --batch 65536 --minibatches 8 --policy mlp
+run learn_mlp_plain 300 python3 scripts/ppo_bench.py --agents 65536 --batch 65536 --minibatches 8 --policy mlp
 run gemm_gk16 200 env VOXNAV_LIB=3d-navigation-reinforcement-learning_amd/voxnav/_lib/variants/libvoxnav_gk16.so python3 scripts/gemm_bench.py 20
 run gemm_pmc 300 env TAG=${TAG}_gpmc bash scripts/pmc_run.sh scripts/gemm_bench.py 3
 run prof 1000 env TAG=${TAG}_p PASSES=${PPASSES:-dtrace,dfetch,dwrite,trace_f1} bash scripts/profile.sh

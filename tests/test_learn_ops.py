@@ -306,3 +306,18 @@ def test_adam_step_matches_torch_fused_adam():
             for k in ("exp_avg", "exp_avg_sq"):
                 _close(opt.state[p][k], ref.state[r][k], rel=1e-5, floor=1e-12)
             assert float(opt.state[p]["step"]) == float(ref.state[r]["step"]) == it + 1
+
+
+def test_minibatch_rows_matches_index_arithmetic():
+    """The one-launch minibatch gather against the torch index arithmetic it
+    replaces (env-major ids -> [T, N]-major rows), ragged M."""
+    from voxnav.learn_ops import minibatch_rows
+    dev = "cuda:0"
+    T, N, D = 128, 1000, 80
+    obs = torch.randn((T, N, D), device=dev)
+    idx = torch.randperm(T * N, device=dev)[:4099].contiguous()
+    src, rows = minibatch_rows(idx, T, N, obs)
+    env = idx // T
+    ref = (idx - env * T) * N + env
+    assert torch.equal(src, ref)
+    assert torch.equal(rows, obs.reshape(T * N, D)[ref])
