@@ -394,11 +394,14 @@ def learner_leg(args, torch, dist, dev, world, pol, buf, kind):
     el, = _max_over_ranks(torch, dist, dev, world, time.perf_counter() - t0)
     sps = n * B * world / el
     fl = 3 * (lstm_flops_per_agent_step() if kind == "lstm" else mlp_flops_per_agent_step())  # fwd + bwd ~ 3x fwd
-    inc = ("sequence packing, actor+critic LSTM re-run (fused MFMA step kernels), MLPs (MFMA GEMM kernels), "
-           if kind == "lstm" else "minibatch gather, actor/critic MLPs, ")
+    inc = ("row layout (minibatch = whole env rollouts), actor+critic LSTM re-run in one persistent launch per "
+           "direction (weight gradients inside the backward), MLPs (direct-load MFMA GEMMs), "
+           if kind == "lstm" else "minibatch gather, actor/critic MLPs (direct-load MFMA GEMMs), ")
     return {"value": round(sps, 1), "unit": "samples/s", "batch_size": B, "minibatches": n,
             "ms_per_minibatch": round(el * 1e3 / n, 3), "tflops": round(fl * sps / 1e12, 2),
-            "includes": inc + "losses, backward, grad clip, Adam"
+            "frac_of_f32_mfma_peak": round(fl * sps / 1e12 / 157.3, 4),
+            "includes": inc + "heads + losses + their gradient (fused loss kernel), backward, gradient norm, Adam "
+                        "(library kernels)"
             + (f", gradient all-reduce ({'RCCL' if dist.get_backend() == 'nccl' else dist.get_backend()})"
                if world > 1 else "")}
 
