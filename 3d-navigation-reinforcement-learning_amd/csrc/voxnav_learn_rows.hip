@@ -35,7 +35,7 @@
 //           gate columns] @ W_hh[those rows, 256 units] (W_hh slice resident,
 //           128 VGPRs); rows whose step t starts a sequence pass no gradient
 //           back (their h_{t-1}, c_{t-1} came from the buffer).
-// f32 throughout (the reference's dtype), accurate expf / tanhf.
+// f32 throughout (the reference's dtype); the nonlinearities on the hardware exp / rcp.
 
 #include <hip/hip_runtime.h>
 
@@ -54,7 +54,10 @@ constexpr int UBK = 32;     // units per block
 constexpr int NUB = 8;      // unit blocks per LSTM (H = 256)
 constexpr uint32_t kSpinLimit = 1u << 22;   // ~0.3 s per wait at s_sleep 2
 
-__device__ __forceinline__ float sigm(float x) { return 1.0f / (1.0f + expf(-x)); }
+// gate / cell nonlinearities on the hardware exp and reciprocal (|err| <= ~4e-7,
+// the collector's f32 policy step uses the same: csrc/voxnav_policy_f32.hip)
+__device__ __forceinline__ float sigm(float x) { return __frcp_rn(1.0f + __expf(-x)); }
+__device__ __forceinline__ float tanh_fast(float x) { return 1.0f - 2.0f * __frcp_rn(1.0f + __expf(2.0f * x)); }
 
 __device__ __forceinline__ f32x16_t zero16() {
     f32x16_t z;
@@ -279,13 +282,13 @@ __global__ __launch_bounds__(256, 1) void lstm_rows_fwd_kernel(RowsFwd a) {
 #define VN_CELL(c)                                 \
     ig.c = sigm(pre[0].c);                         \
     fg.c = sigm(pre[1].c);                         \
-    gg.c = tanhf(pre[2].c);                        \
+    gg.c = tanh_fast(pre[2].c);                        \
     og.c = sigm(pre[3].c);                         \
     {                                              \
         const float fc_ = fg.c * cp.c, ig_ = ig.c * gg.c; \
         cn.c = fc_ + ig_;                          \
     }                                              \
-    hn.c = og.c * tanhf(cn.c);
+    hn.c = og.c * tanh_fast(cn.c);
             VN_CELL(x) VN_CELL(y) VN_CELL(z) VN_CELL(w)
 #undef VN_CELL
             cc = cn;
@@ -420,7 +423,7 @@ __global__ __launch_bounds__(256, 1) void lstm_rows_bwd_kernel(RowsBwd a) {
             const float4 cn = *reinterpret_cast<const float4 *>(a.cnew + so);
 #define VN_CELLB(c)                                                   \
     {                                                                 \
-        const float tc = tanhf(cn.c);                                 \
+        const float tc = tanh_fast(cn.c);                                 \
         const float dtc = dh.c * og.c;                                \
         const float dcc = dc.c + dtc * (1.0f - tc * tc);              \
         dG4[0].c = dcc * gg.c * (ig.c * (1.0f - ig.c));               \
@@ -539,13 +542,31 @@ __global__ __launch_bounds__(256, 1) void lstm_rows_bwd_kernel(RowsBwd a) {
     }
 }
 
-// out[i] = sum over row tiles (in order) of part[rt][i]
-__global__ void rows_wsum_kernel(const float *__restrict__ part, int nt, int64_t per, float *__restrict__ out) {
+// sum over row tiles (in order) of the [2][4H][H + D] weight-gradient partials,
+// written straight into the two parameters' layouts: dW_hh [2][4H][H] and
+// dW_ih [2][4H][D]
+__global__ void rows_wsum_kernel(const float *__restrict__ part, int nt, int G, int H, int D,
+                                 float *__restrict__ dw_hh, float *__restrict__ dw_ih) {
+    const int64_t per = (int64_t)2 * G * (H + D);
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= per) return;
     float s = part[i];
     for (int k = 1; k < nt; ++k) s += part[(int64_t)k * per + i];
-    out[i] = s;
+    const int64_t row = i / (H + D);
+    const int c = (int)(i - row * (H + D));
+    if (c < H) dw_hh[row * H + c] = s;
+    else dw_ih[row * D + (c - H)] = s;
+}
+
+// the bias gradient (sum over row tiles, in order) into both bias parameters
+__global__ void rows_bsum_kernel(const float *__restrict__ part, int nt, int64_t per, float *__restrict__ db_ih,
+                                 float *__restrict__ db_hh) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= per) return;
+    float s = part[i];
+    for (int k = 1; k < nt; ++k) s += part[(int64_t)k * per + i];
+    db_ih[i] = s;
+    db_hh[i] = s;
 }
 
 int rows_supported(int D, int H) { return D == 80 && H == 256; }
@@ -606,9 +627,11 @@ int vn_lstm_rows_fwd(const float *x, int32_t D, const float *w_ih, const float *
 }
 
 int vn_lstm_rows_bwd(const float *dh_out, const float *w_hh, const float *act, const float *cprev, const float *cnew,
-                     const float *hprev, const float *x, const uint8_t *start, float *dG, float *dw, float *db,
-                     float *part, uint32_t *cnt, int32_t *err, int32_t L, int32_t B, int32_t H, void *stream) {
-    if (!dh_out || !w_hh || !act || !cprev || !cnew || !hprev || !x || !start || !dw || !db || !part || !cnt || !err)
+                     const float *hprev, const float *x, const uint8_t *start, float *dG, float *dw_hh,
+                     float *dw_ih, float *db_ih, float *db_hh, float *part, uint32_t *cnt, int32_t *err, int32_t L,
+                     int32_t B, int32_t H, void *stream) {
+    if (!dh_out || !w_hh || !act || !cprev || !cnew || !hprev || !x || !start || !dw_hh || !dw_ih || !db_ih ||
+        !db_hh || !part || !cnt || !err)
         return fail(VN_ERR_INVALID, "NULL argument");
     if (!rows_supported(80, H)) return fail(VN_ERR_INVALID, "row-layout LSTM: H 256 only (got %d)", H);
     if (L < 1) return fail(VN_ERR_INVALID, "L < 1");
@@ -625,8 +648,10 @@ int vn_lstm_rows_bwd(const float *dh_out, const float *w_hh, const float *act, c
     RowsBwd a{dh_out, w_hh, act, cprev, cnew, hprev, x, start, dG, part, wpart, bpart, cnt, err, L, B, NT};
     hipLaunchKernelGGL((lstm_rows_bwd_kernel<80, 256>), dim3((unsigned)grid), dim3(256), 0, st, a);
     const int64_t pw = (int64_t)2 * 4 * H * (H + D), pb = (int64_t)2 * 4 * H;
-    hipLaunchKernelGGL(rows_wsum_kernel, dim3((unsigned)((pw + 255) / 256)), dim3(256), 0, st, wpart, NT, pw, dw);
-    hipLaunchKernelGGL(rows_wsum_kernel, dim3((unsigned)((pb + 255) / 256)), dim3(256), 0, st, bpart, NT, pb, db);
+    hipLaunchKernelGGL(rows_wsum_kernel, dim3((unsigned)((pw + 255) / 256)), dim3(256), 0, st, wpart, NT, 4 * H, H, D,
+                       dw_hh, dw_ih);
+    hipLaunchKernelGGL(rows_bsum_kernel, dim3((unsigned)((pb + 255) / 256)), dim3(256), 0, st, bpart, NT, pb, db_ih,
+                       db_hh);
     VN_HIP(hipGetLastError());
     return VN_OK;
 }

@@ -98,7 +98,8 @@ _SIGS = {
     "vn_lstm_rows_part_floats": (C.c_int, [C.c_int32, P]),
     "vn_lstm_rows_fwd": (C.c_int, [P, C.c_int32, P, P, P, P, P, C.c_int64, P, P, P, P, P, P, P, P, P, P,
                                    C.c_int32, C.c_int32, C.c_int32, P]),
-    "vn_lstm_rows_bwd": (C.c_int, [P, P, P, P, P, P, P, P, P, P, P, P, P, P, C.c_int32, C.c_int32, C.c_int32, P]),
+    "vn_lstm_rows_bwd": (C.c_int, [P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, C.c_int32, C.c_int32, C.c_int32,
+                                   P]),
     "vn_ppo_loss_part_floats": (C.c_int, [C.c_int32, C.c_int32, C.c_int32, P, P]),
     "vn_ppo_loss": (C.c_int, [P, P, C.c_int64, P, P, P, P, P, P, P, P, P, C.c_int32, C.c_int32, C.c_int32, C.c_float,
                               C.c_float, C.c_float, C.c_int32, P, P, P, P, P, P, P, P]),

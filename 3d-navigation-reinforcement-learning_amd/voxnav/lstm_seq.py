@@ -171,19 +171,21 @@ class _DualLSTMRows(torch.autograd.Function):
         _native.check(lib.vn_lstm_rows_part_floats(B, C.byref(nf)), "vn_lstm_rows_part_floats")
         part = torch.empty(nf.value, dtype=torch.float32, device=dev)
         cnt = torch.empty(2 * -(-B // 32), dtype=torch.int32, device=dev)
-        # dG and, inside the same persistent launch, [dW_hh | dW_ih] and db
-        dw = torch.empty((2, G, H + D), dtype=torch.float32, device=dev)
-        db = torch.empty((2, G), dtype=torch.float32, device=dev)
+        # dG and, inside the same persistent launch, the weight and bias gradients,
+        # written in the parameters' own layouts (no slicing copies)
+        d_w_hh = torch.empty((2, G, H), dtype=torch.float32, device=dev)
+        d_w_ih = torch.empty((2, G, D), dtype=torch.float32, device=dev)
+        db_ih = torch.empty((2, G), dtype=torch.float32, device=dev)
+        db_hh = torch.empty((2, G), dtype=torch.float32, device=dev)
         _native.check(lib.vn_lstm_rows_bwd(_p(dh_out), _p(w_hh), _p(act), _p(cprev), _p(cnew), _p(hprev), _p(xc),
-                                           _p(start), _p(dG), _p(dw), _p(db), _p(part), _p(cnt), _p(_rows_err(dev)),
-                                           L, B, H, st), "vn_lstm_rows_bwd")
-        d_w_hh, d_w_ih = dw[:, :, :H].contiguous(), dw[:, :, H:].contiguous()
+                                           _p(start), _p(dG), _p(d_w_hh), _p(d_w_ih), _p(db_ih), _p(db_hh), _p(part),
+                                           _p(cnt), _p(_rows_err(dev)), L, B, H, st), "vn_lstm_rows_bwd")
         dx = None
         if need_dx:
             dGf = dG.view(2, L * B, G)
             dx = (dGf[0] @ w_ih_a + dGf[1] @ w_ih_c).view(L, B, D)
-        return (dx, None, None, None, None, None, d_w_ih[0], d_w_hh[0], db[0].clone(), db[0].clone(), d_w_ih[1],
-                d_w_hh[1], db[1].clone(), db[1].clone())
+        return (dx, None, None, None, None, None, d_w_ih[0], d_w_hh[0], db_ih[0], db_hh[0], d_w_ih[1], d_w_hh[1],
+                db_ih[1], db_hh[1])
 
 
 _ERR = {}

@@ -430,7 +430,8 @@ int vn_lstm_seq_bwd_mfma(const float *dh_out, const float *w_hh, float *wpack, c
  *   counters (zeroed by the call; 32-row tiles); err: set to 1 if a hand-off timed out.
  * Backward: dh_out [2][L][B][H] (+ the forward's hprev, cprev, cnew, act and x) ->
  * dG [2][L][B][4H] (may be NULL) and, accumulated inside the same launch, the weight gradients
- * dw [2][4H][H + D] = [dW_hh | dW_ih] and db [2][4H] (= d b_ih = d b_hh); part:
+ * dw_hh [2][4H][H], dw_ih [2][4H][D] and db_ih, db_hh [2][4H] (equal values, separate
+ * storages: the parameters' own layouts); part:
  * vn_lstm_rows_part_floats floats of workspace.  vn_lstm_rows_supported: 1 when (D, H, B) can run (every
  * block co-resident on this device), else 0 (use vn_lstm_seq_*).
  */
@@ -441,8 +442,9 @@ int vn_lstm_rows_fwd(const float *x, int32_t D, const float *w_ih, const float *
                      const uint8_t *start, const float *keep, float *hout, float *hprev, float *cprev, float *cnew,
                      float *act, uint32_t *cnt, int32_t *err, int32_t L, int32_t B, int32_t H, void *stream);
 int vn_lstm_rows_bwd(const float *dh_out, const float *w_hh, const float *act, const float *cprev, const float *cnew,
-                     const float *hprev, const float *x, const uint8_t *start, float *dG, float *dw, float *db,
-                     float *part, uint32_t *cnt, int32_t *err, int32_t L, int32_t B, int32_t H, void *stream);
+                     const float *hprev, const float *x, const uint8_t *start, float *dG, float *dw_hh,
+                     float *dw_ih, float *db_ih, float *db_hh, float *part, uint32_t *cnt, int32_t *err, int32_t L,
+                     int32_t B, int32_t H, void *stream);
 
 /*
  * The learner's matrix products on the f32 matrix cores (csrc/voxnav_gemm_f32.hip):
