@@ -36,6 +36,7 @@ run ab_win 600 bash scripts/_ab_win.sh
 run ab_pset 600 bash scripts/_ab_pset.sh
 run ab_pset2 600 bash scripts/_ab_pset2.sh
 run ab_rowst 600 bash scripts/_ab_rowst.sh
+run ab_fill 600 bash scripts/_ab_fill.sh
 run sq_p3 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_LDS SQ_WAIT_ANY SQ_WAVE_CYCLES -d gpurun_out/${TAG}_sq_p3 -o sq --output-format csv -- python3 bench.py --steps 20 --warmup 5 --cpu-seconds 0 --single-step-check 0 --collector none --simple 0 --fuse-check 0 --episode-window 0 --room-sets P3_training --room-set-steps 256
 run learn_lstm_gk16 300 env VOXNAV_LIB=3d-navigation-reinforcement-learning_amd/voxnav/_lib/variants/libvoxnav_gk16.so python3 scripts/ppo_bench.py --agents 65536 --batch 65536 --minibatches 8 --policy lstm
 run learn_mlp_gk16 300 env VOXNAV_LIB=3d-navigation-reinforcement-learning_amd/voxnav/_lib/variants/libvoxnav_gk16.so python3 scripts/ppo_bench.py --agents 65536 --batch 65536 --minibatches 8 --policy mlp
@@ -45,6 +46,7 @@ run learn_mlp_k32 300 env VN_GEMM_GKD=32 python3 scripts/ppo_bench.py --agents 6
 run learn_mlp_plain 300 python3 scripts/ppo_bench.py --agents 65536 --batch 65536 --minibatches 8 --policy mlp
 run gemm_gk16 200 env VOXNAV_LIB=3d-navigation-reinforcement-learning_amd/voxnav/_lib/variants/libvoxnav_gk16.so python3 scripts/gemm_bench.py 20
 run gemm_pmc 300 env TAG=${TAG}_gpmc bash scripts/pmc_run.sh scripts/gemm_bench.py 3
+run learn_pmc 400 env TAG=${TAG}_lpmc bash scripts/pmc_run.sh scripts/ppo_bench.py --agents 65536 --batch 65536 --minibatches 4 --policy lstm
 run prof 1000 env TAG=${TAG}_p PASSES=${PPASSES:-dtrace,dfetch,dwrite,trace_f1} bash scripts/profile.sh
 run bench 600 python3 bench.py ${BENCH_ARGS:-}
 exit 0
