@@ -399,6 +399,25 @@ __global__ __launch_bounds__(256, 1) void lstm_rows_bwd_kernel(RowsBwd a) {
         const int t = L - 1 - s;
         // the step's sequence-start flag, loaded ahead of the hand-off wait
         const bool st_ld = !elive || t == 0 || a.start[(size_t)t * B + erow];
+        // the step's h_{t-1} and x_t rows (the weight gradients' B operands; rows
+        // past B clamped: their dG is zero), copied global -> LDS directly (no
+        // registers: the kernel sits at the VGPR cap, and register staging made
+        // the compiler serialise the loads), issued before the hand-off wait so
+        // they land while it is awaited (the previous step's weight-gradient
+        // reads of hsl / xsl ended at its closing barrier).  One wave
+        // instruction = one row.
+#pragma unroll
+        for (int i = 0; i < RW / 4; ++i) {
+            const int rr = (RW / 4) * wv + i;
+            const int row = min(row0 + rr, B - 1);
+            __builtin_amdgcn_global_load_lds(
+                (const __attribute__((address_space(1))) void *)(a.hprev + (((size_t)l * L + t) * B + row) * H + 4 * lane),
+                (__attribute__((address_space(3))) void *)&hsl[rr][0], 16, 0, 0);
+            if (lane < D / 4)
+                __builtin_amdgcn_global_load_lds(
+                    (const __attribute__((address_space(1))) void *)(a.x + ((size_t)t * B + row) * D + 4 * lane),
+                    (__attribute__((address_space(3))) void *)&xsl[rr][0], 16, 0, 0);
+        }
         if (s > 0) {
             if (tid == 0) wait_ge(cnt, (uint32_t)(NUB * s), a.err);
             __syncthreads();
@@ -481,23 +500,6 @@ __global__ __launch_bounds__(256, 1) void lstm_rows_bwd_kernel(RowsBwd a) {
             }
             publish(cnt);
         }
-        // the step's h_{t-1} and x_t rows (the weight gradients' B operands; rows
-        // past B clamped: their dG is zero), copied global -> LDS directly (no
-        // registers: the kernel sits at the VGPR cap, and register staging made
-        // the compiler serialise the loads), after the publish -- off the
-        // recurrence's critical path.  One wave instruction = one row.
-#pragma unroll
-        for (int i = 0; i < RW / 4; ++i) {
-            const int rr = (RW / 4) * wv + i;
-            const int row = min(row0 + rr, B - 1);
-            __builtin_amdgcn_global_load_lds(
-                (const __attribute__((address_space(1))) void *)(a.hprev + (((size_t)l * L + t) * B + row) * H + 4 * lane),
-                (__attribute__((address_space(3))) void *)&hsl[rr][0], 16, 0, 0);
-            if (lane < D / 4)
-                __builtin_amdgcn_global_load_lds(
-                    (const __attribute__((address_space(1))) void *)(a.x + ((size_t)t * B + row) * D + 4 * lane),
-                    (__attribute__((address_space(3))) void *)&xsl[rr][0], 16, 0, 0);
-        }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
         // weight gradients of gate wv's 32 rows (while the next hand-off is in flight):
@@ -513,8 +515,8 @@ __global__ __launch_bounds__(256, 1) void lstm_rows_bwd_kernel(RowsBwd a) {
             for (int j = 0; j < NXT; ++j)
                 xacc[j] = __builtin_amdgcn_mfma_f32_32x32x2f32(av, xsl[r][32 * j + cl], xacc[j], 0, 0, 0);
         }
-        // (the next step's LDS writes come after its wait barrier, which every
-        // wave reaches only after these reads)
+        // every wave done reading hsl / xsl before the next step's copies into them
+        __syncthreads();
         if (t == 0) break;
     }
     // per-row-tile weight-gradient partials: register v of a tile = gate row
