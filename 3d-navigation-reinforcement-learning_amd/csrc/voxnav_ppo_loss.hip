@@ -1,5 +1,7 @@
-// voxnav_ppo_loss.hip -- the PPO minibatch loss and its gradient down to the
-// MLP latents in three launches (f32, the reference's dtype).
+// voxnav_ppo_loss.hip -- the PPO learner's per-minibatch kernels around the
+// matrix products (f32, the reference's dtype): the loss and its gradient down
+// to the MLP latents in three launches, the gradient norm of the clip, the Adam
+// step, and the feed-forward minibatch gather (each below its own header).
 //
 // Restates, per minibatch, what sb3 RecurrentPPO.train / PPO.train run after
 // the MLP extractor (train/Grid_Train.py:228 -> model.learn; SURVEY.md App.

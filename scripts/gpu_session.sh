@@ -49,5 +49,6 @@ run gemm_gk16 200 env VOXNAV_LIB=3d-navigation-reinforcement-learning_amd/voxnav
 run gemm_pmc 300 env TAG=${TAG}_gpmc bash scripts/pmc_run.sh scripts/gemm_bench.py 3
 run learn_pmc 400 env TAG=${TAG}_lpmc bash scripts/pmc_run.sh scripts/ppo_bench.py --agents 65536 --batch 65536 --minibatches 4 --policy lstm
 run prof 1000 env TAG=${TAG}_p PASSES=${PPASSES:-dtrace,dfetch,dwrite,trace_f1} bash scripts/profile.sh
+run ddp2 600 env VOXNAV_BENCH_SHARED_DEVICE=1 python3 bench.py --gpus 2 --steps 256 --warmup 32 --agents 16384 --cpu-seconds 0 --simple 0 --room-sets none
 run bench 600 python3 bench.py ${BENCH_ARGS:-}
 exit 0
