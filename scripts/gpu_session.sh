@@ -38,6 +38,7 @@ run ab_pset2 600 bash scripts/_ab_pset2.sh
 run ab_rowst 600 bash scripts/_ab_rowst.sh
 run ab_fill 600 bash scripts/_ab_fill.sh
 run ab_f1obs 600 bash scripts/_ab_f1obs.sh
+run ab_rowstnt 600 bash scripts/_ab_rowstnt.sh
 run sq_p3 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_LDS SQ_WAIT_ANY SQ_WAVE_CYCLES -d gpurun_out/${TAG}_sq_p3 -o sq --output-format csv -- python3 bench.py --steps 20 --warmup 5 --cpu-seconds 0 --single-step-check 0 --collector none --simple 0 --fuse-check 0 --episode-window 0 --room-sets P3_training --room-set-steps 256
 run learn_lstm_gk16 300 env VOXNAV_LIB=3d-navigation-reinforcement-learning_amd/voxnav/_lib/variants/libvoxnav_gk16.so python3 scripts/ppo_bench.py --agents 65536 --batch 65536 --minibatches 8 --policy lstm
 run learn_mlp_gk16 300 env VOXNAV_LIB=3d-navigation-reinforcement-learning_amd/voxnav/_lib/variants/libvoxnav_gk16.so python3 scripts/ppo_bench.py --agents 65536 --batch 65536 --minibatches 8 --policy mlp
