@@ -440,8 +440,10 @@ struct AdamList {
     int count;
 };
 
-__global__ __launch_bounds__(256) void adam_kernel(AdamList al, const float *__restrict__ scale, float lr, float b1,
-                                                   float b2, float eps, float bc1, float bc2_sqrt, float step_value) {
+__global__ __launch_bounds__(256) void adam_kernel(AdamList al, const float *__restrict__ scale,
+                                                   const int32_t *__restrict__ skip, float lr, float b1, float b2,
+                                                   float eps, float bc1, float bc2_sqrt, float step_value) {
+    if (skip && skip[0] != 0) return;   // gradients from a failed launch: leave every tensor as it was
     const bool div = scale != nullptr;
     const float s = scale ? scale[0] : 1.0f;
     const float step_size = lr / bc1;
@@ -570,8 +572,8 @@ int vn_grad_norm(const float *const *grads, const int64_t *sizes, int32_t count,
 }
 
 int vn_adam_step(float *const *params, const float *const *grads, float *const *exp_avg, float *const *exp_avg_sq,
-                 float *const *steps, const int64_t *sizes, int32_t count, const float *clip_scale, float lr,
-                 float beta1, float beta2, float eps, int64_t step, void *stream) {
+                 float *const *steps, const int64_t *sizes, int32_t count, const float *clip_scale,
+                 const int32_t *skip, float lr, float beta1, float beta2, float eps, int64_t step, void *stream) {
     if (!params || !grads || !exp_avg || !exp_avg_sq || !sizes) return fail(VN_ERR_INVALID, "NULL argument");
     if (count < 1 || count > kMaxGradTensors)
         return fail(VN_ERR_INVALID, "parameter count %d outside 1..%d", count, kMaxGradTensors);
@@ -593,8 +595,8 @@ int vn_adam_step(float *const *params, const float *const *grads, float *const *
     const double bc1 = 1.0 - pow((double)beta1, (double)step), bc2 = 1.0 - pow((double)beta2, (double)step);
     int blocks = (int)((total / 4 + 255) / 256);
     blocks = blocks < 1 ? 1 : (blocks > 2048 ? 2048 : blocks);
-    hipLaunchKernelGGL(adam_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, al, clip_scale, lr, beta1, beta2,
-                       eps, (float)bc1, (float)sqrt(bc2), (float)step);
+    hipLaunchKernelGGL(adam_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, al, clip_scale, skip, lr, beta1,
+                       beta2, eps, (float)bc1, (float)sqrt(bc2), (float)step);
     VN_HIP(hipGetLastError());
     return VN_OK;
 }

@@ -104,7 +104,7 @@ _SIGS = {
     "vn_ppo_loss": (C.c_int, [P, P, C.c_int64, P, P, P, P, P, P, P, P, P, C.c_int32, C.c_int32, C.c_int32, C.c_float,
                               C.c_float, C.c_float, C.c_int32, P, P, P, P, P, P, P, P]),
     "vn_grad_norm": (C.c_int, [P, P, C.c_int32, C.c_float, P, P, P, P]),
-    "vn_adam_step": (C.c_int, [P, P, P, P, P, P, C.c_int32, P, C.c_float, C.c_float, C.c_float, C.c_float,
+    "vn_adam_step": (C.c_int, [P, P, P, P, P, P, C.c_int32, P, P, C.c_float, C.c_float, C.c_float, C.c_float,
                                C.c_int64, P]),
     "vn_minibatch_rows": (C.c_int, [P, C.c_int32, C.c_int32, C.c_int32, P, C.c_int32, P, P, P]),
     "vn_gemm_f32_linear": (C.c_int, [P, C.c_int64, C.c_int64, P, C.c_int64, C.c_int64, P, C.c_int64, P, C.c_int64,

@@ -184,10 +184,26 @@ def load_checkpoint(path: Union[str, Path], device="cpu") -> Tuple[torch.nn.Modu
 
 
 def load_optimizer_state(path: Union[str, Path], optimizer: torch.optim.Optimizer) -> bool:
-    """Restore ``policy.optimizer.pth`` into ``optimizer`` (False if absent)."""
+    """Restore ``policy.optimizer.pth`` into ``optimizer`` (False if absent).
+
+    The file's hyperparameters and moments are loaded; the execution flags of
+    the target groups (``fused`` / ``foreach`` / ``capturable``: how this
+    build runs the step, saved as torch's defaults) are kept, and the
+    per-parameter ``step`` counters are moved next to their parameters as
+    f32 scalars -- what the learner's fused step (``PPOLearner._clip_step``,
+    ``learn_ops.adam_step``) expects, so a resumed run stays on it."""
     with zipfile.ZipFile(path) as z:
         if "policy.optimizer.pth" not in z.namelist():
             return False
         st = torch.load(io.BytesIO(z.read("policy.optimizer.pth")), map_location="cpu", weights_only=True)
+    flags = [{k: g[k] for k in ("fused", "foreach", "capturable") if k in g} for g in optimizer.param_groups]
     optimizer.load_state_dict(st)
+    for g, f in zip(optimizer.param_groups, flags):
+        g.update(f)
+        if not g.get("fused"):
+            continue
+        for prm in g["params"]:
+            s = optimizer.state.get(prm)
+            if s and "step" in s and torch.is_tensor(s["step"]):
+                s["step"] = s["step"].to(device=prm.device, dtype=torch.float32)
     return True

@@ -275,14 +275,17 @@ def grad_norm_scale(params, max_norm: float, work: Optional[torch.Tensor] = None
     return out[0], out[1]
 
 
-def adam_step(optimizer: torch.optim.Adam, clip_scale: Optional[torch.Tensor] = None) -> None:
+def adam_step(optimizer: torch.optim.Adam, clip_scale: Optional[torch.Tensor] = None,
+              skip: Optional[torch.Tensor] = None) -> None:
     """``optimizer.step()`` for a single-group ``torch.optim.Adam`` (no
     amsgrad / weight decay / maximize) on the library's kernel
     (csrc/voxnav_ppo_loss.hip vn_adam_step): one launch over every parameter,
     the gradients divided by ``clip_scale`` (``grad_norm_scale``'s divisor) on
     the way.  The optimizer's own state tensors are updated in place
     (``exp_avg``, ``exp_avg_sq``, ``step``), so ``state_dict()`` / checkpoints
-    are torch's."""
+    are torch's.  ``skip``: a device int32 word; when it is nonzero at run
+    time the step changes nothing (the row-layout LSTM's error word: the
+    gradients of a timed-out launch are never applied)."""
     lib = _native.load()
     if len(optimizer.param_groups) != 1:
         raise ValueError("adam_step: one parameter group")
@@ -321,7 +324,7 @@ def adam_step(optimizer: torch.optim.Adam, clip_scale: Optional[torch.Tensor] = 
     _native.check(lib.vn_adam_step(arr(params), arr([p.grad for p in params]),
                                    arr([optimizer.state[p]["exp_avg"] for p in params]),
                                    arr([optimizer.state[p]["exp_avg_sq"] for p in params]), steps_arr, sizes, n,
-                                   _p(clip_scale), float(grp["lr"]), float(b1), float(b2), float(grp["eps"]), t,
+                                   _p(clip_scale), _p(skip), float(grp["lr"]), float(b1), float(b2), float(grp["eps"]), t,
                                    _stream(dev)), "vn_adam_step")
     for s, x in zip(steps, st_ptrs):
         if x is None:                       # a CPU / other-dtype step counter (a loaded state): set on the host

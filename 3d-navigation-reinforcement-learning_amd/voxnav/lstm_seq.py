@@ -199,6 +199,12 @@ def _rows_err(dev) -> torch.Tensor:
     return _ERR[key]
 
 
+def rows_err_word(dev):
+    """The device error word of the row-layout launches on ``dev`` (None before
+    the first one): what the learner's Adam step is gated on."""
+    return _ERR.get(str(dev))
+
+
 def rows_check(dev) -> None:
     """Raise if a row-layout launch on `dev` timed out (one host read)."""
     e = _ERR.get(str(dev))

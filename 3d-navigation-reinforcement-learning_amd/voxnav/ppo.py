@@ -86,6 +86,11 @@ class PPOLearner:
         # the Adam step on the library's kernel (learn_ops.adam_step, the optimizer's
         # own state tensors); VOXNAV_NATIVE_ADAM=0: torch's fused Adam
         self.native_adam = os.environ.get("VOXNAV_NATIVE_ADAM", "1") != "0"
+        # the row-layout LSTM keeps all its blocks resident and hands states over
+        # inside the launch: with another rank's grid on the same device that
+        # co-residency is not guaranteed, so such ranks take the packed path
+        self._rows_off = self.recurrent and process_group is not None and _ranks_share_device(process_group,
+                                                                                             self.params)
 
     # ------------------------------------------------------------ helpers
     def _orders(self, total: int) -> List:
@@ -119,14 +124,19 @@ class PPOLearner:
         entropy = -(logp_all.exp() * logp_all).sum(-1)
         return values, log_prob, entropy
 
-    def _pack_begin(self, buf, idx: torch.Tensor) -> dict:
+    def _pack_begin(self, buf, idx: torch.Tensor, window: bool = False) -> dict:
         """The sequence structure of minibatch rows ``idx`` (env-major flat
         ids): sequences start at episode starts and env changes
         (sb3_contrib create_sequencers).  Everything but the padded size
         (n_seq, max_len) stays on the device; on CUDA the structure is
         computed on a side stream and the size copied to pinned host memory,
         so the one host read per minibatch can wait for it while the previous
-        minibatch's update still runs (``update_many``)."""
+        minibatch's update still runs (``update_many``).
+
+        ``window``: the caller guarantees ``idx`` is one contiguous window of
+        the rolled env-major order (``(idx[0] + i) mod T N``, what ``train``
+        cuts) -- the row layout's mapping is only valid for such minibatches;
+        any other index set takes the packed per-sequence path."""
         T, N = buf.actions.shape
         dev = idx.device
         side = None
@@ -136,7 +146,7 @@ class PPOLearner:
             side = self._side
             side.wait_stream(torch.cuda.current_stream(dev))
         n = idx.numel()
-        rows = n // T if (dev.type == "cuda" and n % T == 0 and n // T <= N) else 0
+        rows = n // T if (window and dev.type == "cuda" and n % T == 0 and n // T <= N) else 0
         if rows and not self._rows_ok(buf.obs.shape[-1], rows):
             rows = 0
         with torch.cuda.stream(side) if side is not None else _nullctx():
@@ -201,7 +211,8 @@ class PPOLearner:
         key = (D, rows)
         if key not in cache:
             # VOXNAV_LSTM_ROWS=0: the per-sequence packed path (A/B knob)
-            cache[key] = os.environ.get("VOXNAV_LSTM_ROWS", "1") != "0" and lstm_seq.rows_supported(self.policy, D, rows)
+            cache[key] = (not self._rows_off and os.environ.get("VOXNAV_LSTM_ROWS", "1") != "0"
+                          and lstm_seq.rows_supported(self.policy, D, rows))
         return cache[key]
 
     def _evaluate_rows(self, buf, pk: dict):
@@ -330,7 +341,11 @@ class PPOLearner:
         if fused and self.params[0].is_cuda:
             gnorm, scale = learn_ops.grad_norm_scale(self.params, self.max_grad_norm)
             if self.native_adam:
-                learn_ops.adam_step(self.optimizer, scale)
+                # the recurrent learner's row-layout launches set a device error word
+                # when an in-launch hand-off times out; the step is skipped on the
+                # device while it is set (rows_check raises after the minibatches)
+                skip = lstm_seq.rows_err_word(self.params[0].device) if self.recurrent else None
+                learn_ops.adam_step(self.optimizer, scale, skip=skip)
             else:
                 self.optimizer.grad_scale = scale
                 try:
@@ -343,23 +358,31 @@ class PPOLearner:
         self.n_updates += 1
         return gnorm
 
-    def update_many(self, buf, idxs: Sequence[torch.Tensor]) -> torch.Tensor:
+    def update_many(self, buf, idxs: Sequence[torch.Tensor], windows: bool = False) -> torch.Tensor:
         """``update`` over consecutive minibatches, the next minibatch's
         sequence structure computed (side stream) while this one's update is
         queued, so the host read of its size does not idle the GPU.
-        Returns the stacked logs [n, 7]."""
+        ``windows``: every ``idx`` is a contiguous window of the rolled
+        env-major order (``train``'s minibatches), which lets whole-rollout
+        minibatches take the row-layout LSTM.  Returns the stacked logs [n, 7]."""
         idxs = list(idxs)
         if not idxs:
             return torch.zeros((0, 7), dtype=torch.float64)
-        nxt = self._pack_begin(buf, idxs[0]) if self.recurrent else None
+        nxt = self._pack_begin(buf, idxs[0], windows) if self.recurrent else None
         logs = []
         for i, idx in enumerate(idxs):
             cur = nxt
             if self.recurrent and i + 1 < len(idxs):
-                nxt = self._pack_begin(buf, idxs[i + 1])
+                nxt = self._pack_begin(buf, idxs[i + 1], windows)
             logs.append(self.update(buf, idx, packed=cur))
         if self.recurrent and idxs[0].is_cuda:
-            lstm_seq.rows_check(idxs[0].device)      # a timed-out row-layout launch raises
+            try:
+                lstm_seq.rows_check(idxs[0].device)      # a timed-out row-layout launch raises
+            except Exception:
+                # the skipped Adam steps did not advance the device step counters:
+                # re-read them on the next step
+                self.optimizer._vn_adam_t = None
+                raise
         return torch.stack(logs)
 
     # ------------------------------------------------------------ train
@@ -380,7 +403,8 @@ class PPOLearner:
                 perm = torch.roll(torch.arange(total, device=dev), -int(order))
             else:
                 perm = torch.as_tensor(np.asarray(order), dtype=torch.int64, device=dev)
-            logs = self.update_many(buf, [perm[s:s + self.batch_size] for s in range(0, total, self.batch_size)])
+            logs = self.update_many(buf, [perm[s:s + self.batch_size] for s in range(0, total, self.batch_size)],
+                                    windows=self.recurrent)
             acc += logs.sum(0)
             n_mb += logs.shape[0]
         m = (acc / max(1, n_mb)).tolist()
@@ -391,6 +415,20 @@ class PPOLearner:
         return dict(policy_gradient_loss=m[0], value_loss=m[1], entropy_loss=m[2], loss=m[3], approx_kl=m[4],
                     clip_fraction=m[5], grad_norm=m[6], explained_variance=ev, n_minibatches=n_mb,
                     n_updates=self.n_updates)
+
+
+def _ranks_share_device(group, params) -> bool:
+    """Whether another rank of ``group`` drives the same GPU as this one (one
+    all-gather of (host, device uuid) at construction; False off the GPU)."""
+    if not params or not params[0].is_cuda:
+        return False
+    import socket
+    import torch.distributed as dist
+    dev = params[0].device
+    me = (socket.gethostname(), str(torch.cuda.get_device_properties(dev).uuid))
+    allk = [None] * dist.get_world_size(group)
+    dist.all_gather_object(allk, me, group=group)
+    return allk.count(me) > 1
 
 
 def learn(collector, learner: PPOLearner, total_timesteps: int, callback=None) -> List[Dict[str, float]]:

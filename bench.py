@@ -381,13 +381,14 @@ def learner_leg(args, torch, dist, dev, world, pol, buf, kind):
     perm = torch.roll(torch.arange(T * N, device=dev), -12345 % (T * N))
     if kind == "mlp":
         perm = torch.randperm(T * N, device=dev, generator=torch.Generator(device=dev).manual_seed(0))
-    ln.update_many(buf, [perm[m * B:(m + 1) * B] for m in range(2)])
+    win = kind == "lstm"          # rolled contiguous windows, as train() cuts them
+    ln.update_many(buf, [perm[m * B:(m + 1) * B] for m in range(2)], windows=win)
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
     t0 = time.perf_counter()
     nb = (T * N) // B
-    ln.update_many(buf, [perm[(m % nb) * B:(m % nb + 1) * B] for m in range(n)])
+    ln.update_many(buf, [perm[(m % nb) * B:(m % nb + 1) * B] for m in range(n)], windows=win)
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()

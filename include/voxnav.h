@@ -500,9 +500,13 @@ int vn_grad_norm(const float *const *grads, const int64_t *sizes, int32_t count,
  * lr 3e-4): the gradients divided by *clip_scale (vn_grad_norm's divisor; NULL:
  * 1), then torch's fused-Adam update with the bias corrections of `step`
  * (1-based); `steps` (nullable) receive the step count (torch's per-parameter
- * state["step"] scalars).  The gradients are not rewritten. */
+ * state["step"] scalars).  The gradients are not rewritten.  skip (nullable
+ * device int32): when *skip != 0 at run time the launch changes nothing --
+ * the learner passes the row-layout LSTM's error word (vn_lstm_rows_fwd/bwd
+ * `err`), so gradients from a timed-out launch never reach the parameters. */
 int vn_adam_step(float *const *params, const float *const *grads, float *const *exp_avg, float *const *exp_avg_sq,
-                 float *const *steps, const int64_t *sizes, int32_t count, const float *clip_scale, float lr,
+                 float *const *steps, const int64_t *sizes, int32_t count, const float *clip_scale,
+                 const int32_t *skip, float lr,
                  float beta1, float beta2, float eps, int64_t step, void *stream);
 
 /* A PPO minibatch's rows (sb3 PPO.train over the env-major flattened rollout

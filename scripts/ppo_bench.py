@@ -44,10 +44,10 @@ def main():
         # time individual minibatches through the learner's internals
         idx_all = torch.roll(torch.arange(total, device=dev), -split)
         ln.optimizer.zero_grad()
-        ln.update_many(buf, [idx_all[w * B:(w + 1) * B] for w in range(2)])
+        ln.update_many(buf, [idx_all[w * B:(w + 1) * B] for w in range(2)], windows=True)
         torch.cuda.synchronize()
         t0 = time.perf_counter()
-        ln.update_many(buf, [idx_all[m * B:(m + 1) * B] for m in range(nmb)])
+        ln.update_many(buf, [idx_all[m * B:(m + 1) * B] for m in range(nmb)], windows=True)
         torch.cuda.synchronize()
         el = time.perf_counter() - t0
         sps = nmb * B / el

@@ -506,3 +506,89 @@ def test_linear_f32_exact_mapping(voxnav, M, K, nout, nb):
                 np.testing.assert_allclose(got, np.tanh(ref), atol=1e-6, rtol=1e-5)   # hardware exp / rcp
             else:
                 np.testing.assert_array_equal(got, ref.astype(np.float32))
+
+
+# ---------------------------------------------------------------- bench shapes
+# The collector bench (C4: 65,536 agents, H = 256) runs the persistent fused
+# LSTM kernel with n_items = ceil(N / 128) x 2 LSTMs x H / 64 far above its
+# 2-blocks-per-CU slots, so every block walks several items and the K-chunk
+# stream runs on across them; these cases take that branch (and an N % 128
+# tail) on exact data, with the float64 restatement computed on the device.
+def _f64_lstm_ref(x, h_in, c0, w_ih, w_hh, bias, start):
+    keep = (start == 0).view(1, -1, 1) if start is not None else None
+    hm = h_in if keep is None else torch.where(keep, h_in, 0.0)
+    cm = c0 if keep is None else torch.where(keep, c0, 0.0)
+    d = torch.float64
+    pre = (torch.einsum("nk,bgk->bng", x.to(d), w_ih.to(d)) + torch.einsum("bnk,bgk->bng", hm.to(d), w_hh.to(d))
+           + bias.to(d)[:, None, :])
+    i, f, g, o = pre.chunk(4, dim=-1)
+    c1 = torch.sigmoid(f) * cm.to(d) + torch.sigmoid(i) * torch.tanh(g)
+    return torch.sigmoid(o) * torch.tanh(c1), c1
+
+
+@pytest.mark.parametrize("N,masked", [(65536 + 77, True), (65536, False)])
+def test_fused_f32_lstm_bench_shape(voxnav, N, masked):
+    """vn_lstm_fused_f32 at the collector bench's shape (H = 256, both LSTMs,
+    65,536 agents and a ragged 65,613) -- the multi-item persistent path --
+    against float64 on exact small-integer / 8 data: every row of h and c
+    within 2e-6 (the gate sums are exact; only the hardware exp / rcp of the
+    nonlinearities round)."""
+    import ctypes as C
+    from voxnav.collector import pack_lstm_f32
+    lib = voxnav.load_library()
+    dev = "cuda:0"
+    B, H, od = 2, 256, 80
+    g = torch.Generator(device=dev).manual_seed(N)
+    ri = lambda lo, hi, shape, den: (torch.randint(lo, hi + 1, shape, generator=g, device=dev) / den).float()  # noqa: E731
+    x = ri(-4, 4, (N, od), 8.0)
+    h_in = ri(-4, 4, (B, N, H), 8.0)
+    w_ih = ri(-3, 3, (B, 4 * H, od), 8.0)
+    w_hh = ri(-3, 3, (B, 4 * H, H), 8.0)
+    bias = ri(-8, 8, (B, 4 * H), 8.0)
+    c0 = torch.randn((B, N, H), generator=g, device=dev)
+    start = (torch.rand(N, generator=g, device=dev) < 0.3).float() if masked else None
+    wp = pack_lstm_f32([w_ih[b].contiguous() for b in range(B)], [w_hh[b].contiguous() for b in range(B)])
+    Kp = (od + 15) // 16 * 16 + H
+    c_out = torch.full((B, N, H), float("nan"), device=dev)
+    h_out = torch.full((B, N, H), float("nan"), device=dev)
+    p = lambda a: None if a is None else C.c_void_p(a.data_ptr())  # noqa: E731
+    assert lib.vn_lstm_fused_f32(p(x), od, p(h_in), p(wp), Kp, p(bias), p(c0), p(start), p(c_out), p(h_out), B, N, H,
+                                 None) == 0
+    torch.cuda.synchronize()
+    h1, c1 = _f64_lstm_ref(x, h_in, c0, w_ih, w_hh, bias, start)
+    for got, ref, what in ((c_out, c1, "c"), (h_out, h1, "h")):
+        err = (got.double() - ref).abs() - 2e-6 * ref.abs()
+        bad = err > 2e-6
+        assert not bool(bad.any()), f"{what}: {int(bad.sum())} of {bad.numel()} out of tolerance, " \
+                                    f"rows {torch.nonzero(bad.any(-1).any(0)).flatten()[:8].tolist()}"
+
+
+@pytest.mark.parametrize("M,K,nout", [(65536 + 33, 256, 256), (65536 + 33, 256, 128), (65536, 80, 256)])
+def test_linear_f32_bench_shape(voxnav, M, K, nout):
+    """vn_linear_f32 at the collector bench's row count (65,536 agents and a
+    ragged 65,569; the MLP layers 80->256, 256->256, 256->128 of both
+    branches in one launch) against float64 on exact data: the identity form
+    bitwise, the Tanh form within 1e-6 + 1e-5 |y|."""
+    import ctypes as C
+    from voxnav.collector import pack_linear_f32
+    lib = voxnav.load_library()
+    dev = "cuda:0"
+    g = torch.Generator(device=dev).manual_seed(M + K + nout)
+    ri = lambda lo, hi, shape, den: (torch.randint(lo, hi + 1, shape, generator=g, device=dev) / den).float()  # noqa: E731
+    xs = [ri(-4, 4, (M, K), 8.0) for _ in range(2)]
+    ws = [ri(-3, 3, (nout, K), 16.0) for _ in range(2)]
+    bs = [ri(-8, 8, (nout,), 8.0) for _ in range(2)]
+    tw = [pack_linear_f32(w) for w in ws]
+    arr = lambda ts: (C.c_void_p * 2)(*[t.data_ptr() for t in ts])  # noqa: E731
+    for act in (1, 0):
+        ty = [torch.full((M, nout), float("nan"), device=dev) for _ in range(2)]
+        assert lib.vn_linear_f32(2, arr(xs), K, arr(tw), arr(bs), arr(ty), M, K, nout, act, None) == 0
+        torch.cuda.synchronize()
+        for i in range(2):
+            ref = xs[i].double() @ ws[i].double().T + bs[i].double()
+            if act:
+                ref = torch.tanh(ref)
+                bad = (ty[i].double() - ref).abs() > 1e-6 + 1e-5 * ref.abs()
+                assert not bool(bad.any()), f"branch {i}: {int(bad.sum())} out of tolerance"
+            else:
+                assert torch.equal(ty[i], ref.float()), f"branch {i}: identity form not exact"

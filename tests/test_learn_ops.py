@@ -145,14 +145,16 @@ def _rows_reference(x, env, start, keep, hs, cs, lstm, l):
     return torch.stack(outs)
 
 
-@pytest.mark.parametrize("L,B,N,p_start", [(24, 512, 600, 0.03), (9, 37, 40, 0.2), (128, 64, 64, 0.01)])
+@pytest.mark.parametrize("L,B,N,p_start", [(24, 512, 600, 0.03), (9, 37, 40, 0.2), (128, 64, 64, 0.01),
+                                           (128, 512, 512, 0.004)])
 def test_dual_lstm_rows_matches_float64(L, B, N, p_start):
     """The persistent row-layout LSTM (csrc/voxnav_learn_rows.hip: weights
     resident, in-launch h / partial-dh hand-offs between the 8 unit blocks of a
     row tile) against a float64 restatement: outputs and the weight / bias
     gradients of both LSTMs, with sequence starts (stored states x keep) at t = 0,
-    at random steps and mid-row; full 512-row tiles, a ragged last tile, and a
-    whole 128-step rollout."""
+    at random steps and mid-row; full 512-row tiles, a ragged last tile, a
+    whole 128-step rollout, and the learner bench's own shape (512 rows x 128
+    steps: every block of the launch resident, 128 hand-offs per direction)."""
     from types import SimpleNamespace
     from voxnav import lstm_seq
     dev = "cuda:0"

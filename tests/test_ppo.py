@@ -74,7 +74,7 @@ def _as_rollout(b, device):
 
 
 def _run_parity(device, recurrent, T=12, N=5, batch_size=16, epochs=2, full=False, p_start=0.15, atol=2e-5,
-                rtol=1e-4):
+                rtol=1e-4, want_rows=None):
     from voxnav.policy import numpy_weights
     from voxnav.ppo import PPOLearner
     pol = _policy(recurrent, full=full).to(device)
@@ -86,6 +86,8 @@ def _run_parity(device, recurrent, T=12, N=5, batch_size=16, epochs=2, full=Fals
               else [rng.permutation(T * N) for _ in range(epochs)])
     ln = PPOLearner(pol, n_epochs=epochs, batch_size=batch_size)
     st = ln.train(_as_rollout(b, device), epoch_orders=orders)
+    if want_rows is not None:      # which LSTM re-run the minibatches took
+        assert any(ln.__dict__.get("_rows_cache", {}).values()) == want_rows
     w1, ost, _ = po.train(w0, b, orders, batch_size=batch_size)
     got = numpy_weights(pol)
     moved = 0.0
@@ -135,6 +137,80 @@ def test_learner_full_size_matches_oracle_gpu(recurrent):
                       atol=5e-5, rtol=1e-3)
     if recurrent:   # long sequences: on average >= 24 steps each (most run whole 128-step rollouts)
         assert 24 * sum(s["n_seq"] for s in ost) <= 2 * 128 * 8
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("recurrent", [True, False], ids=["lstm", "mlp"])
+def test_learner_bench_shape_minibatch_matches_oracle_gpu(recurrent):
+    """One minibatch at the learner bench's own shape -- 65,536 samples = 512
+    env rollouts x 128 steps (the row-layout LSTM with every one of its 256
+    blocks resident; the MLP / loss / norm / Adam kernels at M = 65,536), the
+    reference's policy -- against the f64 restatement: one train() call of
+    one epoch, one Adam step.  Tolerance as the full-size test."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    _run_parity("cuda:0", recurrent, T=128, N=512, batch_size=65536, epochs=1, full=True, p_start=0.004,
+                atol=5e-5, rtol=1e-3, want_rows=True if recurrent else None)
+
+
+@pytest.mark.gpu
+def test_row_layout_error_word_skips_the_update():
+    """A row-layout launch whose in-launch hand-off timed out (device error
+    word set) must not update the parameters: the Adam step is gated on the
+    word on the device, train() raises, and after the raise the learner
+    trains normally with the step count re-read from the device."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from voxnav import _native, lstm_seq
+    from voxnav.ppo import PPOLearner
+    dev = "cuda:0"
+    pol = _policy(True, full=True).to(dev)
+    T, N = 16, 8
+    b = _buffer(T, N, 256, True, p_start=0.05)
+    ln = PPOLearner(pol, n_epochs=1, batch_size=T * N)
+    buf = _as_rollout(b, dev)
+    ln.train(buf, epoch_orders=[3])                      # a good step first: moments and step = 1
+    assert any(ln._rows_cache.values()), "the row layout must be the path under test"
+    w0 = [p.detach().clone() for p in pol.parameters()]
+    m0 = [ln.optimizer.state[p]["exp_avg"].clone() for p in pol.parameters()]
+    lstm_seq._rows_err(torch.device(dev)).fill_(1)       # as a timed-out hand-off leaves it
+    with pytest.raises(_native.VoxnavError):
+        ln.train(buf, epoch_orders=[5])
+    for p, w, m in zip(pol.parameters(), w0, m0):
+        assert torch.equal(p.detach(), w) and torch.equal(ln.optimizer.state[p]["exp_avg"], m)
+    assert all(float(ln.optimizer.state[p]["step"]) == 1.0 for p in pol.parameters())
+    ln.train(buf, epoch_orders=[5])                      # the word was cleared by the raise
+    assert all(float(ln.optimizer.state[p]["step"]) == 2.0 for p in pol.parameters())
+    assert any(not torch.equal(p.detach(), w) for p, w in zip(pol.parameters(), w0))
+
+
+@pytest.mark.gpu
+def test_optimizer_resume_keeps_fused_step(tmp_path):
+    """A learner resumed from a checkpoint stays on the fused step: the
+    loaded groups keep fused=True and the step counters are f32 device
+    scalars, and the next update equals the one of the never-saved learner."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from voxnav.checkpoint import load_optimizer_state, save_checkpoint
+    from voxnav.ppo import PPOLearner
+    dev = "cuda:0"
+    b = _buffer(12, 5, 16, True)
+    pol = _policy(True).to(dev)
+    ln = PPOLearner(pol, n_epochs=1, batch_size=16)
+    ln.train(_as_rollout(b, dev), epoch_orders=[4])
+    path = save_checkpoint(tmp_path / "r", pol, ln.optimizer)
+    pol2 = _policy(True).to(dev)
+    pol2.load_state_dict(pol.state_dict())
+    ln2 = PPOLearner(pol2, n_epochs=1, batch_size=16)
+    assert load_optimizer_state(path, ln2.optimizer)
+    assert ln2.optimizer.param_groups[0]["fused"] is True
+    for p in pol2.parameters():
+        s = ln2.optimizer.state[p]["step"]
+        assert s.device == p.device and s.dtype == torch.float32
+    ln.train(_as_rollout(b, dev), epoch_orders=[7])
+    ln2.train(_as_rollout(b, dev), epoch_orders=[7])
+    for p, q in zip(pol.parameters(), pol2.parameters()):
+        assert torch.equal(p, q)
 
 
 @pytest.mark.gpu
