@@ -23,7 +23,7 @@
     defined(VN_STAGE_OBS) || defined(VN_LF_ROWS) || defined(VN_LF_KC) || defined(VN_LF_RAW_BARRIER) || \
     defined(VN_LF_MIN_WAVES) || defined(VN_LF_WPE) || defined(VN_STOOD) || defined(VN_DPP) || \
     defined(VN_TAB_SWZ) || defined(VN_PF_FAST) || defined(VN_PF_PREF) || defined(VN_OBS_STORE) || \
-    defined(VN_LDS_BARRIER)
+    defined(VN_LDS_BARRIER) || defined(VN_ROW_WB)
 #error "compile-time knobs are for the diagnostics build only (define VN_DIAG)"
 #endif
 #endif
@@ -40,6 +40,29 @@ inline int fail(int code, const char *fmt, ...) {
     va_end(ap);
     g_last_error = buf;
     return code;
+}
+
+// Philox4x32-10 (same rounds as the env's random policy), word 0: the
+// collector's Categorical draws.  The sampler's counter is (global agent id,
+// t | 2^63), so it never collides with the env's random-policy stream (gid,
+// t / 4) under the same key.
+__device__ __forceinline__ uint32_t philox_word0(uint64_t key, uint64_t gid, uint64_t ctr_hi) {
+    uint32_t c0 = (uint32_t)gid, c1 = (uint32_t)(gid >> 32), c2 = (uint32_t)ctr_hi, c3 = (uint32_t)(ctr_hi >> 32);
+    uint32_t k0 = (uint32_t)key, k1 = (uint32_t)(key >> 32);
+#pragma unroll
+    for (int r = 0; r < 10; ++r) {
+        if (r) {
+            k0 += 0x9E3779B9u;
+            k1 += 0xBB67AE85u;
+        }
+        const uint32_t lo0 = 0xD2511F53u * c0, hi0 = __umulhi(0xD2511F53u, c0);
+        const uint32_t lo1 = 0xCD9E8D57u * c2, hi1 = __umulhi(0xCD9E8D57u, c2);
+        c0 = hi1 ^ c1 ^ k0;
+        c1 = lo1;
+        c2 = hi0 ^ c3 ^ k1;
+        c3 = lo0;
+    }
+    return c0;
 }
 
 }  // namespace vn_detail

@@ -59,27 +59,7 @@ __device__ __forceinline__ float4 load4<uint16_t>(const uint16_t *p) {
     return make_float4(bf2f(v.x & 0xffffu), bf2f(v.x >> 16), bf2f(v.y & 0xffffu), bf2f(v.y >> 16));
 }
 
-// Philox4x32-10 (same rounds as the env's random policy); the sampler's
-// counter is (global agent id, t | 2^63) so it never collides with the
-// env's random-policy stream (gid, t / 4) under the same key.
-__device__ __forceinline__ uint32_t philox_word0(uint64_t key, uint64_t gid, uint64_t ctr_hi) {
-    uint32_t c0 = (uint32_t)gid, c1 = (uint32_t)(gid >> 32), c2 = (uint32_t)ctr_hi, c3 = (uint32_t)(ctr_hi >> 32);
-    uint32_t k0 = (uint32_t)key, k1 = (uint32_t)(key >> 32);
-#pragma unroll
-    for (int r = 0; r < 10; ++r) {
-        if (r) {
-            k0 += 0x9E3779B9u;
-            k1 += 0xBB67AE85u;
-        }
-        const uint32_t lo0 = 0xD2511F53u * c0, hi0 = __umulhi(0xD2511F53u, c0);
-        const uint32_t lo1 = 0xCD9E8D57u * c2, hi1 = __umulhi(0xCD9E8D57u, c2);
-        c0 = hi1 ^ c1 ^ k0;
-        c1 = lo1;
-        c2 = hi0 ^ c3 ^ k1;
-        c3 = lo0;
-    }
-    return c0;
-}
+using vn_detail::philox_word0;
 
 // ----------------------------------------------------------------------------
 // LSTM cell, torch gate order (i, f, g, o):

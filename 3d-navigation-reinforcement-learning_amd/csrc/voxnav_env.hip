@@ -454,7 +454,15 @@ __device__ __forceinline__ uint32_t group_or(uint32_t m) {
 struct PlaneCache {      // lane 0: x-plane row, lane 1: y-plane row
     uint64_t w[2];
     int row, w0;         // cached row index and first word; row < 0: invalid
+    uint32_t dirty;      // VN_ROW_WB: words 0 / 1 changed since loaded (written back when the row is left)
 };
+
+// DM (PCM 3): the cached plane row is write-back -- a pass's new row bits stay
+// in the lane's registers until the agent leaves the row (or the launch ends)
+// instead of one 8-byte store per step that marks it.
+#ifndef VN_ROW_WB
+#define VN_ROW_WB 0
+#endif
 
 // Fill the tile from HBM (launch start): lane q loads its 4 window columns.
 // PC: the plane sets (ps, already filled) add their known bits.
@@ -561,7 +569,7 @@ __device__ __forceinline__ uint32_t tile_shift_commit(uint64_t *tile, const Shif
 // in the cache, loaded here together with the step's other loads; wider
 // rooms load a 2-word window lazily inside sense_observe.
 template <int PH>
-__device__ __forceinline__ void plane_prefetch(const Params &p, const int8_t *map, PlaneCache &pc_, int x, int y,
+__device__ __forceinline__ void plane_prefetch(const Params &p, int8_t *map, PlaneCache &pc_, int x, int y,
                                                int z, int q) {
     if (q < 2) {
         const bool xr = q == 0;
@@ -569,14 +577,36 @@ __device__ __forceinline__ void plane_prefetch(const Params &p, const int8_t *ma
         if (nw <= 2 && !(VN_ABLATE & 2u)) {
             const int rowi = (xr ? y : x) * PH + z;
             if (pc_.row != rowi) {
-                const uint64_t *prow =
-                    reinterpret_cast<const uint64_t *>(map + (xr ? p.xp_off : p.yp_off)) + (size_t)rowi * nw;
+                uint64_t *pbase = reinterpret_cast<uint64_t *>(map + (xr ? p.xp_off : p.yp_off));
+                const uint64_t *prow = pbase + (size_t)rowi * nw;
+                // VN_ROW_WB: the left row's changed words go back after the new
+                // row's loads are issued (vmcnt retires in issue order)
+                const uint64_t o0 = pc_.w[0], o1 = pc_.w[1];
+                const int orow = pc_.row;
+                const uint32_t od = VN_ROW_WB ? pc_.dirty : 0u;
                 pc_.row = rowi;
                 pc_.w0 = 0;
                 pc_.w[0] = prow[0];
                 pc_.w[1] = nw > 1 ? prow[1] : 0ull;
+                pc_.dirty = 0u;
+                if (VN_ROW_WB && od) {
+                    uint64_t *op = pbase + (size_t)orow * nw;
+                    if (od & 1u) op[0] = o0;
+                    if (od & 2u) op[1] = o1;
+                }
             }
         }
+    }
+}
+
+// VN_ROW_WB: the cached row's changed words to HBM (launch end)
+__device__ __forceinline__ void plane_wb_flush(const Params &p, int8_t *map, PlaneCache &pc_, int q) {
+    if (VN_ROW_WB && q < 2 && pc_.dirty && pc_.row >= 0) {
+        const int nw = q == 0 ? p.nwx : p.nwy;
+        uint64_t *op = reinterpret_cast<uint64_t *>(map + (q == 0 ? p.xp_off : p.yp_off)) + (size_t)pc_.row * nw;
+        if (pc_.dirty & 1u) op[0] = pc_.w[0];
+        if (pc_.dirty & 2u) op[1] = pc_.w[1];
+        pc_.dirty = 0u;
     }
 }
 
@@ -617,12 +647,14 @@ __device__ __forceinline__ void pend_apply(const Params &p, int8_t *map, PlaneCa
             const uint64_t nv = pn0 | pend.pm0;
             if (pofs == 0) pc_.w[0] = nv;
             else pc_.w[1] = nv;
-            if (!(VN_ABLATE & 2097184u)) prow[pend.pw0] = nv;   // 32 | 2097152: diagnostics
+            if (VN_ROW_WB) pc_.dirty |= pofs == 0 ? 1u : 2u;
+            else if (!(VN_ABLATE & 2097184u)) prow[pend.pw0] = nv;   // 32 | 2097152: diagnostics
         }
         if (nwd1) {
             const uint64_t nv = pn1 | pend.pm1;
             if (pofs == 0) pc_.w[1] = nv;
-            if (!(VN_ABLATE & 2097184u)) prow[pend.pw0 + 1] = nv;
+            if (VN_ROW_WB) pc_.dirty |= 2u;
+            else if (!(VN_ABLATE & 2097184u)) prow[pend.pw0 + 1] = nv;
         }
         const int sh = pend.pa - pend.pw0 * 64;   // 0..63
         rel = sh == 0 ? nwd0 : (nwd0 >> sh) | (nwd1 << (64 - sh));
@@ -755,6 +787,7 @@ __device__ __forceinline__ int sense_observe(const Params &p, int8_t *map, uint6
             pc_.row = rowi;
             pc_.w0 = nw <= 2 ? 0 : pw0;
             pc_.w[0] = pc_.w[1] = 0ull;
+            pc_.dirty = 0u;
         } else if (nw > 2 && (pc_.row != rowi || pc_.w0 != pw0)) {
             pc_.row = rowi;
             pc_.w0 = pw0;
@@ -1034,6 +1067,7 @@ __device__ __forceinline__ void group_reset(const Params &p, int8_t *map, uint64
         g.move_mask = 0;
         dirty = 0;
         pc_.row = -1;
+        pc_.dirty = 0u;                   // the ended episode's cached row: its planes are cleared
         if (PC) {                         // the planes were cleared: empty sets
 #pragma unroll
             for (int k = 0; k < 8; ++k) pset_put(ps, 2 * q + (k >> 2), k & 3, pset_zero<RT>());
@@ -1188,6 +1222,7 @@ __global__ __launch_bounds__((PCM == 1 || PCM == 2) ? VN_PC_BLOCK : BLOCK,
     pc_.row = -1;
     pc_.w0 = 0;
     pc_.w[0] = pc_.w[1] = 0ull;
+    pc_.dirty = 0u;
     PendMarks pend;                        // DM: the previous sensing pass's plane marks, not yet applied
     pend.valid = 0;
     RT *ps = psets + (PC ? (threadIdx.x / GROUP) * PsetGeom<RT>::STRIDE : 0);
@@ -1210,7 +1245,10 @@ __global__ __launch_bounds__((PCM == 1 || PCM == 2) ? VN_PC_BLOCK : BLOCK,
         group_reset<PH, PC, RT, SB, DM>(p, map, tile, dirty, pc_, ps, pdirty, need, seed, g, R, tab,
                                         need ? p.obs + (size_t)i * VN_OBS_DIM : nullptr, nullptr, 0, q, st, pend);
         if (need) {
-            if constexpr (DM) pend_apply<PH>(p, map, pc_, pend, q);
+            if constexpr (DM) {
+                pend_apply<PH>(p, map, pc_, pend, q);
+                plane_wb_flush(p, map, pc_, q);
+            }
             tile_flush<PH>(p, map, tile, g, R, dirty, q);
             if (PC) pset_flush<RT, SB>(p, map, ps, g, R, pdirty, q, st);
             if (SB) {
@@ -1532,7 +1570,10 @@ __global__ __launch_bounds__((PCM == 1 || PCM == 2) ? VN_PC_BLOCK : BLOCK,
     }
     }
     if (active) {
-        if constexpr (DM) pend_apply<PH>(p, map, pc_, pend, q);   // the last step's deferred marks
+        if constexpr (DM) {
+            pend_apply<PH>(p, map, pc_, pend, q);   // the last step's deferred marks
+            plane_wb_flush(p, map, pc_, q);
+        }
         if (!(VN_ABLATE & 32768u)) {   // diagnostics: 32768 skips the launch's flush
             tile_flush<PH>(p, map, tile, g, R, dirty, q);
             if (PC) pset_flush<RT, SB>(p, map, ps, g, R, pdirty, q, st);

@@ -498,6 +498,206 @@ __global__ __launch_bounds__(256, 4) void linear_f32_kernel(LinearArgs a, int64_
     }
 }
 
+
+// ---------------------------------------------------------------------------
+// The policy MLP of both branches and the heads in one launch: per step of
+// the collector, after the LSTM (ActorCriticPolicy.forward: mlp_extractor ->
+// action_net / value_net -> distribution.get_actions / log_prob; net_arch
+// pi/vf [256, 256, 128] with Tanh, train/Grid_Train.py:68-80).  Block: 256
+// threads, 32 rows of one branch (blockIdx.y: pi, vf).  The rows' activations
+// stay in LDS from the input through every Linear + Tanh layer to the head,
+// so no latent reaches memory (vn_linear_f32 x 3 + vn_policy_head wrote and
+// re-read 2 x 3 layers of [M][256] f32 per step).
+//   layer l: act [32][K_l] (LDS, pitch 257 floats: one k of 32 rows = 32
+//            distinct banks for the A operand's ds_read_b32) x W_l^T [K_l][N_l]
+//            (k-major in HBM / L2, streamed through LDS in 16-deep chunks with
+//            global_load_lds -- 1 KB per wave instruction, no staging
+//            registers -- double-buffered; the next layer's first chunk is
+//            fetched during this layer's last); wave w owns columns 64w ..
+//            64w + 63 (N_l = 256: two 32x32 accumulators) or 32w .. 32w + 31
+//            (N_l = 128: one tile, even / odd k-steps in two accumulators,
+//            summed in the epilogue); the epilogue writes tanh(acc + b) over
+//            act in place (after a barrier: every wave has read layer l's A).
+//   head:    8 lanes per row (features j = p, p + 8, ...), xor-reduced over
+//            the 8; pi rows: logits, log-sum-exp, the Philox inverse-CDF draw
+//            (argmax when deterministic) and its log-prob, as vn_policy_head;
+//            vf rows: the value.
+// LDS 65 KB: two blocks (8 waves) per CU.
+// ---------------------------------------------------------------------------
+constexpr int MH_R = 32, MH_P = 257, MH_KC = 16, MH_MAXL = 4, MH_MAXA = 8;
+
+struct MlpHeadArgs {
+    const float *x[2];                 // branch inputs [M][ldx] (pi, vf)
+    const float *wt[2][MH_MAXL];       // W_l^T [K_l][N_l], per branch and layer
+    const float *bias[2][MH_MAXL];     // b_l [N_l]
+    int width[MH_MAXL];                // N_l: 128 or 256
+    const float *wa, *ba, *wv, *bv;    // action_net [A][P], [A]; value_net [P], [1]
+    int32_t *actions;
+    float *log_probs, *values;
+    uint64_t seed, t;
+    int64_t gid_base, ldx;
+    int K0, n_layers, A, M, br0, deterministic;
+};
+
+__global__ __launch_bounds__(256, 2) void mlp_head_f32_kernel(MlpHeadArgs a) {
+    __shared__ float act[MH_R * MH_P];
+    __shared__ __attribute__((aligned(16))) float Bs[2][MH_KC * 256];
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const int col = lane & 31, kh = lane >> 5;
+    const int br = a.br0 + (int)blockIdx.y;
+    const int m0 = (int)blockIdx.x * MH_R;
+    // chunk ch of layer l (16 k-rows of W_l^T, contiguous) into LDS buffer st
+    auto issue = [&](int l, int ch, int st) {
+        const int N = a.width[l];
+        const float *src = a.wt[br][l] + (size_t)ch * MH_KC * N;
+        const int n_ins = MH_KC * N / 256;                      // 1-KB wave instructions: 16 or 8
+        for (int i = wv; i < n_ins; i += 4)
+            __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void *)(src + i * 256 + lane * 4),
+                                             (__attribute__((address_space(3))) void *)&Bs[st][i * 256], 16, 0, 0);
+    };
+    issue(0, 0, 0);
+    {   // the input rows (rows past M repeat row M - 1; their outputs are not stored)
+        const float *x = a.x[br];
+        const int q4 = a.K0 / 4;
+        for (int f = tid; f < MH_R * q4; f += 256) {
+            const int r = f / q4, k = 4 * (f - r * q4);
+            const int m = min(m0 + r, a.M - 1);
+            const float4 v = *reinterpret_cast<const float4 *>(x + (size_t)m * a.ldx + k);
+            float *d = act + r * MH_P + k;
+            d[0] = v.x;
+            d[1] = v.y;
+            d[2] = v.z;
+            d[3] = v.w;
+        }
+    }
+    int g = 0;                          // chunks computed so far: chunk g is in buffer g & 1
+    int K = a.K0;
+    for (int l = 0; l < a.n_layers; ++l) {
+        const int N = a.width[l];
+        const int nch = K / MH_KC;
+        const bool wide = N == 256;
+        const int n0 = wide ? 64 * wv : 32 * wv;
+        f32x16_t acc0 = zero16(), acc1 = zero16();
+        for (int ch = 0; ch < nch; ++ch) {
+            // this chunk landed (own loads, then every wave's); every wave is
+            // past chunk g - 1, whose buffer the next issue overwrites
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __syncthreads();
+            if (ch + 1 < nch) issue(l, ch + 1, (g + 1) & 1);
+            else if (l + 1 < a.n_layers) issue(l + 1, 0, (g + 1) & 1);
+            const float *B = Bs[g & 1];
+            const float *Ar = act + col * MH_P + ch * MH_KC + kh;
+            if (wide) {
+                const float *Bc = B + kh * 256 + n0 + col;
+#pragma unroll
+                for (int s = 0; s < MH_KC / 2; ++s) {
+                    const float av = Ar[2 * s];
+                    const float b0 = Bc[2 * s * 256], b1 = Bc[2 * s * 256 + 32];
+                    acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(av, b0, acc0, 0, 0, 0);
+                    acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(av, b1, acc1, 0, 0, 0);
+                }
+            } else {
+                const float *Bc = B + kh * 128 + n0 + col;
+#pragma unroll
+                for (int s = 0; s < MH_KC / 2; s += 2) {
+                    const float a0 = Ar[2 * s], a1 = Ar[2 * s + 2];
+                    const float b0 = Bc[2 * s * 128], b1 = Bc[(2 * s + 2) * 128];
+                    acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b0, acc0, 0, 0, 0);
+                    acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b1, acc1, 0, 0, 0);
+                }
+            }
+            ++g;
+        }
+        __syncthreads();                // every wave has read layer l's input rows
+        // epilogue: register v of a tile = row 8 (v / 4) + 4 kh + v % 4, column col
+        const float *bias = a.bias[br][l];
+        if (wide) {
+            const float bj0 = bias[n0 + col], bj1 = bias[n0 + 32 + col];
+#pragma unroll
+            for (int reg = 0; reg < 16; ++reg) {
+                float *d = act + (8 * (reg >> 2) + 4 * kh + (reg & 3)) * MH_P + n0 + col;
+                d[0] = PF_TANH(acc0[reg] + bj0);
+                d[32] = PF_TANH(acc1[reg] + bj1);
+            }
+        } else {
+            const float bj = bias[n0 + col];
+#pragma unroll
+            for (int reg = 0; reg < 16; ++reg)
+                act[(8 * (reg >> 2) + 4 * kh + (reg & 3)) * MH_P + n0 + col] = PF_TANH((acc0[reg] + acc1[reg]) + bj);
+        }
+        K = N;
+    }
+    __syncthreads();
+    // ---- head: 8 lanes per row ----
+    const int P = K;
+    const int r = tid >> 3, p = tid & 7;
+    const int m = m0 + r;
+    const float *h = act + r * MH_P;
+    if (br == 0) {
+        float lg[MH_MAXA];
+#pragma unroll
+        for (int k = 0; k < MH_MAXA; ++k) lg[k] = 0.0f;
+        for (int j = p; j < P; j += 8) {
+            const float hv = h[j];
+#pragma unroll
+            for (int k = 0; k < MH_MAXA; ++k)
+                if (k < a.A) lg[k] += hv * a.wa[k * P + j];
+        }
+#pragma unroll
+        for (int k = 0; k < MH_MAXA; ++k) {
+            lg[k] += __shfl_xor(lg[k], 1, 8);
+            lg[k] += __shfl_xor(lg[k], 2, 8);
+            lg[k] += __shfl_xor(lg[k], 4, 8);
+        }
+        if (p != 0 || m >= a.M) return;
+        float mx = -INFINITY;
+#pragma unroll
+        for (int k = 0; k < MH_MAXA; ++k) {
+            lg[k] = k < a.A ? lg[k] + a.ba[k] : -INFINITY;
+            mx = fmaxf(mx, lg[k]);
+        }
+        float se = 0.0f;
+#pragma unroll
+        for (int k = 0; k < MH_MAXA; ++k)
+            if (k < a.A) se += expf(lg[k] - mx);
+        const float lse = mx + logf(se);
+        int act_i = a.A - 1;
+        if (a.deterministic) {
+            float best = lg[0];
+            act_i = 0;
+#pragma unroll
+            for (int k = 1; k < MH_MAXA; ++k)
+                if (k < a.A && lg[k] > best) {
+                    best = lg[k];
+                    act_i = k;
+                }
+        } else {
+            const uint32_t w0 = vn_detail::philox_word0(a.seed, (uint64_t)(a.gid_base + m), a.t | (1ull << 63));
+            const float u = (float)(w0 >> 8) * (1.0f / 16777216.0f);
+            float cdf = 0.0f;
+#pragma unroll
+            for (int k = 0; k < MH_MAXA; ++k)
+                if (k < a.A - 1) {
+                    cdf += expf(lg[k] - lse);
+                    if (u < cdf && act_i == a.A - 1) act_i = k;   // the first crossing
+                }
+        }
+        float lp = lg[0];
+#pragma unroll
+        for (int k = 1; k < MH_MAXA; ++k)
+            if (k == act_i) lp = lg[k];
+        a.actions[m] = act_i;
+        a.log_probs[m] = lp - lse;
+    } else {
+        float v = 0.0f;
+        for (int j = p; j < P; j += 8) v += h[j] * a.wv[j];
+        v += __shfl_xor(v, 1, 8);
+        v += __shfl_xor(v, 2, 8);
+        v += __shfl_xor(v, 4, 8);
+        if (p == 0 && m < a.M) a.values[m] = v + a.bv[0];
+    }
+}
+
 }  // namespace
 
 extern "C" {
@@ -564,6 +764,59 @@ int vn_linear_f32(int32_t n_branch, const float *const *x, int64_t ldx, const fl
     else
         hipLaunchKernelGGL((linear_f32_kernel<false>), grid, dim3(256), 0, (hipStream_t)stream, a, ldx, (int)M,
                            (int)K, (int)Nout, ncb);
+    VN_HIP(hipGetLastError());
+    return VN_OK;
+}
+
+int vn_mlp_head_f32(int32_t n_branch, const float *const *x, int64_t ldx, int32_t K0, int32_t n_layers,
+                    const int32_t *widths, const float *const *w_t, const float *const *bias, const float *w_action,
+                    const float *b_action, int32_t n_actions, const float *w_value, const float *b_value,
+                    uint64_t sample_seed, uint64_t t, int64_t agent_id_base, int32_t deterministic, int32_t *actions,
+                    float *log_probs, float *values, int32_t M, void *stream) {
+    if ((n_branch != 1 && n_branch != 2) || !x || !widths || !w_t || !bias || !w_value || !b_value || !values)
+        return fail(VN_ERR_INVALID, "bad arguments");
+    if (n_layers < 1 || n_layers > MH_MAXL) return fail(VN_ERR_INVALID, "n_layers %d outside 1..%d", n_layers, MH_MAXL);
+    if (M < 1 || K0 < MH_KC || K0 > 256 || (K0 % MH_KC) || ldx < K0 || (ldx & 3))
+        return fail(VN_ERR_INVALID, "bad sizes M=%d K0=%d ldx=%lld (K0 %% 16, <= 256; ldx %% 4)", M, K0,
+                    (long long)ldx);
+    if (n_branch == 2 && (!w_action || !b_action || !actions || !log_probs || n_actions < 1 || n_actions > MH_MAXA))
+        return fail(VN_ERR_INVALID, "the pi branch needs the action head (1 <= n_actions <= %d) and outputs", MH_MAXA);
+    MlpHeadArgs a{};
+    a.ldx = ldx;
+    a.K0 = K0;
+    a.n_layers = n_layers;
+    for (int l = 0; l < n_layers; ++l) {
+        if (widths[l] != 128 && widths[l] != 256) return fail(VN_ERR_INVALID, "layer %d width %d: 128 or 256", l, widths[l]);
+        a.width[l] = widths[l];
+    }
+    const int br0 = n_branch == 2 ? 0 : 1;
+    for (int b = 0; b < n_branch; ++b) {
+        if (!x[b] || (reinterpret_cast<uintptr_t>(x[b]) & 15)) return fail(VN_ERR_INVALID, "x[%d]: NULL or not 16-B aligned", b);
+        a.x[br0 + b] = x[b];
+        for (int l = 0; l < n_layers; ++l) {
+            const float *w = w_t[b * n_layers + l];
+            if (!w || (reinterpret_cast<uintptr_t>(w) & 15) || !bias[b * n_layers + l])
+                return fail(VN_ERR_INVALID, "branch %d layer %d: NULL or unaligned weights", b, l);
+            a.wt[br0 + b][l] = w;
+            a.bias[br0 + b][l] = bias[b * n_layers + l];
+        }
+    }
+    a.wa = w_action;
+    a.ba = b_action;
+    a.wv = w_value;
+    a.bv = b_value;
+    a.actions = actions;
+    a.log_probs = log_probs;
+    a.values = values;
+    a.seed = sample_seed;
+    a.t = t;
+    a.gid_base = agent_id_base;
+    a.A = n_branch == 2 ? n_actions : 0;
+    a.M = M;
+    a.br0 = br0;
+    a.deterministic = deterministic;
+    const dim3 grid((unsigned)((M + MH_R - 1) / MH_R), (unsigned)n_branch);
+    hipLaunchKernelGGL(mlp_head_f32_kernel, grid, dim3(256), 0, (hipStream_t)stream, a);
     VN_HIP(hipGetLastError());
     return VN_OK;
 }

@@ -82,6 +82,8 @@ _SIGS = {
     "vn_lstm_fused_f32": (C.c_int, [P, C.c_int32, P, P, C.c_int32, P, P, P, P, P, C.c_int32, C.c_int32, C.c_int32,
                                     P]),
     "vn_linear_f32": (C.c_int, [C.c_int32, P, C.c_int64, P, P, P, C.c_int32, C.c_int32, C.c_int32, C.c_int32, P]),
+    "vn_mlp_head_f32": (C.c_int, [C.c_int32, P, C.c_int64, C.c_int32, C.c_int32, P, P, P, P, P, C.c_int32, P, P,
+                                  C.c_uint64, C.c_uint64, C.c_int64, C.c_int32, P, P, P, C.c_int32, P]),
     "vn_collect_compact": (C.c_int, [P, P, C.c_int32, P, P, P]),
     "vn_collect_bootstrap": (C.c_int, [P, P, C.c_int32, C.c_double, P, P]),
     "vn_collect_stash": (C.c_int, [P, P, P, P, C.c_int32, C.c_int32, P, C.c_int32, P, C.c_int32, P, C.c_int32, P, P,

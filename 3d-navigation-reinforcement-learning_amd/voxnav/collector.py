@@ -43,6 +43,7 @@ independent of how agents are sharded over GPUs.
 from __future__ import annotations
 
 import ctypes as C
+import os
 import numpy as np
 from dataclasses import dataclass
 from typing import Optional
@@ -143,6 +144,17 @@ class _Weights:
         self.P = self.wa.shape[1]
         if self.wv.shape[0] != self.P:
             raise NotImplementedError("pi and vf latents must have the same width")
+        # the MLPs and heads in one launch (vn_mlp_head_f32): layer widths 128 / 256,
+        # at most 4 layers, inputs % 16 <= 256, at most 8 actions; W^T per layer.
+        # VOXNAV_MLP_HEAD=0: the per-layer kernels + vn_policy_head (A/B knob)
+        k0 = self.pi[0][0].shape[1] if self.pi else 0
+        self.mlp_head = (self.f32mlp and 1 <= len(self.pi) <= 4 and all(w.shape[0] in (128, 256) for w, _ in self.pi)
+                         and k0 % 16 == 0 and 16 <= k0 <= 256 and self.P == widths[-1] and self.A <= 8
+                         and os.environ.get("VOXNAV_MLP_HEAD", "1") != "0")
+        if self.mlp_head:
+            self.widths = widths
+            self.mh_wt = [w.t().contiguous() for w, _ in self.pi] + [w.t().contiguous() for w, _ in self.vf]
+            self.mh_b = [b for _, b in self.pi] + [b for _, b in self.vf]
 
 
 def pack_lstm_f32(w_ih, w_hh) -> torch.Tensor:
@@ -256,7 +268,7 @@ class RolloutCollector:
             self._stash_c = z(cap, self.w.H)
         # SB3 Monitor on every worker (train/Grid_Train.py:125): it sums the env's
         # f64 rewards, so the env step also writes them (voxnav.monitor)
-        if self.w.f32mlp:
+        if self.w.f32mlp and not self.w.mlp_head:
             rows = max(N, self._stash_cap)
             self._lat32 = [z(2, rows, wt.shape[0]) for wt, _ in self.w.vf]
         if self.recurrent and self.w.fused32:
@@ -346,6 +358,26 @@ class RolloutCollector:
             xs = ys
         return (xs[0] if x_pi is not None else None), xs[-1]
 
+    def _mlp_head32(self, x_pi, x_vf, M, t, actions, values, log_probs):
+        """Both MLP branches and the heads in one launch (vn_mlp_head_f32); the
+        value branch alone when x_pi is None (values only)."""
+        w = self.w
+        xs = [x_pi, x_vf] if x_pi is not None else [x_vf]
+        nb, nl = len(xs), len(w.widths)
+        if nb == 2 and x_pi.stride(0) != x_vf.stride(0):
+            raise ValueError("pi and vf inputs must share a row stride")
+        wt = w.mh_wt if nb == 2 else w.mh_wt[nl:]
+        bs = w.mh_b if nb == 2 else w.mh_b[nl:]
+        arr = lambda ts: (C.c_void_p * len(ts))(*[x.data_ptr() for x in ts])  # noqa: E731
+        pi = nb == 2
+        _native.check(self.lib.vn_mlp_head_f32(nb, arr(xs), xs[0].stride(0), xs[0].shape[1], nl,
+                                               (C.c_int32 * nl)(*w.widths), arr(wt), arr(bs),
+                                               _p(w.wa) if pi else None, _p(w.ba) if pi else None, w.A if pi else 0,
+                                               _p(w.wv), _p(w.bv), self.sample_seed if pi else 0, t if pi else 0,
+                                               self.env.agent_id_base if pi else 0,
+                                               int(self.deterministic) if pi else 0, _p(actions), _p(log_probs),
+                                               _p(values), M, self._stream()), "vn_mlp_head_f32")
+
     def hidden_state(self):
         """(h, c) f32 [2, N, H] of the (actor, critic) LSTMs after the last step
         (h from its bf16 copy on the fused bf16 path)."""
@@ -383,6 +415,10 @@ class RolloutCollector:
                     self._hs[t + 1].copy_(h_out)
                     self._cs[t + 1].copy_(self.c)
                 self.h, self._h_alt = h_out, self.h
+            if w.mlp_head:
+                self._mlp_head32(h_out[0], h_out[1], N, self.t_global, self.actions[t], self.values[t],
+                                 self.log_probs[t])
+                return
             lat_pi, lat_vf = self._mlp32(h_out[0], h_out[1], N)
             self._head(lat_pi, lat_vf, N, self.t_global, self.actions[t], self.values[t], self.log_probs[t])
             return
@@ -415,6 +451,9 @@ class RolloutCollector:
             x_pi, x_vf = (self.h_bf[0], self.h_bf[1]) if self.bf16 else (self.h[0], self.h[1])
         else:
             x_pi = x_vf = x
+        if w.mlp_head and x_pi.stride(0) == x_vf.stride(0) and x_pi.is_contiguous() and x_vf.is_contiguous():
+            self._mlp_head32(x_pi, x_vf, N, self.t_global, self.actions[t], self.values[t], self.log_probs[t])
+            return
         if w.f32mlp:
             lat_pi, lat_vf = self._mlp32(x_pi, x_vf, N)
         else:
@@ -434,10 +473,16 @@ class RolloutCollector:
         if self.recurrent and w.fused32:
             h_out = self._crit_h[:M]
             self._lstm32(obs.contiguous(), h.contiguous(), c, None, c, h_out, 1, M, 1)
-            self._head(None, self._mlp32(None, h_out, M)[1], M, 0, None, out, None)
+            if w.mlp_head:
+                self._mlp_head32(None, h_out, M, 0, None, out, None)
+            else:
+                self._head(None, self._mlp32(None, h_out, M)[1], M, 0, None, out, None)
             return
         if not self.recurrent and w.f32mlp:
-            self._head(None, self._mlp32(None, obs.contiguous(), M)[1], M, 0, None, out, None)
+            if w.mlp_head:
+                self._mlp_head32(None, obs.contiguous(), M, 0, None, out, None)
+            else:
+                self._head(None, self._mlp32(None, obs.contiguous(), M)[1], M, 0, None, out, None)
             return
         x = obs if not self.bf16 else obs.to(self.cdt)
         if self.recurrent:

@@ -310,6 +310,33 @@ int vn_policy_head_bf16(const uint16_t *latent_pi, const uint16_t *latent_vf, in
                         int32_t deterministic, int32_t *actions, float *values, float *log_probs, void *stream);
 
 /*
+ * The collector's whole policy after the LSTM in ONE launch: the pi and vf
+ * MLPs (MlpExtractor, Linear + Tanh per layer; net_arch [256, 256, 128],
+ * train/Grid_Train.py:68-80) and the heads + Categorical draw of
+ * vn_policy_head (ActorCriticPolicy.forward / predict_values), the
+ * activations kept on chip (no latent reaches memory).  Replaces
+ * vn_linear_f32 x n_layers + vn_policy_head of one collector step.
+ *   n_branch 2: x[0] the pi input, x[1] the vf input; 1: x[0] the vf input
+ *               (value only: the truncation bootstrap, last values)
+ *   x[b]        f32 [M][K0] rows with row stride ldx (% 4), 16-byte aligned;
+ *               K0 % 16 == 0, K0 <= 256
+ *   widths      n_layers (1..4) layer widths, each 128 or 256; the last is P
+ *   w_t[b * n_layers + l]  f32 W_l^T [K_l][N_l] (k-major, 16-byte aligned),
+ *               K_0 = K0, K_l = widths[l - 1];  bias[b * n_layers + l] [N_l]
+ *   w_action [n_actions][P], b_action (pi branch; n_actions <= 8),
+ *   w_value [P], b_value [1]
+ *   actions / log_probs (pi branch) and values: [M], the draw of
+ *   vn_policy_head (Philox4x32-10 key sample_seed, counter (agent_id_base + m,
+ *   t | 2^63); argmax when deterministic).
+ * Host arrays: x (n_branch), widths (n_layers), w_t and bias (n_branch x n_layers).
+ */
+int vn_mlp_head_f32(int32_t n_branch, const float *const *x, int64_t ldx, int32_t K0, int32_t n_layers,
+                    const int32_t *widths, const float *const *w_t, const float *const *bias, const float *w_action,
+                    const float *b_action, int32_t n_actions, const float *w_value, const float *b_value,
+                    uint64_t sample_seed, uint64_t t, int64_t agent_id_base, int32_t deterministic, int32_t *actions,
+                    float *log_probs, float *values, int32_t M, void *stream);
+
+/*
  * Ordered indices of the agents whose step was a time-limit truncation
  * (SB3 VecEnv: done and info["TimeLimit.truncated"] = truncated and not
  * terminated) -> boot_idx (device i32 [N]) and boot_count (device i32 [1]).

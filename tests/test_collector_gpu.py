@@ -592,3 +592,105 @@ def test_linear_f32_bench_shape(voxnav, M, K, nout):
                 assert not bool(bad.any()), f"branch {i}: {int(bad.sum())} out of tolerance"
             else:
                 assert torch.equal(ty[i], ref.float()), f"branch {i}: identity form not exact"
+
+
+def _philox_u(seed, gids, t):
+    """The sampler's uniform (collector_oracle.sample_uniform) for many agents at once (numpy)."""
+    m = np.uint64(0xFFFFFFFF)
+    gids = np.asarray(gids, np.uint64)
+    hi = (int(t) | (1 << 63)) & ((1 << 64) - 1)
+    c0, c1 = gids & m, gids >> np.uint64(32)
+    c2 = np.full_like(gids, hi & 0xFFFFFFFF)
+    c3 = np.full_like(gids, hi >> 32)
+    k0, k1 = np.uint64(seed & 0xFFFFFFFF), np.uint64((seed >> 32) & 0xFFFFFFFF)
+    for r in range(10):
+        if r:
+            k0 = (k0 + np.uint64(0x9E3779B9)) & m
+            k1 = (k1 + np.uint64(0xBB67AE85)) & m
+        p0 = np.uint64(0xD2511F53) * c0
+        p1 = np.uint64(0xCD9E8D57) * c2
+        c0, c1, c2, c3 = (p1 >> np.uint64(32)) ^ c1 ^ k0, p1 & m, (p0 >> np.uint64(32)) ^ c3 ^ k1, p0 & m
+    return (c0 >> np.uint64(8)).astype(np.float64) / 16777216.0
+
+
+def _mlp_head_ref(xs, layers, wa, ba, wv, bv):
+    """float64 restatement of the pi / vf MLPs (Linear + Tanh) and the heads."""
+    d = torch.float64
+    hs = []
+    for x, ls in zip(xs, layers):
+        h = x.to(d)
+        for w, b in ls:
+            h = torch.tanh(h @ w.to(d).T + b.to(d))
+        hs.append(h)
+    logits = hs[0] @ wa.to(d).T + ba.to(d) if wa is not None else None
+    value = hs[-1] @ wv.to(d) + bv.to(d)
+    return logits, value
+
+
+@pytest.mark.parametrize("M,K0,widths,nb", [(65536 + 33, 256, (256, 256, 128), 2), (77, 80, (256, 256, 128), 2),
+                                            (300, 80, (128, 256), 2), (1000, 256, (256, 256, 128), 1),
+                                            (65536, 80, (256, 256, 128), 2)])
+def test_mlp_head_f32_matches_float64(voxnav, M, K0, widths, nb):
+    """vn_mlp_head_f32 (both MLP branches + heads in one launch, activations in
+    LDS) against float64: values and log-probs within 2e-5 + 2e-5 |x| (the
+    hardware exp / rcp of the Tanh), the Philox draw equal to the draw the
+    float64 probabilities give except within 1e-5 of a CDF boundary, argmax in
+    deterministic mode; value-only launches (n_branch 1); ragged M, the
+    collector bench's 65,536 rows, K0 = 80 (PPO-MLP) and 256 (after the LSTM),
+    a 128-wide first layer."""
+    import ctypes as C
+    lib = voxnav.load_library()
+    dev = "cuda:0"
+    g = torch.Generator(device=dev).manual_seed(M + K0 + nb)
+    rn = lambda *s, sc=1.0: (torch.randn(s, generator=g, device=dev) * sc).contiguous()  # noqa: E731
+    xs = [rn(M, K0), rn(M, K0)][:nb] if nb == 2 else [rn(M, K0)]
+    layers = []
+    for _ in range(nb):
+        ls, k = [], K0
+        for n in widths:
+            ls.append((rn(n, k, sc=1.0 / k ** 0.5), rn(n, sc=0.1)))
+            k = n
+        layers.append(ls)
+    P, A = widths[-1], 6
+    wa, ba = rn(A, P, sc=3.0 / P ** 0.5), rn(A, sc=0.5)
+    wv, bv = rn(P, sc=1.0 / P ** 0.5), rn(1)
+    wt = [w.t().contiguous() for ls in layers for w, _ in ls]
+    bs = [b for ls in layers for _, b in ls]
+    arr = lambda ts: (C.c_void_p * len(ts))(*[t.data_ptr() for t in ts])  # noqa: E731
+    p = lambda t: None if t is None else C.c_void_p(t.data_ptr())  # noqa: E731
+    nl = len(widths)
+    ref_lg, ref_v = _mlp_head_ref(xs, layers, wa if nb == 2 else None, ba, wv, bv)
+    for det in (0, 1):
+        acts = torch.full((M,), -1, dtype=torch.int32, device=dev)
+        lps = torch.full((M,), float("nan"), device=dev)
+        vals = torch.full((M,), float("nan"), device=dev)
+        assert lib.vn_mlp_head_f32(nb, arr(xs), K0, K0, nl, (C.c_int32 * nl)(*widths), arr(wt), arr(bs),
+                                   p(wa) if nb == 2 else None, p(ba) if nb == 2 else None, A if nb == 2 else 0, p(wv),
+                                   p(bv), 1234, 77, 1000, det, p(acts) if nb == 2 else None,
+                                   p(lps) if nb == 2 else None, p(vals), M, None) == 0
+        torch.cuda.synchronize()
+        bad = (vals.double() - ref_v).abs() > 2e-5 + 2e-5 * ref_v.abs()
+        assert not bool(bad.any()), f"values: {int(bad.sum())} out of tolerance"
+        if nb == 1:
+            assert int((acts == -1).sum()) == M and bool(torch.isnan(lps).all())     # pi outputs untouched
+            break
+        lsm = torch.log_softmax(ref_lg, -1)
+        if det:
+            srt = ref_lg.sort(-1, descending=True).values
+            clear = (srt[:, 0] - srt[:, 1]) > 1e-5
+            assert torch.equal(acts.long()[clear], ref_lg.argmax(-1)[clear])
+        else:
+            # the draw the float64 probabilities give for the same uniform
+            from oracle.collector_oracle import sample_uniform
+            un = _philox_u(1234, 1000 + np.arange(M, dtype=np.uint64), 77)
+            assert all(un[i] == sample_uniform(1234, 1000 + i, 77) for i in (0, 1, M - 1))
+            u = torch.as_tensor(un, dtype=torch.float64, device=dev)
+            cdf = lsm.exp().cumsum(-1)
+            want = (u[:, None] < cdf[:, :A - 1]).to(torch.int64)
+            want = torch.where(want.any(-1), want.argmax(-1), torch.full_like(want[:, 0], A - 1))
+            margin = (cdf[:, :A - 1] - u[:, None]).abs().min(-1).values
+            diff = acts.long() != want
+            assert bool((margin[diff] < 1e-5).all()), f"{int(diff.sum())} draws differ away from a cdf boundary"
+        lp_ref = lsm.gather(1, acts.long()[:, None])[:, 0]
+        bad = (lps.double() - lp_ref).abs() > 2e-5 + 2e-5 * lp_ref.abs()
+        assert not bool(bad.any()), f"log_probs: {int(bad.sum())} out of tolerance"
