@@ -504,31 +504,34 @@ __global__ __launch_bounds__(256, 4) void linear_f32_kernel(LinearArgs a, int64_
 // the collector, after the LSTM (ActorCriticPolicy.forward: mlp_extractor ->
 // action_net / value_net -> distribution.get_actions / log_prob; net_arch
 // pi/vf [256, 256, 128] with Tanh, train/Grid_Train.py:68-80).  Block: 256
-// threads, 32 rows of one branch (blockIdx.y: pi, vf).  The rows' activations
-// stay in LDS from the input through every Linear + Tanh layer to the head,
-// so no latent reaches memory (vn_linear_f32 x 3 + vn_policy_head wrote and
-// re-read 2 x 3 layers of [M][256] f32 per step).
-//   layer l: act [32][K_l] (LDS, pitch 257 floats: one k of 32 rows = 32
-//            distinct banks for the A operand's ds_read_b32) x W_l^T [K_l][N_l]
-//            (k-major in HBM / L2, streamed through LDS in 16-deep chunks with
-//            global_load_lds -- 1 KB per wave instruction, no staging
-//            registers -- double-buffered; the next layer's first chunk is
-//            fetched during this layer's last); wave w owns columns 64w ..
-//            64w + 63 (N_l = 256: two 32x32 accumulators) or 32w .. 32w + 31
-//            (N_l = 128: one tile, even / odd k-steps in two accumulators,
-//            summed in the epilogue); the epilogue writes tanh(acc + b) over
-//            act in place (after a barrier: every wave has read layer l's A).
-//   head:    8 lanes per row (features j = p, p + 8, ...), xor-reduced over
-//            the 8; pi rows: logits, log-sum-exp, the Philox inverse-CDF draw
-//            (argmax when deterministic) and its log-prob, as vn_policy_head;
-//            vf rows: the value.
-// LDS 65 KB: two blocks (8 waves) per CU.
+// threads, 32 rows of one branch (blockIdx.y: pi, vf).  The rows'
+// activations stay in LDS from the input through every Linear + Tanh layer to
+// the head, so no latent reaches memory (vn_linear_f32 x 3 + vn_policy_head
+// wrote and re-read [M][256] f32 per layer and branch).
+//   A operand: act [32][260] in LDS; within a group of 8 k the two lane halves
+//     take k 0..3 and 4..7 over the 4 k-steps (a reordering of the dot
+//     product's terms, the same for both operands), so one ds_read_b128 of a
+//     lane's row carries its 4 k-steps (pitch 260: rows 0..15 of a 16-lane
+//     group land on 16 distinct 16-B bank slots).
+//   B operand: the weights packed per lane on the host (vn_mlp_head_f32
+//     layout: [N/32][K/8][64 lanes][4]): each wave streams its own columns
+//     through its own LDS ring (global_load_lds, MH_D k-groups ahead, one
+//     ds_read_b128 per lane per 4 k-steps and 32-column tile) -- no register
+//     staging and no barrier inside a layer.
+//   wave w owns columns 64w .. 64w + 63 (N = 256: two 32x32 tiles) or 32w ..
+//   32w + 31 (N = 128: one tile, even / odd k-groups in two accumulators,
+//   summed in the epilogue); the epilogue writes tanh(acc + b) over act.
+//   head: 8 lanes per row (features j = p, p + 8, ...) with the head weights
+//     in LDS, xor-reduced over the 8; pi rows: logits, log-sum-exp, the Philox
+//     inverse-CDF draw (argmax when deterministic) and its log-prob, as
+//     vn_policy_head; vf rows: the value.
+// LDS 49 KB: three blocks per CU.
 // ---------------------------------------------------------------------------
-constexpr int MH_R = 32, MH_P = 257, MH_KC = 16, MH_MAXL = 4, MH_MAXA = 8;
+constexpr int MH_R = 32, MH_P = 260, MH_MAXL = 4, MH_MAXA = 8, MH_MAXP = 256, MH_D = 2;
 
 struct MlpHeadArgs {
     const float *x[2];                 // branch inputs [M][ldx] (pi, vf)
-    const float *wt[2][MH_MAXL];       // W_l^T [K_l][N_l], per branch and layer
+    const float *wp[2][MH_MAXL];       // packed weights per branch and layer
     const float *bias[2][MH_MAXL];     // b_l [N_l]
     int width[MH_MAXL];                // N_l: 128 or 256
     const float *wa, *ba, *wv, *bv;    // action_net [A][P], [A]; value_net [P], [1]
@@ -539,78 +542,127 @@ struct MlpHeadArgs {
     int K0, n_layers, A, M, br0, deterministic;
 };
 
-__global__ __launch_bounds__(256, 2) void mlp_head_f32_kernel(MlpHeadArgs a) {
-    __shared__ float act[MH_R * MH_P];
-    __shared__ __attribute__((aligned(16))) float Bs[2][MH_KC * 256];
+// One layer's K loop of a wave: A from the act rows (one ds_read_b128 per
+// k-group of 8), B from the per-lane packed weights through a ring of MH_D
+// k-groups in registers (refilled MH_D ahead; past the end the slot reloads a
+// k-group already read, so the loop has no branch and the waits are counted).
+// WIDE: two column tiles; else one tile, even / odd k-groups into acc0 / acc1.
+typedef float mh_f4 __attribute__((ext_vector_type(4)));
+
+// One layer's K loop of a wave: A from the act rows (one ds_read_b128 per
+// k-group of 8), B from the per-lane packed weights through the wave's own
+// LDS ring of MH_D k-groups (global_load_lds, 16 B per lane; each wave reads
+// only what it loaded, so no barrier -- its own vmcnt says the group landed).
+// Past the end a slot reloads a k-group already read (no branch; drained at
+// the end).  WIDE: two column tiles; else one tile, even / odd k-groups into
+// acc0 / acc1.
+template <bool WIDE>
+__device__ __forceinline__ void mh_layer(const float *Ar, const float4 *B0, const float4 *B1, int KG, float *ring0,
+                                         float *ring1, int lane, f32x16_t &acc0, f32x16_t &acc1) {
+    static_assert(MH_D == 2, "two ring slots, each its own LDS object (the waits then see they do not alias)");
+    constexpr int PER = WIDE ? 2 : 1;                      // 1-KB loads per k-group
+    auto issue = [&](int kg, int slot) {
+        float *ring = slot == 0 ? ring0 : ring1;
+        __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void *)(B0 + kg * 64),
+                                         (__attribute__((address_space(3))) void *)ring, 16, 0, 0);
+        if (WIDE)
+            __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void *)(B1 + kg * 64),
+                                             (__attribute__((address_space(3))) void *)(ring + 256), 16, 0, 0);
+    };
+#pragma unroll
+    for (int j = 0; j < MH_D; ++j) issue(j, j);
+    for (int kg0 = 0; kg0 < KG; kg0 += MH_D) {
+        const int nbase = kg0 + MH_D < KG ? kg0 + MH_D : kg0;
+#pragma unroll
+        for (int j = 0; j < MH_D; ++j) {
+            // k-group kg0 + j landed: the later groups' loads may still be in flight
+            asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PER * (MH_D - 1)) : "memory");
+            const float4 av = *reinterpret_cast<const float4 *>(Ar + 8 * (kg0 + j));
+            // the ring reads in asm: the compiler would otherwise wait for every
+            // LDS-DMA load in flight (vmcnt(0)) before them
+            const float *ring = j == 0 ? ring0 : ring1;
+            mh_f4 b0v, b1v;
+            asm volatile("ds_read_b128 %0, %1" : "=v"(b0v) : "v"((uint32_t)(uintptr_t)(ring + lane * 4)) : "memory");
+            if (WIDE) {
+                asm volatile("ds_read_b128 %0, %1 offset:1024" : "=v"(b1v) : "v"((uint32_t)(uintptr_t)(ring + lane * 4))
+                             : "memory");
+                // the slot's reads are done before the next load overwrites it
+                asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(b0v), "+v"(b1v)::"memory");
+            } else {
+                asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(b0v)::"memory");
+                b1v = b0v;
+            }
+            const float4 b0 = make_float4(b0v[0], b0v[1], b0v[2], b0v[3]);
+            const float4 b1 = make_float4(b1v[0], b1v[1], b1v[2], b1v[3]);
+            issue(nbase + j, j);
+            if (WIDE) {
+                acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(av.x, b0.x, acc0, 0, 0, 0);
+                acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(av.x, b1.x, acc1, 0, 0, 0);
+                acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(av.y, b0.y, acc0, 0, 0, 0);
+                acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(av.y, b1.y, acc1, 0, 0, 0);
+                acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(av.z, b0.z, acc0, 0, 0, 0);
+                acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(av.z, b1.z, acc1, 0, 0, 0);
+                acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(av.w, b0.w, acc0, 0, 0, 0);
+                acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(av.w, b1.w, acc1, 0, 0, 0);
+            } else if ((j & 1) == 0) {
+                acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(av.x, b0.x, acc0, 0, 0, 0);
+                acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(av.y, b0.y, acc0, 0, 0, 0);
+                acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(av.z, b0.z, acc0, 0, 0, 0);
+                acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(av.w, b0.w, acc0, 0, 0, 0);
+            } else {
+                acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(av.x, b0.x, acc1, 0, 0, 0);
+                acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(av.y, b0.y, acc1, 0, 0, 0);
+                acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(av.z, b0.z, acc1, 0, 0, 0);
+                acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(av.w, b0.w, acc1, 0, 0, 0);
+            }
+        }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the trailing reloads landed: the ring is free
+}
+
+__global__ __launch_bounds__(256, 3) void mlp_head_f32_kernel(MlpHeadArgs a) {
+    __shared__ __attribute__((aligned(16))) float act[MH_R * MH_P];
+    // per wave the B ring (2 slots, each k-group x 2 tiles x 1 KB); after the
+    // last layer the head's weights (action weights in slot 0, value weights in 1)
+    __shared__ __attribute__((aligned(16))) float ring0s[4 * 2 * 256];
+    __shared__ __attribute__((aligned(16))) float ring1s[4 * 2 * 256];
+    static_assert(4 * 2 * 256 >= MH_MAXA * MH_MAXP && 4 * 2 * 256 >= MH_MAXP, "head weights fit the ring");
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const int col = lane & 31, kh = lane >> 5;
     const int br = a.br0 + (int)blockIdx.y;
     const int m0 = (int)blockIdx.x * MH_R;
-    // chunk ch of layer l (16 k-rows of W_l^T, contiguous) into LDS buffer st
-    auto issue = [&](int l, int ch, int st) {
-        const int N = a.width[l];
-        const float *src = a.wt[br][l] + (size_t)ch * MH_KC * N;
-        const int n_ins = MH_KC * N / 256;                      // 1-KB wave instructions: 16 or 8
-        for (int i = wv; i < n_ins; i += 4)
-            __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void *)(src + i * 256 + lane * 4),
-                                             (__attribute__((address_space(3))) void *)&Bs[st][i * 256], 16, 0, 0);
-    };
-    issue(0, 0, 0);
+    const int P = a.width[a.n_layers - 1];
     {   // the input rows (rows past M repeat row M - 1; their outputs are not stored)
         const float *x = a.x[br];
         const int q4 = a.K0 / 4;
         for (int f = tid; f < MH_R * q4; f += 256) {
             const int r = f / q4, k = 4 * (f - r * q4);
             const int m = min(m0 + r, a.M - 1);
-            const float4 v = *reinterpret_cast<const float4 *>(x + (size_t)m * a.ldx + k);
-            float *d = act + r * MH_P + k;
-            d[0] = v.x;
-            d[1] = v.y;
-            d[2] = v.z;
-            d[3] = v.w;
+            *reinterpret_cast<float4 *>(act + r * MH_P + k) = *reinterpret_cast<const float4 *>(x + (size_t)m * a.ldx + k);
+        }
+        const int qp = ((a.K0 + 31) / 32 * 32) / 4;          // zero columns up to the padded K
+        for (int f = tid; f < MH_R * (qp - q4); f += 256) {
+            const int r = f / (qp - q4), k = 4 * (q4 + f - r * (qp - q4));
+            *reinterpret_cast<float4 *>(act + r * MH_P + k) = make_float4(0.f, 0.f, 0.f, 0.f);
         }
     }
-    int g = 0;                          // chunks computed so far: chunk g is in buffer g & 1
-    int K = a.K0;
+    __syncthreads();
+    int K = (a.K0 + 31) / 32 * 32;      // layer 0's K padded to whole prefetch rounds (zero rows / weights)
     for (int l = 0; l < a.n_layers; ++l) {
         const int N = a.width[l];
-        const int nch = K / MH_KC;
         const bool wide = N == 256;
-        const int n0 = wide ? 64 * wv : 32 * wv;
+        const int KG = K / 8;
+        const int cb0 = wide ? 2 * wv : wv;                     // this wave's first 32-column block
+        const float4 *B0 = reinterpret_cast<const float4 *>(a.wp[br][l]) + (size_t)cb0 * KG * 64 + lane;
+        const float *Ar = act + col * MH_P + 4 * kh;
         f32x16_t acc0 = zero16(), acc1 = zero16();
-        for (int ch = 0; ch < nch; ++ch) {
-            // this chunk landed (own loads, then every wave's); every wave is
-            // past chunk g - 1, whose buffer the next issue overwrites
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            __syncthreads();
-            if (ch + 1 < nch) issue(l, ch + 1, (g + 1) & 1);
-            else if (l + 1 < a.n_layers) issue(l + 1, 0, (g + 1) & 1);
-            const float *B = Bs[g & 1];
-            const float *Ar = act + col * MH_P + ch * MH_KC + kh;
-            if (wide) {
-                const float *Bc = B + kh * 256 + n0 + col;
-#pragma unroll
-                for (int s = 0; s < MH_KC / 2; ++s) {
-                    const float av = Ar[2 * s];
-                    const float b0 = Bc[2 * s * 256], b1 = Bc[2 * s * 256 + 32];
-                    acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(av, b0, acc0, 0, 0, 0);
-                    acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(av, b1, acc1, 0, 0, 0);
-                }
-            } else {
-                const float *Bc = B + kh * 128 + n0 + col;
-#pragma unroll
-                for (int s = 0; s < MH_KC / 2; s += 2) {
-                    const float a0 = Ar[2 * s], a1 = Ar[2 * s + 2];
-                    const float b0 = Bc[2 * s * 128], b1 = Bc[(2 * s + 2) * 128];
-                    acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b0, acc0, 0, 0, 0);
-                    acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b1, acc1, 0, 0, 0);
-                }
-            }
-            ++g;
-        }
+        float *r0 = ring0s + wv * 512, *r1 = ring1s + wv * 512;
+        if (wide) mh_layer<true>(Ar, B0, B0 + (size_t)KG * 64, KG, r0, r1, lane, acc0, acc1);
+        else mh_layer<false>(Ar, B0, B0, KG, r0, r1, lane, acc0, acc1);
         __syncthreads();                // every wave has read layer l's input rows
         // epilogue: register v of a tile = row 8 (v / 4) + 4 kh + v % 4, column col
         const float *bias = a.bias[br][l];
+        const int n0 = 32 * cb0;
         if (wide) {
             const float bj0 = bias[n0 + col], bj1 = bias[n0 + 32 + col];
 #pragma unroll
@@ -625,11 +677,16 @@ __global__ __launch_bounds__(256, 2) void mlp_head_f32_kernel(MlpHeadArgs a) {
             for (int reg = 0; reg < 16; ++reg)
                 act[(8 * (reg >> 2) + 4 * kh + (reg & 3)) * MH_P + n0 + col] = PF_TANH((acc0[reg] + acc1[reg]) + bj);
         }
+        __syncthreads();
         K = N;
     }
+    // ---- head: the weights into the (drained) ring space, then 8 lanes per row ----
+    float *hwa = ring0s, *hwv = ring1s;
+    if (br == 0)
+        for (int f = tid; f < a.A * P; f += 256) hwa[f] = a.wa[f];
+    else
+        for (int f = tid; f < P; f += 256) hwv[f] = a.wv[f];
     __syncthreads();
-    // ---- head: 8 lanes per row ----
-    const int P = K;
     const int r = tid >> 3, p = tid & 7;
     const int m = m0 + r;
     const float *h = act + r * MH_P;
@@ -641,7 +698,7 @@ __global__ __launch_bounds__(256, 2) void mlp_head_f32_kernel(MlpHeadArgs a) {
             const float hv = h[j];
 #pragma unroll
             for (int k = 0; k < MH_MAXA; ++k)
-                if (k < a.A) lg[k] += hv * a.wa[k * P + j];
+                if (k < a.A) lg[k] += hv * hwa[k * P + j];
         }
 #pragma unroll
         for (int k = 0; k < MH_MAXA; ++k) {
@@ -690,7 +747,7 @@ __global__ __launch_bounds__(256, 2) void mlp_head_f32_kernel(MlpHeadArgs a) {
         a.log_probs[m] = lp - lse;
     } else {
         float v = 0.0f;
-        for (int j = p; j < P; j += 8) v += h[j] * a.wv[j];
+        for (int j = p; j < P; j += 8) v += h[j] * hwv[j];
         v += __shfl_xor(v, 1, 8);
         v += __shfl_xor(v, 2, 8);
         v += __shfl_xor(v, 4, 8);
@@ -776,7 +833,7 @@ int vn_mlp_head_f32(int32_t n_branch, const float *const *x, int64_t ldx, int32_
     if ((n_branch != 1 && n_branch != 2) || !x || !widths || !w_t || !bias || !w_value || !b_value || !values)
         return fail(VN_ERR_INVALID, "bad arguments");
     if (n_layers < 1 || n_layers > MH_MAXL) return fail(VN_ERR_INVALID, "n_layers %d outside 1..%d", n_layers, MH_MAXL);
-    if (M < 1 || K0 < MH_KC || K0 > 256 || (K0 % MH_KC) || ldx < K0 || (ldx & 3))
+    if (M < 1 || K0 < 16 || K0 > 256 || (K0 % 16) || ldx < K0 || (ldx & 3))
         return fail(VN_ERR_INVALID, "bad sizes M=%d K0=%d ldx=%lld (K0 %% 16, <= 256; ldx %% 4)", M, K0,
                     (long long)ldx);
     if (n_branch == 2 && (!w_action || !b_action || !actions || !log_probs || n_actions < 1 || n_actions > MH_MAXA))
@@ -789,6 +846,7 @@ int vn_mlp_head_f32(int32_t n_branch, const float *const *x, int64_t ldx, int32_
         if (widths[l] != 128 && widths[l] != 256) return fail(VN_ERR_INVALID, "layer %d width %d: 128 or 256", l, widths[l]);
         a.width[l] = widths[l];
     }
+    if (a.width[n_layers - 1] > MH_MAXP) return fail(VN_ERR_INVALID, "head width > %d", MH_MAXP);
     const int br0 = n_branch == 2 ? 0 : 1;
     for (int b = 0; b < n_branch; ++b) {
         if (!x[b] || (reinterpret_cast<uintptr_t>(x[b]) & 15)) return fail(VN_ERR_INVALID, "x[%d]: NULL or not 16-B aligned", b);
@@ -797,7 +855,7 @@ int vn_mlp_head_f32(int32_t n_branch, const float *const *x, int64_t ldx, int32_
             const float *w = w_t[b * n_layers + l];
             if (!w || (reinterpret_cast<uintptr_t>(w) & 15) || !bias[b * n_layers + l])
                 return fail(VN_ERR_INVALID, "branch %d layer %d: NULL or unaligned weights", b, l);
-            a.wt[br0 + b][l] = w;
+            a.wp[br0 + b][l] = w;
             a.bias[br0 + b][l] = bias[b * n_layers + l];
         }
     }

@@ -153,7 +153,7 @@ class _Weights:
                          and os.environ.get("VOXNAV_MLP_HEAD", "1") != "0")
         if self.mlp_head:
             self.widths = widths
-            self.mh_wt = [w.t().contiguous() for w, _ in self.pi] + [w.t().contiguous() for w, _ in self.vf]
+            self.mh_wt = [pack_mlp_head_f32(w) for w, _ in self.pi] + [pack_mlp_head_f32(w) for w, _ in self.vf]
             self.mh_b = [b for _, b in self.pi] + [b for _, b in self.vf]
 
 
@@ -178,6 +178,16 @@ def pack_linear_f32(w: torch.Tensor) -> torch.Tensor:
     """W [Nout, K] in vn_linear_f32's layout [Nout/128][K][128]."""
     n, k = w.shape
     return w.detach().to(torch.float32).reshape(n // 128, 128, k).permute(0, 2, 1).contiguous()
+
+
+def pack_mlp_head_f32(w: torch.Tensor) -> torch.Tensor:
+    """W [N, K] in vn_mlp_head_f32's per-lane layout [N/32][Kp/8][64][4], K
+    zero-padded to Kp = a multiple of 32: element [cb][kg][lane][s] =
+    W[32 cb + lane % 32][8 kg + 4 (lane // 32) + s]."""
+    n, k = w.shape
+    kp = (k + 31) // 32 * 32
+    w = torch.nn.functional.pad(w.detach().to(torch.float32), (0, kp - k))
+    return w.reshape(n // 32, 32, kp // 8, 2, 4).permute(0, 2, 3, 1, 4).contiguous()
 
 
 def _mlp(layers, x):

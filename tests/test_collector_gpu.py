@@ -654,7 +654,8 @@ def test_mlp_head_f32_matches_float64(voxnav, M, K0, widths, nb):
     P, A = widths[-1], 6
     wa, ba = rn(A, P, sc=3.0 / P ** 0.5), rn(A, sc=0.5)
     wv, bv = rn(P, sc=1.0 / P ** 0.5), rn(1)
-    wt = [w.t().contiguous() for ls in layers for w, _ in ls]
+    from voxnav.collector import pack_mlp_head_f32
+    wt = [pack_mlp_head_f32(w) for ls in layers for w, _ in ls]
     bs = [b for ls in layers for _, b in ls]
     arr = lambda ts: (C.c_void_p * len(ts))(*[t.data_ptr() for t in ts])  # noqa: E731
     p = lambda t: None if t is None else C.c_void_p(t.data_ptr())  # noqa: E731
