@@ -549,6 +549,11 @@ struct MlpHeadArgs {
 // WIDE: two column tiles; else one tile, even / odd k-groups into acc0 / acc1.
 typedef float mh_f4 __attribute__((ext_vector_type(4)));
 
+// the MLP layers' Tanh on the hardware exp and reciprocal (v_rcp_f32, 1 ulp;
+// |err| <= ~3e-7 absolute) -- the correctly rounded __frcp_rn costs a
+// division sequence per element in the epilogues
+__device__ __forceinline__ float mh_tanh(float x) { return 1.0f - 2.0f * __builtin_amdgcn_rcpf(1.0f + __expf(2.0f * x)); }
+
 // One layer's K loop of a wave: A from the act rows (one ds_read_b128 per
 // k-group of 8), B from the per-lane packed weights through the wave's own
 // LDS ring of MH_D k-groups (global_load_lds, 16 B per lane; each wave reads
@@ -563,10 +568,10 @@ __device__ __forceinline__ void mh_layer(const float *Ar, const float4 *B0, cons
     constexpr int PER = WIDE ? 2 : 1;                      // 1-KB loads per k-group
     auto issue = [&](int kg, int slot) {
         float *ring = slot == 0 ? ring0 : ring1;
-        __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void *)(B0 + kg * 64),
+        __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void *)(B0 + kg * 64 + lane),
                                          (__attribute__((address_space(3))) void *)ring, 16, 0, 0);
         if (WIDE)
-            __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void *)(B1 + kg * 64),
+            __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void *)(B1 + kg * 64 + lane),
                                              (__attribute__((address_space(3))) void *)(ring + 256), 16, 0, 0);
     };
 #pragma unroll
@@ -627,7 +632,8 @@ __global__ __launch_bounds__(256, 3) void mlp_head_f32_kernel(MlpHeadArgs a) {
     __shared__ __attribute__((aligned(16))) float ring0s[4 * 2 * 256];
     __shared__ __attribute__((aligned(16))) float ring1s[4 * 2 * 256];
     static_assert(4 * 2 * 256 >= MH_MAXA * MH_MAXP && 4 * 2 * 256 >= MH_MAXP, "head weights fit the ring");
-    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);   // wave-uniform: the ring and weight bases in SGPRs
     const int col = lane & 31, kh = lane >> 5;
     const int br = a.br0 + (int)blockIdx.y;
     const int m0 = (int)blockIdx.x * MH_R;
@@ -640,20 +646,20 @@ __global__ __launch_bounds__(256, 3) void mlp_head_f32_kernel(MlpHeadArgs a) {
             const int m = min(m0 + r, a.M - 1);
             *reinterpret_cast<float4 *>(act + r * MH_P + k) = *reinterpret_cast<const float4 *>(x + (size_t)m * a.ldx + k);
         }
-        const int qp = ((a.K0 + 31) / 32 * 32) / 4;          // zero columns up to the padded K
+        const int qp = ((a.K0 + 8 * MH_D - 1) / (8 * MH_D) * (8 * MH_D)) / 4;   // zero columns up to the padded K
         for (int f = tid; f < MH_R * (qp - q4); f += 256) {
             const int r = f / (qp - q4), k = 4 * (q4 + f - r * (qp - q4));
             *reinterpret_cast<float4 *>(act + r * MH_P + k) = make_float4(0.f, 0.f, 0.f, 0.f);
         }
     }
     __syncthreads();
-    int K = (a.K0 + 31) / 32 * 32;      // layer 0's K padded to whole prefetch rounds (zero rows / weights)
+    int K = (a.K0 + 8 * MH_D - 1) / (8 * MH_D) * (8 * MH_D);   // layer 0's K: whole ring rounds (zero rows / weights)
     for (int l = 0; l < a.n_layers; ++l) {
         const int N = a.width[l];
         const bool wide = N == 256;
         const int KG = K / 8;
         const int cb0 = wide ? 2 * wv : wv;                     // this wave's first 32-column block
-        const float4 *B0 = reinterpret_cast<const float4 *>(a.wp[br][l]) + (size_t)cb0 * KG * 64 + lane;
+        const float4 *B0 = reinterpret_cast<const float4 *>(a.wp[br][l]) + (size_t)cb0 * KG * 64;   // uniform
         const float *Ar = act + col * MH_P + 4 * kh;
         f32x16_t acc0 = zero16(), acc1 = zero16();
         float *r0 = ring0s + wv * 512, *r1 = ring1s + wv * 512;
@@ -668,14 +674,14 @@ __global__ __launch_bounds__(256, 3) void mlp_head_f32_kernel(MlpHeadArgs a) {
 #pragma unroll
             for (int reg = 0; reg < 16; ++reg) {
                 float *d = act + (8 * (reg >> 2) + 4 * kh + (reg & 3)) * MH_P + n0 + col;
-                d[0] = PF_TANH(acc0[reg] + bj0);
-                d[32] = PF_TANH(acc1[reg] + bj1);
+                d[0] = mh_tanh(acc0[reg] + bj0);
+                d[32] = mh_tanh(acc1[reg] + bj1);
             }
         } else {
             const float bj = bias[n0 + col];
 #pragma unroll
             for (int reg = 0; reg < 16; ++reg)
-                act[(8 * (reg >> 2) + 4 * kh + (reg & 3)) * MH_P + n0 + col] = PF_TANH((acc0[reg] + acc1[reg]) + bj);
+                act[(8 * (reg >> 2) + 4 * kh + (reg & 3)) * MH_P + n0 + col] = mh_tanh((acc0[reg] + acc1[reg]) + bj);
         }
         __syncthreads();
         K = N;

@@ -182,10 +182,10 @@ def pack_linear_f32(w: torch.Tensor) -> torch.Tensor:
 
 def pack_mlp_head_f32(w: torch.Tensor) -> torch.Tensor:
     """W [N, K] in vn_mlp_head_f32's per-lane layout [N/32][Kp/8][64][4], K
-    zero-padded to Kp = a multiple of 32: element [cb][kg][lane][s] =
+    zero-padded to Kp = a multiple of 16: element [cb][kg][lane][s] =
     W[32 cb + lane % 32][8 kg + 4 (lane // 32) + s]."""
     n, k = w.shape
-    kp = (k + 31) // 32 * 32
+    kp = (k + 15) // 16 * 16
     w = torch.nn.functional.pad(w.detach().to(torch.float32), (0, kp - k))
     return w.reshape(n // 32, 32, kp // 8, 2, 4).permute(0, 2, 3, 1, 4).contiguous()
 

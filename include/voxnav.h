@@ -324,7 +324,7 @@ int vn_policy_head_bf16(const uint16_t *latent_pi, const uint16_t *latent_vf, in
  *   w_t[b * n_layers + l]  f32 W_l [N_l][K_l] packed per MFMA lane (16-byte
  *               aligned): [N_l/32][K_l/8][64][4], element [cb][kg][lane][s] =
  *               W_l[32 cb + lane % 32][8 kg + 4 (lane / 32) + s];
- *               K_0 = K0 rounded up to a multiple of 32 (zero weights past K0),
+ *               K_0 = K0 rounded up to a multiple of 16 (zero weights past K0),
  *               K_l = widths[l - 1];  bias[b * n_layers + l] [N_l]
  *   w_action [n_actions][P], b_action (pi branch; n_actions <= 8),
  *   w_value [P], b_value [1]
