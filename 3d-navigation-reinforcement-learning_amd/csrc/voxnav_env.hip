@@ -451,150 +451,6 @@ __device__ __forceinline__ uint32_t group_or(uint32_t m) {
     return m;
 }
 
-// ----------------------------------------------------------------------------
-// Plane-set mode with a z band (PCM 4: PH 16, rooms <= 64 x 64, u64 rows --
-// the reference's training rooms, up to 48 x 37 x 12).  The full-height sets
-// of PCM 1/2 (8 sets x PH rows) do not fit the LDS at PH 16 with 4 waves per
-// SIMD; but the window only ever shows levels z-2 .. z+1 and a sensing pass
-// marks level z, so each of the 8 sets keeps just those 4 rows, at slot
-// (level & 3) -- toroidal like the tile's columns (256 B per agent).
-//   * a horizontal move swaps one set: lane q the row of its level slot;
-//   * a z move swaps one level of every set: the leaving level's rows written
-//     back if dirty, the entering level's loaded, and its plane bits merged
-//     into the 16 window columns of the tile;
-//   * a column entering the window merges the band levels' plane bits.
-// Tile bytes outside the band may lack plane bits; nothing reads them before
-// a z move merges their level.  The byte map in HBM is, as in PCM 1/2, the
-// room image (latent walls) plus the agent's own columns (visits, z rays);
-// every x / y ray mark lives only in the planes.
-// LDS: ps[set * 4 + slot], sets 0..3 the x-plane rows of window row y' (set
-// y' & 3), 4..7 the y-plane rows of window column x' (set 4 + (x' & 3));
-// pdirty bit set * 4 + slot.
-// ----------------------------------------------------------------------------
-constexpr int ZB_STRIDE = 8 * 4;      // u64 per agent
-
-// the level of the band around z whose slot is q (levels z-2 .. z+1 cover each residue once)
-__device__ __forceinline__ int zb_level(int z, int q) { return z - 2 + ((q - (z - 2)) & 3); }
-
-__device__ __forceinline__ uint64_t *zb_row(const Params &p, int8_t *map, bool xs, int c, int lev) {
-    return reinterpret_cast<uint64_t *>(map + (xs ? p.xp_off : p.yp_off)) + (size_t)(c * 16 + lev);
-}
-
-// launch start: lane q loads the rows of its level slot of the 8 sets
-__device__ __forceinline__ void zb_fill(const Params &p, int8_t *map, uint64_t *ps, const Agent &g, const Room &R,
-                                        int q) {
-    const int lev = zb_level(g.z, q);
-    const bool lin = lev >= 0 && lev < R.H;
-    uint64_t v[8];
-#pragma unroll
-    for (int s = 0; s < 4; ++s) {
-        const int yy = g.y - 2 + s, xx = g.x - 2 + s;
-        v[s] = (lin && yy >= 0 && yy < R.D) ? *zb_row(p, map, true, yy, lev) : 0ull;
-        v[4 + s] = (lin && xx >= 0 && xx < R.W) ? *zb_row(p, map, false, xx, lev) : 0ull;
-    }
-#pragma unroll
-    for (int s = 0; s < 4; ++s) {
-        ps[((g.y - 2 + s) & 3) * 4 + q] = v[s];
-        ps[(4 + ((g.x - 2 + s) & 3)) * 4 + q] = v[4 + s];
-    }
-    __builtin_amdgcn_wave_barrier();
-}
-
-// launch end: the dirty rows back to HBM
-__device__ __forceinline__ void zb_flush(const Params &p, int8_t *map, const uint64_t *ps, const Agent &g,
-                                         const Room &R, uint32_t pdirty, int q) {
-    const int lev = zb_level(g.z, q);
-    if (lev < 0 || lev >= R.H) return;
-#pragma unroll
-    for (int s = 0; s < 4; ++s) {
-        const int yy = g.y - 2 + s, xx = g.x - 2 + s;
-        const int sx = (yy & 3), sy = 4 + (xx & 3);
-        if (((pdirty >> (sx * 4 + q)) & 1u) && yy >= 0 && yy < R.D) *zb_row(p, map, true, yy, lev) = ps[sx * 4 + q];
-        if (((pdirty >> (sy * 4 + q)) & 1u) && xx >= 0 && xx < R.W) *zb_row(p, map, false, xx, lev) = ps[sy * 4 + q];
-    }
-}
-
-struct ZbLoad {
-    uint64_t v, v2;      // horizontal move: v (the entering set's row); z move: v (x set q), v2 (y set q)
-    int slot;            // horizontal: the set replaced; z move: the level slot replaced
-};
-
-// after a horizontal move in axis dir to (x, y): lane q's row of the entering
-// set (load first), the leaving set's row back if dirty
-__device__ __forceinline__ void zb_shift_issue(const Params &p, int8_t *map, const uint64_t *ps, int dir, int x, int y,
-                                               int z, const Room &R, uint32_t pdirty, int q, ZbLoad &zl) {
-    const bool xm = dir < 2;
-    const int e = xm ? (dir == 0 ? x + 1 : x - 2) : (dir == 2 ? y + 1 : y - 2);
-    const int l = (dir == 0 || dir == 2) ? e - 4 : e + 4;
-    const int lim = xm ? R.W : R.D;
-    const int lev = zb_level(z, q);
-    const bool lin = lev >= 0 && lev < R.H;
-    zl.slot = xm ? 4 + (e & 3) : (e & 3);
-    zl.v = (lin && e >= 0 && e < lim) ? *zb_row(p, map, !xm, e, lev) : 0ull;
-    if (((pdirty >> (zl.slot * 4 + q)) & 1u) && lin && l >= 0 && l < lim) *zb_row(p, map, !xm, l, lev) = ps[zl.slot * 4 + q];
-}
-
-__device__ __forceinline__ uint32_t zb_shift_commit(uint64_t *ps, const ZbLoad &zl, uint32_t pdirty, int q) {
-    ps[zl.slot * 4 + q] = zl.v;
-    __builtin_amdgcn_wave_barrier();
-    return pdirty & ~(0xfu << (zl.slot * 4));
-}
-
-// after a z move to (x, y, z): the entering level (z + 1 up, z - 2 down)
-// replaces the leaving one (z - 3 up, z + 2 down) in slot e & 3 of every set;
-// lane q takes x set q and y set 4 + q (window row / column of residue q)
-__device__ __forceinline__ void zb_level_issue(const Params &p, int8_t *map, const uint64_t *ps, bool up, int x, int y,
-                                               int z, const Room &R, uint32_t pdirty, int q, ZbLoad &zl) {
-    const int e = up ? z + 1 : z - 2, lv = up ? z - 3 : z + 2;
-    const int es = e & 3;
-    zl.slot = es;
-    const int yy = y - 2 + ((q - (y - 2)) & 3), xx = x - 2 + ((q - (x - 2)) & 3);
-    const bool ein = e >= 0 && e < R.H, lin = lv >= 0 && lv < R.H;
-    zl.v = (ein && yy >= 0 && yy < R.D) ? *zb_row(p, map, true, yy, e) : 0ull;
-    zl.v2 = (ein && xx >= 0 && xx < R.W) ? *zb_row(p, map, false, xx, e) : 0ull;
-    if (lin && ((pdirty >> (q * 4 + es)) & 1u) && yy >= 0 && yy < R.D) *zb_row(p, map, true, yy, lv) = ps[q * 4 + es];
-    if (lin && ((pdirty >> ((4 + q) * 4 + es)) & 1u) && xx >= 0 && xx < R.W)
-        *zb_row(p, map, false, xx, lv) = ps[(4 + q) * 4 + es];
-}
-
-// commit, then merge the entering level's plane bits into lane q's 4 window
-// columns (row y + q - 2) of the tile
-template <int PH>
-__device__ __forceinline__ uint32_t zb_level_commit(uint64_t *ps, uint64_t *tile, const ZbLoad &zl, uint32_t pdirty,
-                                                    bool up, int x, int y, int z, const Room &R, int q) {
-    const int es = zl.slot;
-    ps[q * 4 + es] = zl.v;
-    ps[(4 + q) * 4 + es] = zl.v2;
-    __builtin_amdgcn_wave_barrier();
-    const int e = up ? z + 1 : z - 2;
-    const int cy = y + q - 2;
-    if (e >= 0 && e < R.H && cy >= 0 && cy < R.D) {
-        const uint64_t xr = ps[(cy & 3) * 4 + es];
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            const int cx = x + i - 2;
-            if (cx < 0 || cx >= R.W) continue;
-            const uint64_t yr = ps[(4 + (cx & 3)) * 4 + es];
-            if (((xr >> cx) | (yr >> cy)) & 1ull) {
-                uint8_t *b = reinterpret_cast<uint8_t *>(tile + tslot(cx, cy) * TileGeom<PH>::QW) + e;
-                *b = (uint8_t)(*b | KNOWN);
-            }
-        }
-    }
-    return pdirty & ~(0x11111111u << es);
-}
-
-// KNOWN at the band levels z-2 .. z+1 (inside the room) of column (cx, cy), both in the window
-template <int PH>
-__device__ __forceinline__ void zb_merge(Col<PH> &c, const uint64_t *ps, int cx, int cy, int z, int H) {
-    const uint64_t *xs = ps + (cy & 3) * 4, *ys = ps + (4 + (cx & 3)) * 4;
-#pragma unroll
-    for (int d = 0; d < 4; ++d) {
-        const int lev = z - 2 + d;
-        if (lev >= 0 && lev < H) col_or<PH>(c, lev, (uint32_t)(((xs[lev & 3] >> cx) | (ys[lev & 3] >> cy)) & 1ull) << 7);
-    }
-}
-
 struct PlaneCache {      // lane 0: x-plane row, lane 1: y-plane row
     uint64_t w[2];
     int row, w0;         // cached row index and first word; row < 0: invalid
@@ -610,7 +466,7 @@ struct PlaneCache {      // lane 0: x-plane row, lane 1: y-plane row
 
 // Fill the tile from HBM (launch start): lane q loads its 4 window columns.
 // PC: the plane sets (ps, already filled) add their known bits.
-template <int PH, bool PC, typename RT, bool SB = false, bool ZB = false>
+template <int PH, bool PC, typename RT, bool SB = false>
 __device__ __forceinline__ void tile_fill(const Params &p, const int8_t *map, uint64_t *tile, const RT *ps,
                                           const Agent &g, const Room &R, int q, const Stood &st) {
     const int cy = g.y + q - 2;
@@ -624,8 +480,7 @@ __device__ __forceinline__ void tile_fill(const Params &p, const int8_t *map, ui
         if (cx >= 0 && cx < R.W && cy >= 0 && cy < R.D) {
             // SB: a column never stood in is the room image's
             col_load<PH>((!SB || ((srow >> cx) & 1u) ? map : img) + boff<PH>(cx, cy, 0, p.nby), c);
-            if constexpr (ZB) zb_merge<PH>(c, reinterpret_cast<const uint64_t *>(ps), cx, cy, g.z, R.H);
-            else if constexpr (PC) c.w[0] |= pset_known(ps, cx, cy);
+            if constexpr (PC) c.w[0] |= pset_known(ps, cx, cy);
         }
         tile_write<PH>(tile, tslot(cx, cy), c);
     }
@@ -837,7 +692,7 @@ __device__ __forceinline__ void pend_apply(const Params &p, int8_t *map, PlaneCa
 // Returns the center cell's visit count after the update.
 // PC: plane-set mode (ps = the agent's LDS plane sets, pdirty their dirty bits).
 // DM: byte-mark mode with deferred plane marks (PendMarks; PCM 3).
-template <int PH, bool FRESH, bool PC, typename RT, bool DM, bool ZB = false>
+template <int PH, bool FRESH, bool PC, typename RT, bool DM>
 __device__ __forceinline__ int sense_observe(const Params &p, int8_t *map, uint64_t *tile, uint32_t &dirty,
                                              PlaneCache &pc_, RT *ps, uint32_t &pdirty, Agent &g,
                                              const Room &R, bool moved, bool &explored, const float *tab, ObsDst dst,
@@ -859,9 +714,7 @@ __device__ __forceinline__ int sense_observe(const Params &p, int8_t *map, uint6
         (void)nw;
     }
     // PC: lane 0 owns the x-plane row (y, z), lane 1 the y-plane row (x, z), both in LDS
-    // ZB: the band's row of level z (slot z & 3)
-    const int pset_of = q == 0 ? (y & 3) : 4 + (x & 3);
-    RT *prow_lds = (PC && q < 2) ? ps + (ZB ? pset_of * 4 + (z & 3) : pset_of * 8 + z) : nullptr;
+    RT *prow_lds = (PC && q < 2) ? ps + (q == 0 ? (y & 3) : 4 + (x & 3)) * 8 + z : nullptr;
 
     // ---- this lane's 4 window columns from the tile: the window word
     //      (bytes z-2 .. z+1) of each, and the whole column dx = 0 (lane 2's
@@ -1017,7 +870,7 @@ __device__ __forceinline__ int sense_observe(const Params &p, int8_t *map, uint6
             const uint64_t nv = pn[0] | pm[0];
             if (nv != pn[0]) {
                 *prow_lds = (RT)nv;
-                pd = ZB ? 1u << (pset_of * 4 + (z & 3)) : 1u << pset_of;
+                pd = 1u << (q == 0 ? (y & 3) : 4 + (x & 3));
             }
         }
         pdirty |= group_or(pd);
@@ -1189,7 +1042,7 @@ __device__ __noinline__ uint32_t reset_prepare(const EnvConst *ec, uint32_t seed
 // the new room's bricks and planes in HBM by the 4 lanes, a zero tile, then
 // sensing from the start cell.  The old episode's dirty tile is dropped.
 // ----------------------------------------------------------------------------
-template <int PH, bool PC, typename RT, bool SB, bool DM, bool ZB = false>
+template <int PH, bool PC, typename RT, bool SB, bool DM>
 __device__ __forceinline__ void group_reset(const Params &p, int8_t *map, uint64_t *tile, uint32_t &dirty,
                                             PlaneCache &pc_, RT *ps, uint32_t &pdirty, bool need,
                                             uint32_t seed, Agent &g, Room &R, const float *tab, float *obs_row,
@@ -1215,11 +1068,7 @@ __device__ __forceinline__ void group_reset(const Params &p, int8_t *map, uint64
         dirty = 0;
         pc_.row = -1;
         pc_.dirty = 0u;                   // the ended episode's cached row: its planes are cleared
-        if (ZB) {                         // the planes were cleared: empty bands
-#pragma unroll
-            for (int k = 0; k < 8; ++k) ps[k * 4 + q] = (RT)0;
-            pdirty = 0;
-        } else if (PC) {                  // the planes were cleared: empty sets
+        if (PC) {                         // the planes were cleared: empty sets
 #pragma unroll
             for (int k = 0; k < 8; ++k) pset_put(ps, 2 * q + (k >> 2), k & 3, pset_zero<RT>());
             pdirty = 0;
@@ -1236,8 +1085,8 @@ __device__ __forceinline__ void group_reset(const Params &p, int8_t *map, uint64
         if (SB && q == 0) st.row[g.y] |= 1u << g.x;   // the start column
         bool explored = false;
         const uint2 rec = p.rays[R.ray_off + (uint32_t)((g.x * R.D + g.y) * R.H + g.z)];
-        sense_observe<PH, true, PC, RT, DM, ZB>(p, map, tile, dirty, pc_, ps, pdirty, g, R, false, explored, tab,
-                                                ObsDst{obs_row, nullptr, stage, false, false, aslot}, rec, q, pend);
+        sense_observe<PH, true, PC, RT, DM>(p, map, tile, dirty, pc_, ps, pdirty, g, R, false, explored, tab,
+                                            ObsDst{obs_row, nullptr, stage, false, false, aslot}, rec, q, pend);
     }
 }
 
@@ -1318,22 +1167,19 @@ template <int PH, bool EXT, bool FAST, bool RESET_ONLY, int PCM>
 #ifndef VN_MIN_WAVES_PER_SIMD
 #define VN_MIN_WAVES_PER_SIMD 4   // <= 128 VGPRs: the 16 waves of 256 agents per CU resident at once
 #endif
-__global__ __launch_bounds__((PCM == 1 || PCM == 2 || PCM == 4) ? VN_PC_BLOCK : BLOCK,
-                             (PCM == 1 || PCM == 2 || PCM == 4) ? VN_PC_MIN_WAVES : VN_MIN_WAVES_PER_SIMD) void env_kernel(Params p) {
-    constexpr bool ZB = PCM == 4;                // plane-set mode with a z band (PH 16)
-    constexpr bool PC = PCM == 1 || PCM == 2 || ZB;   // plane-set mode
+__global__ __launch_bounds__((PCM == 1 || PCM == 2) ? VN_PC_BLOCK : BLOCK,
+                             (PCM == 1 || PCM == 2) ? VN_PC_MIN_WAVES : VN_MIN_WAVES_PER_SIMD) void env_kernel(Params p) {
+    constexpr bool PC = PCM == 1 || PCM == 2;   // plane-set mode
     constexpr bool DM = PCM == 3;                // byte-mark mode, deferred plane marks
     using RT = typename std::conditional<PCM == 2, uint32_t, uint64_t>::type;
-    static_assert(!ZB || PH == 16, "the z band is the PH 16 plane-set mode");
     constexpr int kAgents = (PC ? VN_PC_BLOCK : BLOCK) / GROUP;
-    constexpr int kPsStride = ZB ? ZB_STRIDE : PsetGeom<RT>::STRIDE;
     static_assert(!PC || kAgents <= 64, "tc_slot has 64 obs[72] codes per block");
     __shared__ float tab[TAB_SIZE];
     __shared__ __attribute__((aligned(16))) uint64_t tiles[kAgents * TileGeom<PH>::STRIDE];
     // obs rows of the step, staged per wave (STAGE_WORDS) so HBM sees 1 KiB contiguous stores
     constexpr int kStageWords = PC ? STAGE_WORDS : STAGE_WORDS_F;
     __shared__ __attribute__((aligned(16))) uint32_t stage[(kAgents / 16) * kStageWords];
-    __shared__ __attribute__((aligned(16))) RT psets[PC ? kAgents * kPsStride : 2];
+    __shared__ __attribute__((aligned(16))) RT psets[PC ? kAgents * PsetGeom<RT>::STRIDE : 2];
     constexpr bool SB = PCM == 2 && VN_STOOD;
     __shared__ uint32_t stood_lds[SB ? kAgents * kStoodStride : 1];
 #ifdef VN_LDS_PAD_U64            // diagnostics: occupancy at a larger LDS footprint
@@ -1379,7 +1225,7 @@ __global__ __launch_bounds__((PCM == 1 || PCM == 2 || PCM == 4) ? VN_PC_BLOCK : 
     pc_.dirty = 0u;
     PendMarks pend;                        // DM: the previous sensing pass's plane marks, not yet applied
     pend.valid = 0;
-    RT *ps = psets + (PC ? (threadIdx.x / GROUP) * kPsStride : 0);
+    RT *ps = psets + (PC ? (threadIdx.x / GROUP) * PsetGeom<RT>::STRIDE : 0);
     uint32_t pdirty = 0;
     Stood st;
     st.row = SB ? stood_lds + (threadIdx.x / GROUP) * kStoodStride : nullptr;
@@ -1396,7 +1242,7 @@ __global__ __launch_bounds__((PCM == 1 || PCM == 2 || PCM == 4) ? VN_PC_BLOCK : 
     if (RESET_ONLY) {
         const bool need = active && (p.mask == nullptr || p.mask[i] != 0);
         const uint32_t seed = need ? (uint32_t)p.seeds[i] : 0u;
-        group_reset<PH, PC, RT, SB, DM, ZB>(p, map, tile, dirty, pc_, ps, pdirty, need, seed, g, R, tab,
+        group_reset<PH, PC, RT, SB, DM>(p, map, tile, dirty, pc_, ps, pdirty, need, seed, g, R, tab,
                                         need ? p.obs + (size_t)i * VN_OBS_DIM : nullptr, nullptr, 0, q, st, pend);
         if (need) {
             if constexpr (DM) {
@@ -1404,8 +1250,7 @@ __global__ __launch_bounds__((PCM == 1 || PCM == 2 || PCM == 4) ? VN_PC_BLOCK : 
                 plane_wb_flush(p, map, pc_, q);
             }
             tile_flush<PH>(p, map, tile, g, R, dirty, q);
-            if constexpr (ZB) zb_flush(p, map, reinterpret_cast<const uint64_t *>(ps), g, R, pdirty, q);
-            else if (PC) pset_flush<RT, SB>(p, map, ps, g, R, pdirty, q, st);
+            if (PC) pset_flush<RT, SB>(p, map, ps, g, R, pdirty, q, st);
             if (SB) {
                 __builtin_amdgcn_wave_barrier();
                 const uint32_t *r = st.row + 8 * q;
@@ -1473,9 +1318,8 @@ __global__ __launch_bounds__((PCM == 1 || PCM == 2 || PCM == 4) ? VN_PC_BLOCK : 
             }
         }
         if (!(VN_ABLATE & 16384u)) {   // diagnostics: 16384 skips the launch's fill
-            if constexpr (ZB) zb_fill(p, map, reinterpret_cast<uint64_t *>(ps), gf, R, q);
-            else if (PC) pset_fill<RT, SB>(p, map, ps, gf, R, q, st);
-            tile_fill<PH, PC, RT, SB, ZB>(p, map, tile, ps, gf, R, q, st);
+            if (PC) pset_fill<RT, SB>(p, map, ps, gf, R, q, st);
+            tile_fill<PH, PC, RT, SB>(p, map, tile, ps, gf, R, q, st);
         }
     }
 #if VN_ENV_PROF
@@ -1560,19 +1404,10 @@ __global__ __launch_bounds__((PCM == 1 || PCM == 2 || PCM == 4) ? VN_PC_BLOCK : 
             // column (and plane set), the new cell's ray record, its plane rows
             // (PREMOVE: the launch's window was filled around step 0's cell)
             const bool shifted = moved && dir < 4 && !(PREMOVE && k == 0);
-            // ZB: a z move shifts the band of every plane set by one level
-            const bool zshifted = ZB && moved && dir >= 4 && !(PREMOVE && k == 0);
             ShiftLoad<PH> sl;
             SetLoad<RT> pl;
-            ZbLoad zl;
             if (shifted) tile_shift_issue<PH, SB>(p, map, tile, dir, g.x, g.y, R, dirty, q, sl, st, g.room);
-            if constexpr (ZB) {
-                uint64_t *pb = reinterpret_cast<uint64_t *>(ps);
-                if (shifted) zb_shift_issue(p, map, pb, dir, g.x, g.y, g.z, R, pdirty, q, zl);
-                else if (zshifted) zb_level_issue(p, map, pb, dir == 4, g.x, g.y, g.z, R, pdirty, q, zl);
-            } else if (PC && shifted) {
-                pset_shift_issue<RT, SB>(p, map, ps, dir, g.x, g.y, R, pdirty, q, pl, st);
-            }
+            if (PC && shifted) pset_shift_issue<RT, SB>(p, map, ps, dir, g.x, g.y, R, pdirty, q, pl, st);
             uint2 rec;
             if (VN_ABLATE & 8192u) {   // diagnostics: the record computed for a walled box (exact for box rooms only)
                 const uint32_t ex = (uint32_t)(R.W - 2 - g.x) | 0x80u, wx = (uint32_t)(g.x - 1) | 0x80u;
@@ -1587,20 +1422,11 @@ __global__ __launch_bounds__((PCM == 1 || PCM == 2 || PCM == 4) ? VN_PC_BLOCK : 
             if (!PC) plane_prefetch<PH>(p, map, pc_, g.x, g.y, g.z, q);
             ENV_T(0);
             if (shifted) {
-                if constexpr (ZB) {
-                    uint64_t *pb = reinterpret_cast<uint64_t *>(ps);
-                    pdirty = zb_shift_commit(pb, zl, pdirty, q);
-                    if (sl.in) zb_merge<PH>(sl.c, pb, sl.ex, sl.ey, g.z, R.H);
-                } else if constexpr (PC) {
+                if constexpr (PC) {
                     pdirty = pset_shift_commit(ps, pl, pdirty, q);
                     if (sl.in) sl.c.w[0] |= pset_known(ps, sl.ex, sl.ey);
                 }
                 dirty = tile_shift_commit<PH>(tile, sl, dirty);
-            }
-            if constexpr (ZB) {
-                if (zshifted)
-                    pdirty = zb_level_commit<PH>(reinterpret_cast<uint64_t *>(ps), tile, zl, pdirty, dir == 4, g.x,
-                                                 g.y, g.z, R, q);
             }
             if (SB && moved && dir < 4 && q == 0) {       // the agent's new column: stood in
                 const uint32_t o = st.row[g.y], b = 1u << g.x;
@@ -1615,8 +1441,8 @@ __global__ __launch_bounds__((PCM == 1 || PCM == 2 || PCM == 4) ? VN_PC_BLOCK : 
             const ObsDst dst{p.obs + row * VN_OBS_DIM,
                              p.terminal_obs ? p.terminal_obs + row * VN_OBS_DIM : nullptr, wst,
                              p.autoreset != 0, truncated, aslot};
-            const int vv = sense_observe<PH, false, PC, RT, DM, ZB>(p, map, tile, dirty, pc_, ps, pdirty, g, R,
-                                                                    moved, explored, tab, dst, rec, q, pend, k == 0);
+            const int vv = sense_observe<PH, false, PC, RT, DM>(p, map, tile, dirty, pc_, ps, pdirty, g, R,
+                                                                moved, explored, tab, dst, rec, q, pend, k == 0);
             ENV_T(2);
 
             if constexpr (STRIPE_R) {
@@ -1682,7 +1508,7 @@ __global__ __launch_bounds__((PCM == 1 || PCM == 2 || PCM == 4) ? VN_PC_BLOCK : 
         const bool need = p.autoreset && finished;
         if (__ballot(need)) {
             const uint32_t seed = next_seed;
-            group_reset<PH, PC, RT, SB, DM, ZB>(p, map, tile, dirty, pc_, ps, pdirty, need, seed, g, R, tab,
+            group_reset<PH, PC, RT, SB, DM>(p, map, tile, dirty, pc_, ps, pdirty, need, seed, g, R, tab,
                                             need ? p.obs + row * VN_OBS_DIM : nullptr, wst, aslot, q, st, pend);
             if (need) next_seed = seed + p.seed_stride;
         }
@@ -1750,8 +1576,7 @@ __global__ __launch_bounds__((PCM == 1 || PCM == 2 || PCM == 4) ? VN_PC_BLOCK : 
         }
         if (!(VN_ABLATE & 32768u)) {   // diagnostics: 32768 skips the launch's flush
             tile_flush<PH>(p, map, tile, g, R, dirty, q);
-            if constexpr (ZB) zb_flush(p, map, reinterpret_cast<const uint64_t *>(ps), g, R, pdirty, q);
-            else if (PC) pset_flush<RT, SB>(p, map, ps, g, R, pdirty, q, st);
+            if (PC) pset_flush<RT, SB>(p, map, ps, g, R, pdirty, q, st);
         }
         if (q == 0) {
             p.hot[i] = pack(g);
@@ -1968,7 +1793,7 @@ Params base_params(VnEnv *e) {
 
 template <int PH, bool RESET_ONLY, int PCM>
 int launch_ph(int N, hipStream_t s, const Params &p) {
-    const int bs = (PCM == 1 || PCM == 2 || PCM == 4) ? VN_PC_BLOCK : BLOCK;
+    const int bs = (PCM == 1 || PCM == 2) ? VN_PC_BLOCK : BLOCK;
     const dim3 block((unsigned)bs);
     const dim3 grid((unsigned)(((size_t)N * GROUP + bs - 1) / bs));
     // FAST: the rollout-buffer call (f32 reward, flags; the f64 reward for the
@@ -1993,7 +1818,6 @@ int launch_ph(int N, hipStream_t s, const Params &p) {
 // else PCM 0.
 static int env_pcm(const VnEnv *e) {
     if (e->ph == 8 && e->pcache) return e->pcache;
-    if (e->ph == 16 && e->pcache == 4) return 4;
     return e->defer ? 3 : 0;
 }
 
@@ -2008,10 +1832,8 @@ int launch_env(VnEnv *e, const Params &p, hipStream_t s) {
         if (pcm == 3) return launch_ph<8, RESET_ONLY, 3>(e->N, s, p);
         return launch_ph<8, RESET_ONLY, 0>(e->N, s, p);
     }
-    if (e->ph == 16) {
-        if (pcm == 4) return launch_ph<16, RESET_ONLY, 4>(e->N, s, p);
+    if (e->ph == 16)
         return pcm == 3 ? launch_ph<16, RESET_ONLY, 3>(e->N, s, p) : launch_ph<16, RESET_ONLY, 0>(e->N, s, p);
-    }
     return pcm == 3 ? launch_ph<32, RESET_ONLY, 3>(e->N, s, p) : launch_ph<32, RESET_ONLY, 0>(e->N, s, p);
 }
 
@@ -2223,14 +2045,10 @@ int vn_create(const VnRoomSet *rooms, int32_t n_agents, const VnConfig *cfg, int
         e->nwx = (e->pw + 63) / 64;
         e->nwy = (e->pd + 63) / 64;
         // plane-set mode: 2 = u32 rows (rooms <= 32 x 32), 1 = u64 rows (<= 64 x 64), 0 = byte marks
-        // PH 16: 4 = u64 rows with a z band of 4 levels (rooms <= 64 x 64; zb_fill)
-        const char *zbk = getenv("VOXNAV_ZBAND");          // PCM 4 switch (1: on)
-        const bool zband = zbk && zbk[0] == '1';
-        e->pcache = e->ph == 16 ? ((zband && e->nwx == 1 && e->nwy == 1) ? 4 : 0)
-                    : e->ph != 8 ? 0 : (e->pw <= 32 && e->pd <= 32) ? 2 : (e->nwx == 1 && e->nwy == 1) ? 1 : 0;
-        if (const char *pc = getenv("VOXNAV_PCACHE")) {   // A/B knob: 0 off, 1 at most u64 rows (PH 8)
+        e->pcache = e->ph != 8 ? 0 : (e->pw <= 32 && e->pd <= 32) ? 2 : (e->nwx == 1 && e->nwy == 1) ? 1 : 0;
+        if (const char *pc = getenv("VOXNAV_PCACHE")) {   // A/B knob: 0 off, 1 at most u64 rows
             const int v = atoi(pc);
-            if (v >= 0 && v < e->pcache) e->pcache = e->ph == 16 ? 0 : v;
+            if (v >= 0 && v < e->pcache) e->pcache = v;
         }
         // byte-mark mode with plane rows of <= 2 words: defer each pass's plane marks
         // to the next step (PendMarks) so the row loads hide behind a step

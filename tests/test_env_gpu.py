@@ -121,33 +121,6 @@ def test_random_rollout_matches_oracle(voxnav, src, L, N, K):
     assert bad.size == 0, f"obs mismatch at (step, agent) {bad[:5].tolist()}"
 
 
-@pytest.mark.parametrize("src", ["set:P3_training", "set:P2_training", "file:P3_training/kitchen2.txt"])
-def test_byte_mark_mode_matches_oracle(voxnav, src, monkeypatch):
-    """The PH-16 rooms run the z-band plane-set mode (PCM 4) by default; the
-    byte-mark mode with deferred plane marks (PCM 3) stays selectable
-    (VOXNAV_PCACHE=0 at vn_create) and bit-exact: both modes against the
-    oracle on the same rollout, plus equal belief maps."""
-    L, N, K = 10, 512, 160
-    seeds = 42 + np.arange(N, dtype=np.int64)
-    orc = oracle_env(src, L, n_agents=N).run_random(seeds, policy_seed=3, K=K, seed_stride=N)
-    beliefs = []
-    for mode in ("", "0"):
-        if mode:
-            monkeypatch.setenv("VOXNAV_PCACHE", mode)
-        else:
-            monkeypatch.delenv("VOXNAV_PCACHE", raising=False)
-        env = make_env(voxnav, src, L, n=N, autoreset=True)
-        env.reset(seed=42)
-        ro = env.step_random(K, policy_seed=3, t0=0, reward_f64=True)
-        np.testing.assert_array_equal(ro.reward.cpu().numpy(), orc["reward"], err_msg=f"mode {mode!r}")
-        np.testing.assert_array_equal(ro.terminated.cpu().numpy(), orc["terminated"])
-        np.testing.assert_array_equal(ro.truncated.cpu().numpy(), orc["truncated"])
-        assert ro.obs.cpu().numpy().tobytes() == orc["obs"].tobytes(), f"obs, mode {mode!r}"
-        beliefs.append(env.belief().cpu().numpy())
-        env.close()
-    np.testing.assert_array_equal(beliefs[0], beliefs[1])
-
-
 FAST_CASES = [("ctor:32x32x8", 10, 1024, 160), ("set:P3_training", 10, 1000, 120), ("box:8x8x4", 4, 333, 200)]
 
 
