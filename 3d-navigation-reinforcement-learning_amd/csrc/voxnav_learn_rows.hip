@@ -40,6 +40,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <cstdlib>
 
 #include "vn_common.h"
 
@@ -53,6 +54,10 @@ constexpr int RW = 32;      // rows per tile
 constexpr int UBK = 32;     // units per block
 constexpr int NUB = 8;      // unit blocks per LSTM (H = 256)
 constexpr uint32_t kSpinLimit = 1u << 22;   // ~0.3 s per wait at s_sleep 2
+// one 256-B line per group counter: the counters of all groups in one line put
+// every poll and add of the launch on one memory channel (measured: with two
+// blocks per CU every memory section of a step ran 3-6x slower)
+constexpr int CSTRIDE = 64;
 
 // gate / cell nonlinearities on the hardware exp and reciprocal (|err| <= ~4e-7,
 // the collector's f32 policy step uses the same: csrc/voxnav_policy_f32.hip)
@@ -122,10 +127,11 @@ struct RowsFwd {
     float *hprev;            // [2][L][B][H]  the h_{t-1} each step used
     float *cprev, *cnew;     // [2][L][B][H]
     float *act;              // [2][L][B][4H] i, f, g, o
-    uint32_t *cnt;           // [2 * NT] group counters (zeroed per call)
+    uint32_t *cnt;           // [2 * NT * CSTRIDE] group counters, a line each (zeroed per call)
     int32_t *err;
     int64_t n_env;
     int L, B, NT;
+    uint32_t *diag;          // diagnostics (NULL): placement + per-step clocks
 };
 
 template <int D, int H>
@@ -169,7 +175,7 @@ __global__ __launch_bounds__(256, 1) void lstm_rows_fwd_kernel(RowsFwd a) {
 
     const __amdgpu_buffer_rsrc_t hrs =
         __builtin_amdgcn_make_buffer_rsrc(a.hout, 0, (int)((size_t)2 * L * B * H * 4), 0x00020000);
-    uint32_t *cnt = a.cnt + g;
+    uint32_t *cnt = a.cnt + (size_t)g * CSTRIDE;
 
     // x rows of a step: RW x D floats, float4 f -> (row f / (D/4), col 4 (f % (D/4)))
     constexpr int XF = RW * D / 4, XPT = (XF + 255) / 256;
@@ -199,9 +205,12 @@ __global__ __launch_bounds__(256, 1) void lstm_rows_fwd_kernel(RowsFwd a) {
     __syncthreads();
 
     __shared__ uint8_t stf[RW];       // the tile's sequence-start flags of the step
+    // loaded a step ahead (a load consumed in the same step stalled the x part)
+    uint8_t st_next = (tid < RW && row0 + tid < B) ? 1 : 0;
     for (int t = 0; t < L; ++t) {
         const int xb = t & 1;
-        if (tid < RW) stf[tid] = (row0 + tid < B && (t == 0 || a.start[(size_t)t * B + row0 + tid])) ? 1 : 0;
+        if (tid < RW) stf[tid] = st_next;
+        if (tid < RW && t + 1 < L) st_next = (row0 + tid < B && a.start[(size_t)(t + 1) * B + row0 + tid]) ? 1 : 0;
         float4 xn[XPT];
         if (t + 1 < L) load_x(t + 1, xn);
         // the x part of the product (needs nothing from the group)
@@ -311,6 +320,260 @@ __global__ __launch_bounds__(256, 1) void lstm_rows_fwd_kernel(RowsFwd a) {
     }
 }
 
+// ---------------------------------------------------------------------------
+// Two blocks per CU (the default).  The same recurrence with HALF the units
+// per block (16: 64 gate columns) on v_mfma_f32_16x16x4_f32, so the grid is
+// 2 x 16 x R/32 = 512 blocks, two resident per CU.  A group (LSTM, row tile)
+// is now 16 blocks; the two blocks sharing a CU are different groups (the
+// grid's second half takes the other LSTM of the same row tile), i.e. two
+// independent recurrences, so one's MFMAs run while the other's hand-off is
+// in flight -- in the one-block-per-CU layout each SIMD held one wave and
+// idled for every hand-off.  Same payloads, same protocol; a group's counter
+// counts 16 adds per step.
+// ---------------------------------------------------------------------------
+constexpr int UB2 = 16;     // units per block
+constexpr int NUB2 = 16;    // unit blocks per LSTM
+
+typedef __attribute__((ext_vector_type(4))) float f32x4_t;
+
+__device__ __forceinline__ f32x4_t zero4() { return f32x4_t{0.0f, 0.0f, 0.0f, 0.0f}; }
+__device__ __forceinline__ float2 operator+(float2 a, float2 b) { return make_float2(a.x + b.x, a.y + b.y); }
+__device__ __forceinline__ float2 operator*(float2 a, float2 b) { return make_float2(a.x * b.x, a.y * b.y); }
+__device__ __forceinline__ float2 f2(float a) { return make_float2(a, a); }
+
+__device__ __forceinline__ void st_sc1_b64(__amdgpu_buffer_rsrc_t rs, uint32_t off, float2 v) {
+    __attribute__((ext_vector_type(2))) float w = {v.x, v.y};
+    __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(__attribute__((ext_vector_type(2))) uint32_t, w), rs, off,
+                                          0, 16);
+}
+__device__ __forceinline__ float2 ld_sc1_b64(__amdgpu_buffer_rsrc_t rs, uint32_t off) {
+    const auto u = __builtin_amdgcn_raw_buffer_load_b64(rs, off, 0, 16);
+    const auto v = __builtin_bit_cast(__attribute__((ext_vector_type(2))) float, u);
+    return make_float2(v[0], v[1]);
+}
+
+// block -> (unit block, group): the first half of the grid takes unit blocks
+// 0..7 of every group, the second half 8..15 with the LSTMs swapped, so block
+// b and block b + grid/2 (which the dispatcher places on the same CU,
+// scripts/rows_diag.py) belong to different recurrences.  (They still run in
+// phase: a plain order and a delayed start of LSTM 1 measured the same.)
+// Blocks of one group share blockIdx mod 8 (one XCD's L2 carries the group's
+// hand-offs) when NT % 8 == 0.
+__device__ __forceinline__ void rows2_map(int NT, int &ub, int &g) {
+    const int G = 2 * NT, half = (NUB2 / 2) * G;
+    int b = (int)blockIdx.x;
+    const bool second = b >= half;
+    if (second) b -= half;
+    ub = b / G + (second ? NUB2 / 2 : 0);
+    g = b - (b / G) * G;
+    if (second) g = (g + NT) % G;
+}
+
+template <int D, int H>
+__global__ __launch_bounds__(256, 2) void lstm_rows_fwd2_kernel(RowsFwd a) {
+    constexpr int NCX = D / 16, NCH = H / 16, NC = NCX + NCH;   // 16-deep k chunks
+    constexpr int XP = D + 4, HP = H + 4, GP = UB2 + 4;
+    static_assert(D % 16 == 0 && H == NUB2 * UB2, "shape");
+    __shared__ __attribute__((aligned(16))) float xs[2][RW][XP];
+    __shared__ __attribute__((aligned(16))) float hsl[RW][HP];
+    __shared__ __attribute__((aligned(16))) float gts[4][RW][GP];
+    __shared__ uint8_t stf[RW];
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);   // this wave's gate
+    const int q = lane >> 4, ci = lane & 15;
+    int ub, g;
+    rows2_map(a.NT, ub, g);
+    if (a.diag && tid == 0) {
+        a.diag[2 * blockIdx.x] = __builtin_amdgcn_s_getreg((31 << 11) | 4);        // HW_ID
+        a.diag[2 * blockIdx.x + 1] = __builtin_amdgcn_s_getreg((31 << 11) | 20);   // XCC_ID
+    }
+    const int l = g / a.NT, rt = g - l * a.NT;
+    const int row0 = rt * RW, u0 = ub * UB2;
+    const int B = a.B, L = a.L;
+
+    // resident weights: B operand of gate wv, unit u0 + ci; chunk c, step jj
+    // takes k = 16 c + 4 q + jj (the A reads use the same k order)
+    float4 wr[NC];
+    {
+        const float *wi = a.w_ih + ((size_t)l * 4 * H + (size_t)wv * H + u0 + ci) * D;
+        const float *wh = a.w_hh + ((size_t)l * 4 * H + (size_t)wv * H + u0 + ci) * H;
+#pragma unroll
+        for (int c = 0; c < NC; ++c)
+            wr[c] = c < NCX ? *reinterpret_cast<const float4 *>(wi + 16 * c + 4 * q)
+                            : *reinterpret_cast<const float4 *>(wh + 16 * (c - NCX) + 4 * q);
+    }
+    // epilogue mapping: row er of the tile, units u0 + 2 eq, + 1
+    const int er = tid >> 3, eq = tid & 7;
+    const int erow = row0 + er;
+    const bool elive = erow < B;
+    const int eu = u0 + 2 * eq;
+    float2 bs[4];
+#pragma unroll
+    for (int gq = 0; gq < 4; ++gq) bs[gq] = *reinterpret_cast<const float2 *>(a.bias + (size_t)l * 4 * H + gq * H + eu);
+    float2 cc = f2(0.0f);
+
+    const __amdgpu_buffer_rsrc_t hrs =
+        __builtin_amdgcn_make_buffer_rsrc(a.hout, 0, (int)((size_t)2 * L * B * H * 4), 0x00020000);
+    uint32_t *cnt = a.cnt + (size_t)g * CSTRIDE;
+
+    constexpr int XF = RW * D / 4, XPT = (XF + 255) / 256;
+    auto load_x = [&](int t, float4 *r) {
+#pragma unroll
+        for (int i = 0; i < XPT; ++i) {
+            const int f = tid + 256 * i;
+            const int rr = f / (D / 4), c4 = f - rr * (D / 4);
+            r[i] = (f < XF && row0 + rr < B)
+                       ? *reinterpret_cast<const float4 *>(a.x + ((size_t)t * B + row0 + rr) * D + 4 * c4)
+                       : f4(0.0f);
+        }
+    };
+    auto store_x = [&](int buf, const float4 *r) {
+#pragma unroll
+        for (int i = 0; i < XPT; ++i) {
+            const int f = tid + 256 * i;
+            const int rr = f / (D / 4), c4 = f - rr * (D / 4);
+            if (f < XF) *reinterpret_cast<float4 *>(&xs[buf][rr][4 * c4]) = r[i];
+        }
+    };
+    {
+        float4 r[XPT];
+        load_x(0, r);
+        store_x(0, r);
+    }
+    __syncthreads();
+
+#define VN_DMARK(k_)                                                                          \
+    if (a.diag && tid == 0)                                                                   \
+        a.diag[2 * gridDim.x + ((size_t)blockIdx.x * L + t) * 8 + (k_)] = (uint32_t)__builtin_amdgcn_s_memrealtime();
+    // the tile's sequence-start flags, loaded a step ahead (a load consumed in
+    // the same step stalled the x part behind its round trip)
+    uint8_t st_next = (tid < RW && row0 + tid < B) ? 1 : 0;
+    for (int t = 0; t < L; ++t) {
+        const int xb = t & 1;
+        VN_DMARK(0);
+        if (tid < RW) stf[tid] = st_next;
+        if (tid < RW && t + 1 < L) st_next = (row0 + tid < B && a.start[(size_t)(t + 1) * B + row0 + tid]) ? 1 : 0;
+        float4 xn[XPT];
+        if (t + 1 < L) load_x(t + 1, xn);
+        // the x part (needs nothing from the group): rows ci and 16 + ci
+        f32x4_t acc0 = zero4(), acc1 = zero4();
+#pragma unroll
+        for (int c = 0; c < NCX; ++c) {
+            const float4 a0 = *reinterpret_cast<const float4 *>(&xs[xb][ci][16 * c + 4 * q]);
+            const float4 a1 = *reinterpret_cast<const float4 *>(&xs[xb][16 + ci][16 * c + 4 * q]);
+            acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a0.x, wr[c].x, acc0, 0, 0, 0);
+            acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a1.x, wr[c].x, acc1, 0, 0, 0);
+            acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a0.y, wr[c].y, acc0, 0, 0, 0);
+            acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a1.y, wr[c].y, acc1, 0, 0, 0);
+            acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a0.z, wr[c].z, acc0, 0, 0, 0);
+            acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a1.z, wr[c].z, acc1, 0, 0, 0);
+            acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a0.w, wr[c].w, acc0, 0, 0, 0);
+            acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a1.w, wr[c].w, acc1, 0, 0, 0);
+        }
+        VN_DMARK(1);
+        if (t > 0) {
+            if (tid == 0) wait_ge(cnt, (uint32_t)(NUB2 * t), a.err);
+            __syncthreads();
+        }
+        VN_DMARK(2);
+        float4 hv[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            const int f = tid + 256 * i;
+            const int rr = f >> 6, c4 = f & 63;
+            const int row = min(row0 + rr, B - 1);
+            hv[i] = t > 0 ? ld_sc1(hrs, (uint32_t)((((size_t)l * L + (t - 1)) * B + row) * H + 4 * c4) * 4u)
+                          : f4(0.0f);
+        }
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            const int f = tid + 256 * i;
+            *reinterpret_cast<float4 *>(&hsl[f >> 6][4 * (f & 63)]) = hv[i];
+        }
+        __syncthreads();
+        VN_DMARK(3);
+#pragma unroll
+        for (int i = 0; i < RW / 4; ++i) {
+            const int rr = (tid >> 6) + 4 * i, c4 = tid & 63;
+            const int row = row0 + rr;
+            if (stf[rr]) {
+                const size_t o = (size_t)t * B + row;
+                const float4 sv = *reinterpret_cast<const float4 *>(
+                    a.h_store + (((size_t)t * 2 + l) * a.n_env + a.env[o]) * H + 4 * c4);
+                *reinterpret_cast<float4 *>(&hsl[rr][4 * c4]) = sv * f4(a.keep[o]);
+            } else if (row >= B) {
+                *reinterpret_cast<float4 *>(&hsl[rr][4 * c4]) = f4(0.0f);
+            }
+        }
+        __syncthreads();
+#pragma unroll
+        for (int c = 0; c < NCH; ++c) {
+            const float4 a0 = *reinterpret_cast<const float4 *>(&hsl[ci][16 * c + 4 * q]);
+            const float4 a1 = *reinterpret_cast<const float4 *>(&hsl[16 + ci][16 * c + 4 * q]);
+            const float4 w = wr[NCX + c];
+            acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a0.x, w.x, acc0, 0, 0, 0);
+            acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a1.x, w.x, acc1, 0, 0, 0);
+            acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a0.y, w.y, acc0, 0, 0, 0);
+            acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a1.y, w.y, acc1, 0, 0, 0);
+            acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a0.z, w.z, acc0, 0, 0, 0);
+            acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a1.z, w.z, acc1, 0, 0, 0);
+            acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a0.w, w.w, acc0, 0, 0, 0);
+            acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a1.w, w.w, acc1, 0, 0, 0);
+        }
+        if (t + 1 < L) store_x(xb ^ 1, xn);
+        // gate tiles -> LDS: register r = row 4 q + r (+ 16 for acc1), unit ci
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            gts[wv][4 * q + r][ci] = acc0[r];
+            gts[wv][16 + 4 * q + r][ci] = acc1[r];
+        }
+        __syncthreads();
+        VN_DMARK(4);
+        if (elive) {
+            const size_t o = (size_t)t * B + erow;
+            float2 pre[4];
+#pragma unroll
+            for (int gq = 0; gq < 4; ++gq) pre[gq] = *reinterpret_cast<const float2 *>(&gts[gq][er][2 * eq]) + bs[gq];
+            float2 cp = cc;
+            if (stf[er]) {
+                const float k = a.keep[o];
+                cp = *reinterpret_cast<const float2 *>(a.c_store + (((size_t)t * 2 + l) * a.n_env + a.env[o]) * H + eu) *
+                     f2(k);
+            }
+            float2 ig, fg, gg, og, cn, hn;
+#define VN_CELL2(c)                                       \
+    ig.c = sigm(pre[0].c);                                \
+    fg.c = sigm(pre[1].c);                                \
+    gg.c = tanh_fast(pre[2].c);                           \
+    og.c = sigm(pre[3].c);                                \
+    {                                                     \
+        const float fc_ = fg.c * cp.c, ig_ = ig.c * gg.c; \
+        cn.c = fc_ + ig_;                                 \
+    }                                                     \
+    hn.c = og.c * tanh_fast(cn.c);
+            VN_CELL2(x) VN_CELL2(y)
+#undef VN_CELL2
+            cc = cn;
+            const size_t so = (((size_t)l * L + t) * B + erow) * H + eu;
+            st_sc1_b64(hrs, (uint32_t)(so * 4u), hn);      // the payload first
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            *reinterpret_cast<float2 *>(a.cnew + so) = cn;
+            *reinterpret_cast<float2 *>(a.cprev + so) = cp;
+            *reinterpret_cast<float2 *>(a.hprev + so) = *reinterpret_cast<const float2 *>(&hsl[er][eu]);
+            float *pa = a.act + (((size_t)l * L + t) * B + erow) * 4 * H + eu;
+            *reinterpret_cast<float2 *>(pa) = ig;
+            *reinterpret_cast<float2 *>(pa + H) = fg;
+            *reinterpret_cast<float2 *>(pa + 2 * H) = gg;
+            *reinterpret_cast<float2 *>(pa + 3 * H) = og;
+        }
+        VN_DMARK(5);
+        __syncthreads();
+        if (tid == 0) __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        VN_DMARK(6);
+    }
+#undef VN_DMARK
+}
+
 struct RowsBwd {
     const float *dh_out;     // [2][L][B][H]
     const float *w_hh;       // [2][4H][H]
@@ -323,7 +586,7 @@ struct RowsBwd {
     float *part;             // [2 slots][2][NT][NUB][RW][H] partial dh
     float *wpart;            // [NT][2][4H][H + D] per-row-tile [dW_hh | dW_ih]
     float *bpart;            // [NT][2][4H] per-row-tile db
-    uint32_t *cnt;           // [2 * NT]
+    uint32_t *cnt;           // [2 * NT * CSTRIDE]
     int32_t *err;
     int L, B, NT;
 };
@@ -387,7 +650,7 @@ __global__ __launch_bounds__(256, 1) void lstm_rows_bwd_kernel(RowsBwd a) {
     const size_t slot_f = (size_t)2 * a.NT * NUB * RW * H;     // floats per slot
     const __amdgpu_buffer_rsrc_t prs =
         __builtin_amdgcn_make_buffer_rsrc(a.part, 0, (int)(2 * slot_f * 4), 0x00020000);
-    uint32_t *cnt = a.cnt + g;
+    uint32_t *cnt = a.cnt + (size_t)g * CSTRIDE;
     auto pofs = [&](int slot, int ubb, int row, int unit) -> uint32_t {   // byte offset in part
         return (uint32_t)(((size_t)slot * slot_f + ((((size_t)l * a.NT + rt) * NUB + ubb) * RW + row) * H + unit) * 4u);
     };
@@ -544,6 +807,224 @@ __global__ __launch_bounds__(256, 1) void lstm_rows_bwd_kernel(RowsBwd a) {
     }
 }
 
+// Backward, two blocks per CU (block = 16 units: 64 gate columns; the grid
+// mapping of the forward).  The partial dh_{t-1} [32 rows][256 units] of a
+// block is dG_t[:, its 64 gate columns] @ W_hh[those rows] on 16x16x4 tiles
+// (wave w: units 64 w .. + 63, W_hh slice resident in 64 registers), staged
+// through LDS 16 rows at a time; the weight gradients of gate wv's 16 rows
+// over the 336 [h | x] columns are 21 16x16 accumulators.  Row order of the
+// weight-gradient products: k-step s, lane group q takes row 4 q + (s & 3) +
+// 16 (s >> 2) (the two rows a 32-lane LDS read touches sit 16 banks apart).
+template <int D, int H>
+__global__ __launch_bounds__(256, 2) void lstm_rows_bwd2_kernel(RowsBwd a) {
+    constexpr int GC = 4 * UB2;                  // this block's gate columns (64)
+    constexpr int DP = GC + 4, PP = H + 4, XP = D + 4;
+    constexpr int NHT = H / 16, NXT = D / 16;    // weight-gradient column tiles (16 + 5)
+    static_assert(H == NUB2 * UB2 && D % 16 == 0 && H == 256 && D / 4 <= 64, "shape: a row per wave load");
+    __shared__ __attribute__((aligned(16))) float dgs[RW][DP];
+    __shared__ __attribute__((aligned(16))) float pst[RW / 2][PP];
+    __shared__ __attribute__((aligned(16))) float hsl[RW][PP];
+    __shared__ __attribute__((aligned(16))) float xsl[RW][XP];
+    __shared__ uint8_t stf[RW];
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);   // partial: units 64 wv .. + 63; dW: gate wv
+    const int q = lane >> 4, ci = lane & 15;
+    int ub, g;
+    rows2_map(a.NT, ub, g);
+    const int l = g / a.NT, rt = g - l * a.NT;
+    const int row0 = rt * RW, u0 = ub * UB2;
+    const int B = a.B, L = a.L;
+
+    // resident W_hh slice: B operand [k = gate c * 16 + unit16][n = 64 wv + 16 j + ci],
+    // chunk c = the gate, step jj: k = 16 c + 4 q + jj
+    float4 wb[4][4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+            float v[4];
+#pragma unroll
+            for (int jj = 0; jj < 4; ++jj) {
+                const int grow = c * H + u0 + 4 * q + jj;
+                v[jj] = a.w_hh[((size_t)l * 4 * H + grow) * H + 64 * wv + 16 * j + ci];
+            }
+            wb[j][c] = make_float4(v[0], v[1], v[2], v[3]);
+        }
+    const int er = tid >> 3, eq = tid & 7;
+    const int erow = row0 + er;
+    const bool elive = erow < B;
+    const int eu = u0 + 2 * eq;
+    float2 dc = f2(0.0f);
+    float2 dbs[4] = {f2(0.0f), f2(0.0f), f2(0.0f), f2(0.0f)};
+    f32x4_t wacc[NHT + NXT];
+#pragma unroll
+    for (int j = 0; j < NHT + NXT; ++j) wacc[j] = zero4();
+    const size_t slot_f = (size_t)2 * a.NT * NUB2 * RW * H;     // floats per slot
+    const __amdgpu_buffer_rsrc_t prs =
+        __builtin_amdgcn_make_buffer_rsrc(a.part, 0, (int)(2 * slot_f * 4), 0x00020000);
+    uint32_t *cnt = a.cnt + (size_t)g * CSTRIDE;
+    auto pofs = [&](int slot, int ubb, int row, int unit) -> uint32_t {   // byte offset in part
+        return (uint32_t)(((size_t)slot * slot_f + ((((size_t)l * a.NT + rt) * NUB2 + ubb) * RW + row) * H + unit) * 4u);
+    };
+
+    for (int s = 0; s < L; ++s) {
+        const int t = L - 1 - s;
+        const bool st_ld = !elive || t == 0 || a.start[(size_t)t * B + erow];
+        // the step's h_{t-1} and x_t rows (the weight gradients' B operands),
+        // global -> LDS, issued before the hand-off wait
+#pragma unroll
+        for (int i = 0; i < RW / 4; ++i) {
+            const int rr = (RW / 4) * wv + i;
+            const int row = min(row0 + rr, B - 1);
+            __builtin_amdgcn_global_load_lds(
+                (const __attribute__((address_space(1))) void *)(a.hprev + (((size_t)l * L + t) * B + row) * H + 4 * lane),
+                (__attribute__((address_space(3))) void *)&hsl[rr][0], 16, 0, 0);
+            if (lane < D / 4)
+                __builtin_amdgcn_global_load_lds(
+                    (const __attribute__((address_space(1))) void *)(a.x + ((size_t)t * B + row) * D + 4 * lane),
+                    (__attribute__((address_space(3))) void *)&xsl[rr][0], 16, 0, 0);
+        }
+        if (s > 0) {
+            if (tid == 0) wait_ge(cnt, (uint32_t)(NUB2 * s), a.err);
+            __syncthreads();
+        }
+        float2 dG2[4] = {f2(0.0f), f2(0.0f), f2(0.0f), f2(0.0f)};
+        bool st = true;
+        if (elive) {
+            st = st_ld;
+            float2 dhr = f2(0.0f);
+            if (s > 0) {
+#pragma unroll
+                for (int k = 0; k < NUB2; ++k) dhr = dhr + ld_sc1_b64(prs, pofs((t + 1) & 1, k, er, eu));
+            }
+            const size_t so = (((size_t)l * L + t) * B + erow) * H + eu;
+            const float2 dh = *reinterpret_cast<const float2 *>(a.dh_out + so) + dhr;
+            const float *pa = a.act + (((size_t)l * L + t) * B + erow) * 4 * H + eu;
+            const float2 ig = *reinterpret_cast<const float2 *>(pa), fg = *reinterpret_cast<const float2 *>(pa + H);
+            const float2 gg = *reinterpret_cast<const float2 *>(pa + 2 * H);
+            const float2 og = *reinterpret_cast<const float2 *>(pa + 3 * H);
+            const float2 cp = *reinterpret_cast<const float2 *>(a.cprev + so);
+            const float2 cn = *reinterpret_cast<const float2 *>(a.cnew + so);
+#define VN_CELLB2(c)                                                  \
+    {                                                                 \
+        const float tc = tanh_fast(cn.c);                             \
+        const float dtc = dh.c * og.c;                                \
+        const float dcc = dc.c + dtc * (1.0f - tc * tc);              \
+        dG2[0].c = dcc * gg.c * (ig.c * (1.0f - ig.c));               \
+        dG2[1].c = dcc * cp.c * (fg.c * (1.0f - fg.c));               \
+        dG2[2].c = dcc * ig.c * (1.0f - gg.c * gg.c);                 \
+        dG2[3].c = dh.c * tc * (og.c * (1.0f - og.c));                \
+        dc.c = dcc * fg.c;                                            \
+    }
+            VN_CELLB2(x) VN_CELLB2(y)
+#undef VN_CELLB2
+            if (st) dc = f2(0.0f);
+            if (a.dG) {
+                float *pg = a.dG + (((size_t)l * L + t) * B + erow) * 4 * H + eu;
+#pragma unroll
+                for (int gq = 0; gq < 4; ++gq) *reinterpret_cast<float2 *>(pg + gq * H) = dG2[gq];
+            }
+#pragma unroll
+            for (int gq = 0; gq < 4; ++gq) dbs[gq] = dbs[gq] + dG2[gq];
+        }
+#pragma unroll
+        for (int gq = 0; gq < 4; ++gq) *reinterpret_cast<float2 *>(&dgs[er][gq * UB2 + 2 * eq]) = dG2[gq];
+        if (eq == 0) stf[er] = st ? 1 : 0;
+        __syncthreads();
+        if (t > 0) {
+            f32x4_t acc[2][4];
+#pragma unroll
+            for (int h = 0; h < 2; ++h)
+#pragma unroll
+                for (int j = 0; j < 4; ++j) acc[h][j] = zero4();
+#pragma unroll
+            for (int c = 0; c < 4; ++c) {
+                const float4 a0 = *reinterpret_cast<const float4 *>(&dgs[ci][16 * c + 4 * q]);
+                const float4 a1 = *reinterpret_cast<const float4 *>(&dgs[16 + ci][16 * c + 4 * q]);
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    acc[0][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a0.x, wb[j][c].x, acc[0][j], 0, 0, 0);
+                    acc[1][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a1.x, wb[j][c].x, acc[1][j], 0, 0, 0);
+                }
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    acc[0][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a0.y, wb[j][c].y, acc[0][j], 0, 0, 0);
+                    acc[1][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a1.y, wb[j][c].y, acc[1][j], 0, 0, 0);
+                }
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    acc[0][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a0.z, wb[j][c].z, acc[0][j], 0, 0, 0);
+                    acc[1][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a1.z, wb[j][c].z, acc[1][j], 0, 0, 0);
+                }
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    acc[0][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a0.w, wb[j][c].w, acc[0][j], 0, 0, 0);
+                    acc[1][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a1.w, wb[j][c].w, acc[1][j], 0, 0, 0);
+                }
+            }
+            // the partial [RW][H], 16 rows at a time through LDS, 16-B sc1
+            // stores; rows whose step t starts a sequence pass no gradient back
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const bool cut = stf[16 * h + 4 * q + r] != 0;
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) pst[4 * q + r][64 * wv + 16 * j + ci] = cut ? 0.0f : acc[h][j][r];
+                }
+                __syncthreads();
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    const int f = tid + 256 * i;
+                    const int rr = f >> 6, c4 = f & 63;
+                    st_sc1(prs, pofs(t & 1, ub, 16 * h + rr, 4 * c4), *reinterpret_cast<const float4 *>(&pst[rr][4 * c4]));
+                }
+                if (h == 0) __syncthreads();
+            }
+            publish(cnt);
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        // weight gradients of gate wv's 16 rows: A = dG^T [unit][row], B = the
+        // h_{t-1} | x_t rows [row][col], K = the 32 rows
+#pragma unroll
+        for (int s4 = 0; s4 < RW / 4; ++s4) {
+            const int r = 4 * q + (s4 & 3) + 16 * (s4 >> 2);
+            const float av = dgs[r][wv * UB2 + ci];
+#pragma unroll
+            for (int j = 0; j < NHT; ++j)
+                wacc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, hsl[r][16 * j + ci], wacc[j], 0, 0, 0);
+#pragma unroll
+            for (int j = 0; j < NXT; ++j)
+                wacc[NHT + j] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, xsl[r][16 * j + ci], wacc[NHT + j], 0, 0, 0);
+        }
+        __syncthreads();
+        if (t == 0) break;
+    }
+    // per-row-tile weight-gradient partials: register r of tile j = gate row
+    // u0 + 4 q + r of gate wv, column 16 j + ci
+    float *wp = a.wpart + (((size_t)rt * 2 + l) * 4 * H) * (H + D);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        const int grow = wv * H + u0 + 4 * q + r;
+        float *prow = wp + (size_t)grow * (H + D);
+#pragma unroll
+        for (int j = 0; j < NHT; ++j) prow[16 * j + ci] = wacc[j][r];
+#pragma unroll
+        for (int j = 0; j < NXT; ++j) prow[H + 16 * j + ci] = wacc[NHT + j][r];
+    }
+    // db: the 32 rows' sums, reduced through LDS (dgs reused)
+    __syncthreads();
+#pragma unroll
+    for (int gq = 0; gq < 4; ++gq) *reinterpret_cast<float2 *>(&dgs[er][gq * UB2 + 2 * eq]) = dbs[gq];
+    __syncthreads();
+    if (tid < GC) {
+        float sum = 0.0f;
+        for (int r = 0; r < RW; ++r) sum += dgs[r][tid];
+        a.bpart[((size_t)rt * 2 + l) * 4 * H + (tid >> 4) * H + u0 + (tid & 15)] = sum;
+    }
+}
+
 // sum over row tiles (in order) of the [2][4H][H + D] weight-gradient partials,
 // written straight into the two parameters' layouts: dW_hh [2][4H][H] and
 // dW_ih [2][4H][D]
@@ -573,16 +1054,44 @@ __global__ void rows_bsum_kernel(const float *__restrict__ part, int nt, int64_t
 
 int rows_supported(int D, int H) { return D == 80 && H == 256; }
 
-int rows_grid_ok(int B, int NT, int *grid) {
-    *grid = 2 * NUB * NT;
+// which layout a direction runs: the 16-unit blocks (v2) whenever their grid
+// is at most one block per CU (measured 6.8 vs 9.4 us per forward step at 256
+// rows); at two per CU the two blocks of a CU run their steps in phase (their
+// matrix work shares the SIMDs, an offset start decays to alignment within ~8
+// steps), so the forward keeps the 32-unit blocks there (9.4 vs 9.9 us) and the
+// backward the 16-unit ones (14.8 vs 15.4 us).  VOXNAV_ROWS_V1=1 / _V2=1 force
+// one layout (A/B and tests; read per call).
+bool rows_v2(int NT, bool fwd) {
+    const char *e1 = getenv("VOXNAV_ROWS_V1");
+    if (e1 && e1[0] == '1') return false;
+    const char *e2 = getenv("VOXNAV_ROWS_V2");
+    if (e2 && e2[0] == '1') return true;
+    int dev = 0, ncu = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+        return false;
+    return 2 * NUB2 * NT <= ncu || !fwd;
+}
+
+uint32_t *g_rows_diag = nullptr;   // vn_lstm_rows_set_diag (diagnostics)
+
+int rows_grid_ok(int B, int NT, bool v2, int *grid) {
+    *grid = 2 * (v2 ? NUB2 : NUB) * NT;
     if (B < 1 || NT < 1 || B > NT * RW) return 0;
     int dev = 0, ncu = 0, per_fwd = 0, per_bwd = 0;
     if (hipGetDevice(&dev) != hipSuccess) return 0;
     if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_fwd, lstm_rows_fwd_kernel<80, 256>, 256, 0) != hipSuccess)
-        return 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_bwd, lstm_rows_bwd_kernel<80, 256>, 256, 0) != hipSuccess)
-        return 0;
+    if (v2) {
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_fwd, lstm_rows_fwd2_kernel<80, 256>, 256, 0) != hipSuccess)
+            return 0;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_bwd, lstm_rows_bwd2_kernel<80, 256>, 256, 0) != hipSuccess)
+            return 0;
+    } else {
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_fwd, lstm_rows_fwd_kernel<80, 256>, 256, 0) != hipSuccess)
+            return 0;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_bwd, lstm_rows_bwd_kernel<80, 256>, 256, 0) != hipSuccess)
+            return 0;
+    }
     const int cap = ncu * (per_fwd < per_bwd ? per_fwd : per_bwd);
     return *grid <= cap;
 }
@@ -594,14 +1103,23 @@ extern "C" {
 int vn_lstm_rows_supported(int32_t D, int32_t H, int32_t B) {
     if (!rows_supported(D, H)) return 0;
     int grid = 0;
-    return rows_grid_ok(B, (B + RW - 1) / RW, &grid);
+    const int NT = (B + RW - 1) / RW;
+    return rows_grid_ok(B, NT, rows_v2(NT, true), &grid) && rows_grid_ok(B, NT, rows_v2(NT, false), &grid);
+}
+
+// diagnostics: the forward (two-per-CU layout) records each block's HW_ID /
+// XCC_ID in diag[2 b], diag[2 b + 1] and the 100-MHz clock at 7 points of
+// its step t in diag[2 grid + (b L + t) 8 + k]; NULL turns it off.  Not in voxnav.h.
+int vn_lstm_rows_set_diag(void *diag) {
+    g_rows_diag = (uint32_t *)diag;
+    return VN_OK;
 }
 
 int vn_lstm_rows_part_floats(int32_t B, int64_t *floats) {
     if (!floats || B < 1) return fail(VN_ERR_INVALID, "bad argument");
     const int NT = (B + RW - 1) / RW;
     // the two partial-dh slots, the per-row-tile [dW_hh | dW_ih] and db partials
-    *floats = (int64_t)2 * 2 * NT * NUB * RW * 256 + (int64_t)NT * 2 * 1024 * (256 + 80) + (int64_t)NT * 2 * 1024;
+    *floats = (int64_t)2 * 2 * NT * NUB2 * RW * 256 + (int64_t)NT * 2 * 1024 * (256 + 80) + (int64_t)NT * 2 * 1024;
     return VN_OK;
 }
 
@@ -615,15 +1133,17 @@ int vn_lstm_rows_fwd(const float *x, int32_t D, const float *w_ih, const float *
     if (!rows_supported(D, H)) return fail(VN_ERR_INVALID, "row-layout LSTM: D 80 and H 256 only (got %d, %d)", D, H);
     if (L < 1) return fail(VN_ERR_INVALID, "L < 1");
     const int NT = (B + RW - 1) / RW;
+    const bool v2 = rows_v2(NT, true);
     int grid = 0;
-    if (!rows_grid_ok(B, NT, &grid))
+    if (!rows_grid_ok(B, NT, v2, &grid))
         return fail(VN_ERR_INVALID, "row-layout LSTM: %d blocks are not co-resident (B = %d)", grid, B);
     if ((size_t)2 * L * B * H * 4 >= (1ull << 31)) return fail(VN_ERR_INVALID, "row-layout LSTM: hout over 2 GB");
     const hipStream_t st = (hipStream_t)stream;
-    VN_HIP(hipMemsetAsync(cnt, 0, (size_t)2 * NT * sizeof(uint32_t), st));
+    VN_HIP(hipMemsetAsync(cnt, 0, (size_t)2 * NT * CSTRIDE * sizeof(uint32_t), st));
     RowsFwd a{x, w_ih, w_hh, bias, h_store, c_store, env, start, keep, hout, hprev, cprev, cnew, act, cnt, err,
-              n_env, L, B, NT};
-    hipLaunchKernelGGL((lstm_rows_fwd_kernel<80, 256>), dim3((unsigned)grid), dim3(256), 0, st, a);
+              n_env, L, B, NT, g_rows_diag};
+    if (v2) hipLaunchKernelGGL((lstm_rows_fwd2_kernel<80, 256>), dim3((unsigned)grid), dim3(256), 0, st, a);
+    else hipLaunchKernelGGL((lstm_rows_fwd_kernel<80, 256>), dim3((unsigned)grid), dim3(256), 0, st, a);
     VN_HIP(hipGetLastError());
     return VN_OK;
 }
@@ -638,17 +1158,19 @@ int vn_lstm_rows_bwd(const float *dh_out, const float *w_hh, const float *act, c
     if (!rows_supported(80, H)) return fail(VN_ERR_INVALID, "row-layout LSTM: H 256 only (got %d)", H);
     if (L < 1) return fail(VN_ERR_INVALID, "L < 1");
     const int NT = (B + RW - 1) / RW;
+    const bool v2 = rows_v2(NT, false);
     int grid = 0;
-    if (!rows_grid_ok(B, NT, &grid))
+    if (!rows_grid_ok(B, NT, v2, &grid))
         return fail(VN_ERR_INVALID, "row-layout LSTM: %d blocks are not co-resident (B = %d)", grid, B);
     const hipStream_t st = (hipStream_t)stream;
     constexpr int D = 80;
-    const size_t slot_f = (size_t)2 * NT * NUB * RW * H;
+    const size_t slot_f = (size_t)2 * NT * (v2 ? NUB2 : NUB) * RW * H;
     float *wpart = part + 2 * slot_f;
     float *bpart = wpart + (size_t)NT * 2 * 4 * H * (H + D);
-    VN_HIP(hipMemsetAsync(cnt, 0, (size_t)2 * NT * sizeof(uint32_t), st));
+    VN_HIP(hipMemsetAsync(cnt, 0, (size_t)2 * NT * CSTRIDE * sizeof(uint32_t), st));
     RowsBwd a{dh_out, w_hh, act, cprev, cnew, hprev, x, start, dG, part, wpart, bpart, cnt, err, L, B, NT};
-    hipLaunchKernelGGL((lstm_rows_bwd_kernel<80, 256>), dim3((unsigned)grid), dim3(256), 0, st, a);
+    if (v2) hipLaunchKernelGGL((lstm_rows_bwd2_kernel<80, 256>), dim3((unsigned)grid), dim3(256), 0, st, a);
+    else hipLaunchKernelGGL((lstm_rows_bwd_kernel<80, 256>), dim3((unsigned)grid), dim3(256), 0, st, a);
     const int64_t pw = (int64_t)2 * 4 * H * (H + D), pb = (int64_t)2 * 4 * H;
     hipLaunchKernelGGL(rows_wsum_kernel, dim3((unsigned)((pw + 255) / 256)), dim3(256), 0, st, wpart, NT, 4 * H, H, D,
                        dw_hh, dw_ih);

@@ -145,7 +145,7 @@ class _DualLSTMRows(torch.autograd.Function):
         hout = torch.empty((2, L, B, H), dtype=torch.float32, device=dev)
         hprev, cprev, cnew = torch.empty_like(hout), torch.empty_like(hout), torch.empty_like(hout)
         act = torch.empty((2, L, B, G), dtype=torch.float32, device=dev)
-        cnt = torch.empty(2 * nt, dtype=torch.int32, device=dev)
+        cnt = torch.empty(2 * nt * 64, dtype=torch.int32, device=dev)   # a 256-B line per group counter
         err = _rows_err(dev)
         _native.check(lib.vn_lstm_rows_fwd(_p(xc), D, _p(w_ih), _p(w_hh), _p(bias), _p(h_store), _p(c_store),
                                            h_store.shape[2], _p(env), _p(start), _p(keep), _p(hout), _p(hprev),
@@ -170,7 +170,7 @@ class _DualLSTMRows(torch.autograd.Function):
         nf = C.c_int64()
         _native.check(lib.vn_lstm_rows_part_floats(B, C.byref(nf)), "vn_lstm_rows_part_floats")
         part = torch.empty(nf.value, dtype=torch.float32, device=dev)
-        cnt = torch.empty(2 * -(-B // 32), dtype=torch.int32, device=dev)
+        cnt = torch.empty(2 * -(-B // 32) * 64, dtype=torch.int32, device=dev)
         # dG and, inside the same persistent launch, the weight and bias gradients,
         # written in the parameters' own layouts (no slicing copies)
         d_w_hh = torch.empty((2, G, H), dtype=torch.float32, device=dev)

@@ -456,7 +456,7 @@ int vn_lstm_seq_bwd_mfma(const float *dh_out, const float *w_hh, float *wpack, c
  *   x [L][B][D]; h_store, c_store [T][2][n_env][H] (the rollout buffer's states);
  *   env [L][B] int32 (the row's env), start [L][B] u8 (1: a sequence starts),
  *   keep [L][B] (1 - episode_start); out: hout, hprev (the h_{t-1} used), cprev,
- *   cnew [2][L][B][H], act [2][L][B][4H] (i, f, g, o); cnt: 2 * ceil(B / 32) u32
+ *   cnew [2][L][B][H], act [2][L][B][4H] (i, f, g, o); cnt: 2 * ceil(B / 32) * 64 u32 (one 256-B line per group counter)
  *   counters (zeroed by the call; 32-row tiles); err: set to 1 if a hand-off timed out.
  * Backward: dh_out [2][L][B][H] (+ the forward's hprev, cprev, cnew, act and x) ->
  * dG [2][L][B][4H] (may be NULL) and, accumulated inside the same launch, the weight gradients

@@ -1,0 +1,70 @@
+#!/usr/bin/env python3
+"""Times the row-layout LSTM launches (csrc/voxnav_learn_rows.hip) alone:
+forward and forward+backward at L = 128 steps for a few row counts, in the
+layout VOXNAV_ROWS_V1 / VOXNAV_ROWS_V2 select (read per call, so one process
+can A/B them).  Kernel time by HIP events on the launch stream."""
+import os
+import sys
+from pathlib import Path
+
+sys.path.insert(0, str(Path(__file__).resolve().parents[1] / "3d-navigation-reinforcement-learning_amd"))
+import torch  # noqa: E402
+from types import SimpleNamespace  # noqa: E402
+
+from voxnav import lstm_seq  # noqa: E402
+
+
+def run(B, L=128, reps=6):
+    dev = "cuda:0"
+    D, H, N = 80, 256, max(B, 64)
+    torch.manual_seed(0)
+    la, lc = torch.nn.LSTM(D, H).to(dev), torch.nn.LSTM(D, H).to(dev)
+    pol = SimpleNamespace(lstm_actor=la, lstm_critic=lc)
+    if not lstm_seq.rows_supported(pol, D, B):
+        return None
+    x = torch.randn((L, B, D), device=dev)
+    env = torch.randint(0, N, (L, B), device=dev, dtype=torch.int32)
+    start = (torch.rand((L, B), device=dev) < 0.004).to(torch.uint8)
+    start[0] = 1
+    keep = torch.ones((L, B), device=dev)
+    hs = 0.5 * torch.randn((L, 2, N, H), device=dev)
+    cs = 0.5 * torch.randn((L, 2, N, H), device=dev)
+    dy = torch.randn((2, L, B, H), device=dev)
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
+    tf, tb = [], []
+    for i in range(reps + 2):
+        for p in list(la.parameters()) + list(lc.parameters()):
+            p.grad = None
+        torch.cuda.synchronize()
+        ev[0].record()
+        out = lstm_seq.dual_lstm_rows_pair(pol, x, env, start, keep, hs, cs)
+        ev[1].record()
+        out.backward(dy)
+        ev[2].record()
+        torch.cuda.synchronize()
+        if i >= 2:
+            tf.append(ev[0].elapsed_time(ev[1]))
+            tb.append(ev[1].elapsed_time(ev[2]))
+    lstm_seq.rows_check(torch.device(dev))
+    tf.sort(), tb.sort()
+    return tf[len(tf) // 2], tb[len(tb) // 2]
+
+
+def main():
+    rows = [int(v) for v in (sys.argv[1] if len(sys.argv) > 1 else "128,256,512").split(",")]
+    modes = [("units32", {"VOXNAV_ROWS_V1": "1"}), ("units16", {"VOXNAV_ROWS_V2": "1"}), ("auto", {})]
+    for B in rows:
+        for name, envs in modes:
+            for k in ("VOXNAV_ROWS_V1", "VOXNAV_ROWS_V2"):
+                os.environ.pop(k, None)
+            os.environ.update(envs)
+            r = run(B)
+            if r is None:
+                print(f"B={B} {name}: not supported", flush=True)
+                continue
+            print(f"B={B:4d} {name:12s} fwd {r[0]:7.3f} ms ({1e3 * r[0] / 128:6.2f} us/step)  "
+                  f"bwd {r[1]:7.3f} ms ({1e3 * r[1] / 128:6.2f} us/step)", flush=True)
+
+
+if __name__ == "__main__":
+    main()

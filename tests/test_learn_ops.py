@@ -145,18 +145,28 @@ def _rows_reference(x, env, start, keep, hs, cs, lstm, l):
     return torch.stack(outs)
 
 
+@pytest.mark.parametrize("layout", ["auto", "units16", "units32"])
 @pytest.mark.parametrize("L,B,N,p_start", [(24, 512, 600, 0.03), (9, 37, 40, 0.2), (128, 64, 64, 0.01),
                                            (128, 512, 512, 0.004)])
-def test_dual_lstm_rows_matches_float64(L, B, N, p_start):
+def test_dual_lstm_rows_matches_float64(L, B, N, p_start, layout, monkeypatch):
     """The persistent row-layout LSTM (csrc/voxnav_learn_rows.hip: weights
-    resident, in-launch h / partial-dh hand-offs between the 8 unit blocks of a
+    resident, in-launch h / partial-dh hand-offs between the unit blocks of a
     row tile) against a float64 restatement: outputs and the weight / bias
     gradients of both LSTMs, with sequence starts (stored states x keep) at t = 0,
     at random steps and mid-row; full 512-row tiles, a ragged last tile, a
     whole 128-step rollout, and the learner bench's own shape (512 rows x 128
-    steps: every block of the launch resident, 128 hand-offs per direction)."""
+    steps: every block of the launch resident, 128 hand-offs per direction).
+    Both layouts, forced: 16 unit blocks of 16 units (VOXNAV_ROWS_V2=1; two
+    blocks per CU at 512 rows) and 8 of 32 (VOXNAV_ROWS_V1=1), and the
+    default pick per direction."""
     from types import SimpleNamespace
     from voxnav import lstm_seq
+    monkeypatch.delenv("VOXNAV_ROWS_V1", raising=False)
+    monkeypatch.delenv("VOXNAV_ROWS_V2", raising=False)
+    if layout == "units32":
+        monkeypatch.setenv("VOXNAV_ROWS_V1", "1")
+    elif layout == "units16":
+        monkeypatch.setenv("VOXNAV_ROWS_V2", "1")
     dev = "cuda:0"
     D, H = 80, 256
     torch.manual_seed(L * B + N)
