@@ -1379,6 +1379,18 @@ __global__ __launch_bounds__((PCM == 1 || PCM == 2) ? VN_PC_BLOCK : BLOCK,
             if (!FAST && p.actions_out && q == 0) p.actions_out[row] = a;
 
             // step() prologue (:111-116)
+// wave issue priority (s_setprio) while the step's move is computed and its
+// loads issued (3), and while the obs flush's stores are issued (2): of the
+// 4 waves on a SIMD the one about to put requests in the memory queues goes
+// first, the sensing VALU work of the others fills the gaps.  Same-process
+// A/B (profiles/r05/ab_setprio.log, four runs): the driver's 20-step window
+// +2 to +4 % in every run; 128-step launches and the P-set rooms moved -9 to
+// +9 % between runs (the spread of the env allocations), one-step calls flat.
+// 0 turns either off.
+#ifndef VN_SETPRIO
+#define VN_SETPRIO 3
+#endif
+            if (VN_SETPRIO) __builtin_amdgcn_s_setprio(VN_SETPRIO);
             if (g.near_wall) {
                 g.was_near_wall = true;
                 g.near_wall = false;
@@ -1420,6 +1432,7 @@ __global__ __launch_bounds__((PCM == 1 || PCM == 2) ? VN_PC_BLOCK : BLOCK,
                 rec = p.rays[R.ray_off + (uint32_t)((g.x * R.D + g.y) * R.H + g.z)];
             }
             if (!PC) plane_prefetch<PH>(p, map, pc_, g.x, g.y, g.z, q);
+            if (VN_SETPRIO) __builtin_amdgcn_s_setprio(0);
             ENV_T(0);
             if (shifted) {
                 if constexpr (PC) {
@@ -1513,6 +1526,10 @@ __global__ __launch_bounds__((PCM == 1 || PCM == 2) ? VN_PC_BLOCK : BLOCK,
             if (need) next_seed = seed + p.seed_stride;
         }
         ENV_T(4);
+#ifndef VN_SETPRIO_FLUSH
+#define VN_SETPRIO_FLUSH 2   // issue priority for the obs flush's stores (VN_SETPRIO above)
+#endif
+        if (VN_SETPRIO_FLUSH) __builtin_amdgcn_s_setprio(VN_SETPRIO_FLUSH);
         // the wave's 16 staged obs rows: contiguous in [K][N][80]
         if (VN_STAGE_OBS && !(VN_ABLATE & 16u)) {
             const float4 *ws4 = reinterpret_cast<const float4 *>(wst);
@@ -1542,6 +1559,7 @@ __global__ __launch_bounds__((PCM == 1 || PCM == 2) ? VN_PC_BLOCK : BLOCK,
                 }
             }
         }
+        if (VN_SETPRIO_FLUSH) __builtin_amdgcn_s_setprio(0);
         ENV_T(5);
     }
     if constexpr (STRIPE_R) {
