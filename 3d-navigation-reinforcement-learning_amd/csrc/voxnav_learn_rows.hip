@@ -131,6 +131,7 @@ struct RowsFwd {
     int32_t *err;
     int64_t n_env;
     int L, B, NT;
+    int prio;                // 16-unit layout: issue priority on the hand-off path (VOXNAV_ROWS_PRIO)
     uint32_t *diag;          // diagnostics (NULL): placement + per-step clocks
 };
 
@@ -471,6 +472,7 @@ __global__ __launch_bounds__(256, 2) void lstm_rows_fwd2_kernel(RowsFwd a) {
             acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a1.w, wr[c].w, acc1, 0, 0, 0);
         }
         VN_DMARK(1);
+        if (a.prio) __builtin_amdgcn_s_setprio(2);   // the hand-off path: wait, rows, products, cell, publish
         if (t > 0) {
             if (tid == 0) wait_ge(cnt, (uint32_t)(NUB2 * t), a.err);
             __syncthreads();
@@ -569,6 +571,7 @@ __global__ __launch_bounds__(256, 2) void lstm_rows_fwd2_kernel(RowsFwd a) {
         VN_DMARK(5);
         __syncthreads();
         if (tid == 0) __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (a.prio) __builtin_amdgcn_s_setprio(0);
         VN_DMARK(6);
     }
 #undef VN_DMARK
@@ -589,6 +592,7 @@ struct RowsBwd {
     uint32_t *cnt;           // [2 * NT * CSTRIDE]
     int32_t *err;
     int L, B, NT;
+    int prio;
 };
 
 // Backward.  Besides the recurrence, each block accumulates the weight
@@ -884,6 +888,7 @@ __global__ __launch_bounds__(256, 2) void lstm_rows_bwd2_kernel(RowsBwd a) {
                     (const __attribute__((address_space(1))) void *)(a.x + ((size_t)t * B + row) * D + 4 * lane),
                     (__attribute__((address_space(3))) void *)&xsl[rr][0], 16, 0, 0);
         }
+        if (a.prio) __builtin_amdgcn_s_setprio(2);   // the hand-off path up to the publish
         if (s > 0) {
             if (tid == 0) wait_ge(cnt, (uint32_t)(NUB2 * s), a.err);
             __syncthreads();
@@ -983,6 +988,7 @@ __global__ __launch_bounds__(256, 2) void lstm_rows_bwd2_kernel(RowsBwd a) {
             }
             publish(cnt);
         }
+        if (a.prio) __builtin_amdgcn_s_setprio(0);       // the weight gradients: off the critical path
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
         // weight gradients of gate wv's 16 rows: A = dG^T [unit][row], B = the
@@ -1073,6 +1079,15 @@ bool rows_v2(int NT, bool fwd) {
     return 2 * NUB2 * NT <= ncu || !fwd;
 }
 
+// the 16-unit kernels raise the issue priority on the hand-off path (wait,
+// rows, products, cell, publish) and drop it for the off-path weight
+// gradients / x part: at two blocks per CU the publishing block goes first
+// (backward 15.1 -> 14.2 us per step at 512 rows).  VOXNAV_ROWS_PRIO=0: off.
+int rows_prio() {
+    const char *e = getenv("VOXNAV_ROWS_PRIO");
+    return (e && e[0] == '0') ? 0 : 1;
+}
+
 uint32_t *g_rows_diag = nullptr;   // vn_lstm_rows_set_diag (diagnostics)
 
 int rows_grid_ok(int B, int NT, bool v2, int *grid) {
@@ -1141,7 +1156,7 @@ int vn_lstm_rows_fwd(const float *x, int32_t D, const float *w_ih, const float *
     const hipStream_t st = (hipStream_t)stream;
     VN_HIP(hipMemsetAsync(cnt, 0, (size_t)2 * NT * CSTRIDE * sizeof(uint32_t), st));
     RowsFwd a{x, w_ih, w_hh, bias, h_store, c_store, env, start, keep, hout, hprev, cprev, cnew, act, cnt, err,
-              n_env, L, B, NT, g_rows_diag};
+              n_env, L, B, NT, rows_prio(), g_rows_diag};
     if (v2) hipLaunchKernelGGL((lstm_rows_fwd2_kernel<80, 256>), dim3((unsigned)grid), dim3(256), 0, st, a);
     else hipLaunchKernelGGL((lstm_rows_fwd_kernel<80, 256>), dim3((unsigned)grid), dim3(256), 0, st, a);
     VN_HIP(hipGetLastError());
@@ -1168,7 +1183,7 @@ int vn_lstm_rows_bwd(const float *dh_out, const float *w_hh, const float *act, c
     float *wpart = part + 2 * slot_f;
     float *bpart = wpart + (size_t)NT * 2 * 4 * H * (H + D);
     VN_HIP(hipMemsetAsync(cnt, 0, (size_t)2 * NT * CSTRIDE * sizeof(uint32_t), st));
-    RowsBwd a{dh_out, w_hh, act, cprev, cnew, hprev, x, start, dG, part, wpart, bpart, cnt, err, L, B, NT};
+    RowsBwd a{dh_out, w_hh, act, cprev, cnew, hprev, x, start, dG, part, wpart, bpart, cnt, err, L, B, NT, rows_prio()};
     if (v2) hipLaunchKernelGGL((lstm_rows_bwd2_kernel<80, 256>), dim3((unsigned)grid), dim3(256), 0, st, a);
     else hipLaunchKernelGGL((lstm_rows_bwd_kernel<80, 256>), dim3((unsigned)grid), dim3(256), 0, st, a);
     const int64_t pw = (int64_t)2 * 4 * H * (H + D), pb = (int64_t)2 * 4 * H;

@@ -52,10 +52,12 @@ def run(B, L=128, reps=6):
 
 def main():
     rows = [int(v) for v in (sys.argv[1] if len(sys.argv) > 1 else "128,256,512").split(",")]
-    modes = [("units32", {"VOXNAV_ROWS_V1": "1"}), ("units16", {"VOXNAV_ROWS_V2": "1"}), ("auto", {})]
+    modes = [("units32", {"VOXNAV_ROWS_V1": "1"}), ("units16", {"VOXNAV_ROWS_V2": "1"}),
+             ("units16-noprio", {"VOXNAV_ROWS_V2": "1", "VOXNAV_ROWS_PRIO": "0"}), ("auto", {}),
+             ("auto-noprio", {"VOXNAV_ROWS_PRIO": "0"})]
     for B in rows:
         for name, envs in modes:
-            for k in ("VOXNAV_ROWS_V1", "VOXNAV_ROWS_V2"):
+            for k in ("VOXNAV_ROWS_V1", "VOXNAV_ROWS_V2", "VOXNAV_ROWS_PRIO"):
                 os.environ.pop(k, None)
             os.environ.update(envs)
             r = run(B)
