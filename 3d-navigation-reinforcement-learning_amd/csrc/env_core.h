@@ -110,6 +110,7 @@ struct Params {
     const int64_t *seeds;    // reset-only launches
     const uint8_t *mask;
     uint32_t ablate;         // unused (ablations are the compile-time VN_ABLATE)
+    int prio;                // step kernel: issue priority around its memory issue (bits, VOXNAV_ENV_PRIO; default 3)
     // simpleEnv variant
     int variant, obs_dim, pd;
     uint32_t *goal;          // per agent gx | gy<<8 | gz<<16

@@ -1382,15 +1382,17 @@ __global__ __launch_bounds__((PCM == 1 || PCM == 2) ? VN_PC_BLOCK : BLOCK,
 // wave issue priority (s_setprio) while the step's move is computed and its
 // loads issued (3), and while the obs flush's stores are issued (2): of the
 // 4 waves on a SIMD the one about to put requests in the memory queues goes
-// first, the sensing VALU work of the others fills the gaps.  Same-process
-// A/B (profiles/r05/ab_setprio.log, four runs): the driver's 20-step window
-// +2 to +4 % in every run; 128-step launches and the P-set rooms moved -9 to
-// +9 % between runs (the spread of the env allocations), one-step calls flat.
-// 0 turns either off.
+// first, the sensing VALU work of the others fills the gaps.  Paired A/B on
+// one env allocation (scripts/ab_same.py, profiles/r05/ab_setprio_paired.log):
+// box rooms +3.3 % at 20- and 128-step launches, +0.7 % one-step; P-set rooms
+// +0-1 %.  Also priority on the reward stores, the shift commit, the launch's
+// flush, or level 1 / 2 on the issue: no better.  Runtime switch per call:
+// VOXNAV_ENV_PRIO bit 0 (issue) / bit 1 (flush), default 3; the compile-time
+// VN_SETPRIO / VN_SETPRIO_FLUSH (diagnostics build) set the levels.
 #ifndef VN_SETPRIO
 #define VN_SETPRIO 3
 #endif
-            if (VN_SETPRIO) __builtin_amdgcn_s_setprio(VN_SETPRIO);
+            if (VN_SETPRIO && (p.prio & 1)) __builtin_amdgcn_s_setprio(VN_SETPRIO);
             if (g.near_wall) {
                 g.was_near_wall = true;
                 g.near_wall = false;
@@ -1432,7 +1434,7 @@ __global__ __launch_bounds__((PCM == 1 || PCM == 2) ? VN_PC_BLOCK : BLOCK,
                 rec = p.rays[R.ray_off + (uint32_t)((g.x * R.D + g.y) * R.H + g.z)];
             }
             if (!PC) plane_prefetch<PH>(p, map, pc_, g.x, g.y, g.z, q);
-            if (VN_SETPRIO) __builtin_amdgcn_s_setprio(0);
+            if (VN_SETPRIO && (p.prio & 1)) __builtin_amdgcn_s_setprio(0);
             ENV_T(0);
             if (shifted) {
                 if constexpr (PC) {
@@ -1529,7 +1531,7 @@ __global__ __launch_bounds__((PCM == 1 || PCM == 2) ? VN_PC_BLOCK : BLOCK,
 #ifndef VN_SETPRIO_FLUSH
 #define VN_SETPRIO_FLUSH 2   // issue priority for the obs flush's stores (VN_SETPRIO above)
 #endif
-        if (VN_SETPRIO_FLUSH) __builtin_amdgcn_s_setprio(VN_SETPRIO_FLUSH);
+        if (VN_SETPRIO_FLUSH && (p.prio & 2)) __builtin_amdgcn_s_setprio(VN_SETPRIO_FLUSH);
         // the wave's 16 staged obs rows: contiguous in [K][N][80]
         if (VN_STAGE_OBS && !(VN_ABLATE & 16u)) {
             const float4 *ws4 = reinterpret_cast<const float4 *>(wst);
@@ -1559,7 +1561,7 @@ __global__ __launch_bounds__((PCM == 1 || PCM == 2) ? VN_PC_BLOCK : BLOCK,
                 }
             }
         }
-        if (VN_SETPRIO_FLUSH) __builtin_amdgcn_s_setprio(0);
+        if (VN_SETPRIO_FLUSH && (p.prio & 2)) __builtin_amdgcn_s_setprio(0);
         ENV_T(5);
     }
     if constexpr (STRIPE_R) {
@@ -1791,6 +1793,10 @@ Params base_params(VnEnv *e) {
     p.gid_base = (uint64_t)e->cfg.agent_id_base;
     p.K = 1;
     p.ablate = e->ablate;
+    {   // read per call, so one env can A/B it (scripts/ab_same.py)
+        const char *ev = std::getenv("VOXNAV_ENV_PRIO");
+        p.prio = ev ? std::atoi(ev) : 3;   // bit 0: the step's load issue, bit 1: the obs flush
+    }
     p.variant = e->variant;
     p.obs_dim = e->obs_dim;
     p.pd = e->pd;
