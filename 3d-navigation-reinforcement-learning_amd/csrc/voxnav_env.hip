@@ -1163,6 +1163,50 @@ constexpr uint32_t kMoveDir = (2u << 0) | (0u << 2) | (3u << 4) | (1u << 6)     
                               | (0u << 8) | (3u << 10) | (1u << 12) | (2u << 14)   // right
                               | (3u << 16) | (1u << 18) | (2u << 20) | (0u << 22)  // back
                               | (1u << 24) | (2u << 26) | (0u << 28) | (3u << 30); // left
+#ifndef VN_SETPRIO_FLUSH
+#define VN_SETPRIO_FLUSH 2   // issue priority for the obs flush's stores (VN_SETPRIO in env_kernel)
+#endif
+#ifndef VN_STAGE_OBS
+#define VN_STAGE_OBS 1
+#endif
+// The wave's obs flush of launch step kk: its 16 staged rows (PC: code words
+// through the LUT) -> [K][N][80], 1 KiB contiguous per store.
+template <bool PC_>
+__device__ __forceinline__ void wave_obs_flush(const Params &p, const uint32_t *wst, const float *tab, int kk,
+                                               int wave_agent0, int nvalid, int lane, float &abl_sink) {
+    if (VN_SETPRIO_FLUSH && (p.prio & 2)) __builtin_amdgcn_s_setprio(VN_SETPRIO_FLUSH);
+    // the wave's 16 staged obs rows: contiguous in [K][N][80]
+    if (VN_STAGE_OBS && !(VN_ABLATE & 16u)) {
+        const float4 *ws4 = reinterpret_cast<const float4 *>(wst);
+        float4 *dst4 = reinterpret_cast<float4 *>(p.obs + ((size_t)kk * p.N + wave_agent0) * VN_OBS_DIM);
+        if (VN_ABLATE & 256u)      // diagnostics: the same stores into a 1.3 MB (L2-resident) region
+            dst4 = reinterpret_cast<float4 *>(p.obs) + (size_t)((wave_agent0 / 16) & 255) * 320;
+        if constexpr (PC_) {
+            // staged word f = float4 f of the wave's contiguous [16][80] rows: 1 KiB per store
+#pragma unroll
+            for (int jj = 0; jj < (64 / GROUP) * (VN_OBS_DIM / 4) / 64; ++jj) {
+                const int f = lane + 64 * jj;
+                if (VN_ABLATE & 2048u) {          // diagnostics: the stores without the LUT
+                    const uint32_t wb = wst[f];
+                    if (f < nvalid) obs_store(dst4 + f, make_float4(__uint_as_float(wb), 0.f, 0.f, 0.f));
+                } else if (VN_ABLATE & 4096u) {   // diagnostics: the LUT without the stores
+                    const float4 v = code_float4(wst[f], tab);
+                    abl_sink += v.x + v.y + v.z + v.w;
+                } else if (f < nvalid) {
+                    obs_store(dst4 + f, code_float4(wst[f], tab));
+                }
+            }
+        } else {
+#pragma unroll
+            for (int jj = 0; jj < (64 / GROUP) * (VN_OBS_DIM / 4) / 64; ++jj) {
+                const int f = lane + 64 * jj;
+                if (f < nvalid) obs_store(dst4 + f, ws4[f]);
+            }
+        }
+    }
+    if (VN_SETPRIO_FLUSH && (p.prio & 2)) __builtin_amdgcn_s_setprio(0);
+}
+
 template <int PH, bool EXT, bool FAST, bool RESET_ONLY, int PCM>
 #ifndef VN_MIN_WAVES_PER_SIMD
 #define VN_MIN_WAVES_PER_SIMD 4   // <= 128 VGPRs: the 16 waves of 256 agents per CU resident at once
@@ -1327,9 +1371,6 @@ __global__ __launch_bounds__((PCM == 1 || PCM == 2) ? VN_PC_BLOCK : BLOCK,
     uint64_t tprev = __builtin_amdgcn_s_memtime();
     const uint64_t tstart = tprev;
 #endif
-#ifndef VN_STAGE_OBS
-#define VN_STAGE_OBS 1
-#endif
     uint32_t *wst = VN_STAGE_OBS ? stage + (threadIdx.x >> 6) * kStageWords : nullptr;   // this wave's staging block
     const int aslot = (threadIdx.x & 63) >> 2;
     float abl_sink = 0.f;                             // VN_ABLATE 4096 (diagnostics)
@@ -1350,6 +1391,13 @@ __global__ __launch_bounds__((PCM == 1 || PCM == 2) ? VN_PC_BLOCK : BLOCK,
     //    evaluates step q's f64 reward and stores its reward / terminated /
     //    truncated (one store instruction per output per block).
     constexpr bool STRIPE_R = FAST && VN_REWARD_STRIPE;
+    // the wave's obs flush of launch step kk (staged rows -> [K][N][80]); with
+    // p.dflush (full waves) step k's rows go out after step k + 1's loads are
+    // issued, so those loads do not queue behind them (one in-order vmcnt)
+    // (byte-mark kernels only: in the plane-set kernels the deferred path cost 11 spilled VGPRs)
+    // Paired A/B (profiles/r05/ab_dflush_paired.log): P3 / P2 +0.9 / +0.7 % at 128-step
+    // launches, +0.7 % at 20, -0.3 % one-step (so multi-step launches only).
+    const bool dflush = DM && p.dflush && p.K > 1 && (p.N - wave_agent0) >= 64 / GROUP;   // wave-uniform
     for (int k = 0; k < p.K;) {
     const uint64_t tb = p.t0 + (uint64_t)k;
     uint32_t acts = 0;                                    // 4 actions, 8 bits each, by (t & 3)
@@ -1435,6 +1483,7 @@ __global__ __launch_bounds__((PCM == 1 || PCM == 2) ? VN_PC_BLOCK : BLOCK,
             }
             if (!PC) plane_prefetch<PH>(p, map, pc_, g.x, g.y, g.z, q);
             if (VN_SETPRIO && (p.prio & 1)) __builtin_amdgcn_s_setprio(0);
+            if (dflush && k > 0) wave_obs_flush<PC>(p, wst, tab, k - 1, wave_agent0, nvalid, lane, abl_sink);   // the previous step's rows, behind this step's loads
             ENV_T(0);
             if (shifted) {
                 if constexpr (PC) {
@@ -1528,40 +1577,7 @@ __global__ __launch_bounds__((PCM == 1 || PCM == 2) ? VN_PC_BLOCK : BLOCK,
             if (need) next_seed = seed + p.seed_stride;
         }
         ENV_T(4);
-#ifndef VN_SETPRIO_FLUSH
-#define VN_SETPRIO_FLUSH 2   // issue priority for the obs flush's stores (VN_SETPRIO above)
-#endif
-        if (VN_SETPRIO_FLUSH && (p.prio & 2)) __builtin_amdgcn_s_setprio(VN_SETPRIO_FLUSH);
-        // the wave's 16 staged obs rows: contiguous in [K][N][80]
-        if (VN_STAGE_OBS && !(VN_ABLATE & 16u)) {
-            const float4 *ws4 = reinterpret_cast<const float4 *>(wst);
-            float4 *dst4 = reinterpret_cast<float4 *>(p.obs + ((size_t)k * p.N + wave_agent0) * VN_OBS_DIM);
-            if (VN_ABLATE & 256u)      // diagnostics: the same stores into a 1.3 MB (L2-resident) region
-                dst4 = reinterpret_cast<float4 *>(p.obs) + (size_t)((wave_agent0 / 16) & 255) * 320;
-            if constexpr (PC) {
-                // staged word f = float4 f of the wave's contiguous [16][80] rows: 1 KiB per store
-#pragma unroll
-                for (int jj = 0; jj < (64 / GROUP) * (VN_OBS_DIM / 4) / 64; ++jj) {
-                    const int f = lane + 64 * jj;
-                    if (VN_ABLATE & 2048u) {          // diagnostics: the stores without the LUT
-                        const uint32_t wb = wst[f];
-                        if (f < nvalid) obs_store(dst4 + f, make_float4(__uint_as_float(wb), 0.f, 0.f, 0.f));
-                    } else if (VN_ABLATE & 4096u) {   // diagnostics: the LUT without the stores
-                        const float4 v = code_float4(wst[f], tab);
-                        abl_sink += v.x + v.y + v.z + v.w;
-                    } else if (f < nvalid) {
-                        obs_store(dst4 + f, code_float4(wst[f], tab));
-                    }
-                }
-            } else {
-#pragma unroll
-                for (int jj = 0; jj < (64 / GROUP) * (VN_OBS_DIM / 4) / 64; ++jj) {
-                    const int f = lane + 64 * jj;
-                    if (f < nvalid) obs_store(dst4 + f, ws4[f]);
-                }
-            }
-        }
-        if (VN_SETPRIO_FLUSH && (p.prio & 2)) __builtin_amdgcn_s_setprio(0);
+        if (!dflush) wave_obs_flush<PC>(p, wst, tab, k, wave_agent0, nvalid, lane, abl_sink);
         ENV_T(5);
     }
     if constexpr (STRIPE_R) {
@@ -1588,6 +1604,7 @@ __global__ __launch_bounds__((PCM == 1 || PCM == 2) ? VN_PC_BLOCK : BLOCK,
         ENV_T(6);
     }
     }
+    if (dflush && p.K > 0) wave_obs_flush<PC>(p, wst, tab, p.K - 1, wave_agent0, nvalid, lane, abl_sink);      // the launch's last step's rows
     }
     if (active) {
         if constexpr (DM) {
@@ -1796,6 +1813,8 @@ Params base_params(VnEnv *e) {
     {   // read per call, so one env can A/B it (scripts/ab_same.py)
         const char *ev = std::getenv("VOXNAV_ENV_PRIO");
         p.prio = ev ? std::atoi(ev) : 3;   // bit 0: the step's load issue, bit 1: the obs flush
+        const char *ed = std::getenv("VOXNAV_ENV_DFLUSH");
+        p.dflush = (ed && ed[0] == '0') ? 0 : 1;
     }
     p.variant = e->variant;
     p.obs_dim = e->obs_dim;
