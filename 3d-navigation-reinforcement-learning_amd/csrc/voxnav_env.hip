@@ -1128,6 +1128,14 @@ constexpr int AGENTS_PER_BLOCK = BLOCK / GROUP;
 #ifndef VN_ENV_PROF
 #define VN_ENV_PROF 0   // diagnostics build: per-section shader-clock totals of the step loop (vn_debug_env_prof)
 #endif
+#ifndef VN_ENV_WT
+#define VN_ENV_WT 0     // diagnostics build: each wave's start / end clock of the last launch, nothing else
+#endif
+#if VN_ENV_PROF || VN_ENV_WT
+// per wave of the last profiled launch: start / end on the 100-MHz clock and HW_ID / XCC_ID
+__device__ unsigned long long g_env_wt[8192 * 2];
+__device__ unsigned int g_env_wid[8192 * 2];
+#endif
 #if VN_ENV_PROF
 __device__ unsigned long long g_env_prof[16];
 #define ENV_T(k)                                                   \
@@ -1233,6 +1241,9 @@ __global__ __launch_bounds__((PCM == 1 || PCM == 2) ? VN_PC_BLOCK : BLOCK,
 #endif
 #if VN_ENV_PROF
     const uint64_t tkern = __builtin_amdgcn_s_memtime();
+#endif
+#if VN_ENV_PROF || VN_ENV_WT
+    const uint64_t rkern = __builtin_amdgcn_s_memrealtime();
 #endif
     const int q = threadIdx.x & (GROUP - 1);
     const int i = (int)((blockIdx.x * blockDim.x + threadIdx.x) / GROUP);
@@ -1636,12 +1647,32 @@ __global__ __launch_bounds__((PCM == 1 || PCM == 2) ? VN_PC_BLOCK : BLOCK,
     if (FAST && (threadIdx.x & 63) == 0) {
         __builtin_amdgcn_s_waitcnt(0);   // the flush's stores issued and retired
         const uint64_t tend = __builtin_amdgcn_s_memtime();
+        const uint64_t rend = __builtin_amdgcn_s_memrealtime();   // before the profile's own atomics
         for (int k = 0; k < 7; ++k) atomicAdd(&g_env_prof[k], (unsigned long long)eprof[k]);
         atomicAdd(&g_env_prof[7], (unsigned long long)(tprev - tstart));
         atomicAdd(&g_env_prof[8], 1ull);
         atomicAdd(&g_env_prof[9], (unsigned long long)(tstart - tkern));   // prologue: LUT, state, fill
         atomicAdd(&g_env_prof[10], (unsigned long long)(tend - tprev));    // epilogue: flush, state
         atomicMax(&g_env_prof[11], (unsigned long long)(tend - tkern));    // longest wave
+        const unsigned wg = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+        if (wg < 8192u) {
+            g_env_wt[2 * wg] = rkern;
+            g_env_wt[2 * wg + 1] = rend;
+            g_env_wid[2 * wg] = __builtin_amdgcn_s_getreg((31 << 11) | 4);
+            g_env_wid[2 * wg + 1] = __builtin_amdgcn_s_getreg((31 << 11) | 20);
+        }
+    }
+#elif VN_ENV_WT
+    if (FAST && (threadIdx.x & 63) == 0) {
+        __builtin_amdgcn_s_waitcnt(0);   // the wave's stores retired
+        const uint64_t rend = __builtin_amdgcn_s_memrealtime();
+        const unsigned wg = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+        if (wg < 8192u) {
+            g_env_wt[2 * wg] = rkern;
+            g_env_wt[2 * wg + 1] = rend;
+            g_env_wid[2 * wg] = __builtin_amdgcn_s_getreg((31 << 11) | 4);
+            g_env_wid[2 * wg + 1] = __builtin_amdgcn_s_getreg((31 << 11) | 20);
+        }
     }
 #endif
 }
@@ -2323,7 +2354,16 @@ int vn_export_belief(VnEnv *env, int8_t *belief_out, void *stream) {
     return VN_OK;
 }
 
+#if VN_ENV_PROF || VN_ENV_WT
+// the per-wave start / end clocks and ids of the last profiled launch
+int vn_debug_env_wavetimes(unsigned long long *t, unsigned int *ids) {
+    VN_HIP(hipMemcpyFromSymbol(t, HIP_SYMBOL(g_env_wt), sizeof(unsigned long long) * 8192 * 2));
+    VN_HIP(hipMemcpyFromSymbol(ids, HIP_SYMBOL(g_env_wid), sizeof(unsigned int) * 8192 * 2));
+    return 0;
+}
+#endif
 #if VN_ENV_PROF
+
 int vn_debug_env_prof(unsigned long long *out16, int clear) {
     VN_HIP(hipMemcpyFromSymbol(out16, HIP_SYMBOL(g_env_prof), sizeof(unsigned long long) * 16));
     if (clear) {

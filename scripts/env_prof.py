@@ -79,3 +79,32 @@ for k, nm in enumerate(names):
 print(f"  loop total    {prof[7] / waves / F:9.1f}; waves x launches = {waves}")
 print(f"  per launch: prologue {prof[9] / waves:9.1f}, loop {prof[7] / waves:9.1f}, epilogue {prof[10] / waves:9.1f}, "
       f"longest wave {prof[11]:9.1f} cycles")
+# the last profiled launch's per-wave start / end (100-MHz clock): how long the tail is
+wfn = getattr(raw, "vn_debug_env_wavetimes", None) or getattr(getattr(raw, "_lib", raw), "vn_debug_env_wavetimes", None)
+if wfn is not None:
+    import numpy as np
+    nw = min(8192, (a.N * 4 + 63) // 64)
+    t = (ctypes.c_ulonglong * (8192 * 2))()
+    ids = (ctypes.c_uint * (8192 * 2))()
+    wfn(t, ids)
+    tt = np.frombuffer(t, dtype=np.uint64)[:2 * nw].reshape(nw, 2).astype(np.int64)
+    ii = np.frombuffer(ids, dtype=np.uint32)[:2 * nw].reshape(nw, 2)
+    t0 = tt[:, 0].min()
+    st, en = (tt[:, 0] - t0) / 100.0, (tt[:, 1] - t0) / 100.0   # us
+    span = en.max()
+    print(f"  last launch, per wave (us from the first start): start p50 {np.median(st):.2f} max {st.max():.2f}; "
+          f"end p10 {np.percentile(en, 10):.2f} p50 {np.median(en):.2f} p90 {np.percentile(en, 90):.2f} max {span:.2f}")
+    print(f"  waves done at 80 / 90 / 95 % of the launch: {np.mean(en <= 0.8 * span):.3f} / "
+          f"{np.mean(en <= 0.9 * span):.3f} / {np.mean(en <= 0.95 * span):.3f}")
+    xcc = ii[:, 1] & 0xF
+    simd = (ii[:, 0] >> 4) & 3
+    for x in range(8):
+        m = xcc == x
+        if m.any():
+            print(f"    XCC {x}: {m.sum():4d} waves, end p50 {np.median(en[m]):.2f} max {en[m].max():.2f}")
+    # waves per SIMD slot: the last wave on each SIMD
+    key = (ii[:, 1].astype(np.int64) << 32) | (ii[:, 0] >> 4).astype(np.int64)
+    _, inv = np.unique(key, return_inverse=True)
+    last = np.zeros(inv.max() + 1)
+    np.maximum.at(last, inv, en)
+    print(f"  per SIMD, its last wave's end: p10 {np.percentile(last, 10):.2f} p50 {np.median(last):.2f} max {last.max():.2f}")
