@@ -110,7 +110,7 @@ struct Params {
     const int64_t *seeds;    // reset-only launches
     const uint8_t *mask;
     uint32_t ablate;         // unused (ablations are the compile-time VN_ABLATE)
-    int prio;                // step kernel: issue priority around its memory issue (bits, VOXNAV_ENV_PRIO; default 3)
+    int prio;                // step kernel: issue priority (bits, VOXNAV_ENV_PRIO; default 67)
     int dflush;              // step kernel: a step's obs flush after the next step's load issue (VOXNAV_ENV_DFLUSH)
     // simpleEnv variant
     int variant, obs_dim, pd;

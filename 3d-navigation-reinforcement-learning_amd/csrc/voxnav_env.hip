@@ -1177,11 +1177,19 @@ constexpr uint32_t kMoveDir = (2u << 0) | (0u << 2) | (3u << 4) | (1u << 6)     
 #ifndef VN_STAGE_OBS
 #define VN_STAGE_OBS 1
 #endif
+// s_setprio with a wave-uniform runtime level (the instruction takes an immediate)
+__device__ __forceinline__ void vn_setprio(int v) {
+    if (v <= 0) __builtin_amdgcn_s_setprio(0);
+    else if (v == 1) __builtin_amdgcn_s_setprio(1);
+    else if (v == 2) __builtin_amdgcn_s_setprio(2);
+    else __builtin_amdgcn_s_setprio(3);
+}
+
 // The wave's obs flush of launch step kk: its 16 staged rows (PC: code words
 // through the LUT) -> [K][N][80], 1 KiB contiguous per store.
 template <bool PC_>
 __device__ __forceinline__ void wave_obs_flush(const Params &p, const uint32_t *wst, const float *tab, int kk,
-                                               int wave_agent0, int nvalid, int lane, float &abl_sink) {
+                                               int wave_agent0, int nvalid, int lane, float &abl_sink, int bprio) {
     if (VN_SETPRIO_FLUSH && (p.prio & 2)) __builtin_amdgcn_s_setprio(VN_SETPRIO_FLUSH);
     // the wave's 16 staged obs rows: contiguous in [K][N][80]
     if (VN_STAGE_OBS && !(VN_ABLATE & 16u)) {
@@ -1212,7 +1220,7 @@ __device__ __forceinline__ void wave_obs_flush(const Params &p, const uint32_t *
             }
         }
     }
-    if (VN_SETPRIO_FLUSH && (p.prio & 2)) __builtin_amdgcn_s_setprio(0);
+    if (VN_SETPRIO_FLUSH && (p.prio & 2)) vn_setprio(bprio);
 }
 
 template <int PH, bool EXT, bool FAST, bool RESET_ONLY, int PCM>
@@ -1408,6 +1416,22 @@ __global__ __launch_bounds__((PCM == 1 || PCM == 2) ? VN_PC_BLOCK : BLOCK,
     // (byte-mark kernels only: in the plane-set kernels the deferred path cost 11 spilled VGPRs)
     // Paired A/B (profiles/r05/ab_dflush_paired.log): P3 / P2 +0.9 / +0.7 % at 128-step
     // launches, +0.7 % at 20, -0.3 % one-step (so multi-step launches only).
+    // A base priority that rotates over the 4 blocks sharing a CU (blocks b,
+    // b + grid/4, ... are dispatched to the same CU, oldest first): the SIMD
+    // arbiter favours older waves, so without it the CU's 4 blocks finished in
+    // dispatch order, 112 / 118 / 125 / 135 us (p50) in the driver's 20-step
+    // launch, and the youngest set the launch's end; rotating the base level
+    // every 4 steps brings them to 128 / 127 / 122 / 128 (scripts/env_wt.py,
+    // profiles/r05/env_wave_times_rotating.log).  Paired A/B
+    // (profiles/r05/ab_rotating_prio_paired.log): box +3.0 % (20-step) /
+    // +1.5 % (128-step); the byte-mark kernels -0.5 %, so plane-set only.
+    // VOXNAV_ENV_PRIO bit 6 (default on).
+    const int drank = (int)(blockIdx.x / max(1u, gridDim.x / 4u));
+    auto base_prio = [&](int kk) -> int {
+        return (PC && (p.prio & 64) && p.K >= 8) ? min((drank + (kk >> 2)) & 3, 2) : 0;   // launches of >= 8 steps
+    };
+    int bprio = base_prio(0);
+    if (bprio) vn_setprio(bprio);
     const bool dflush = DM && p.dflush && p.K > 1 && (p.N - wave_agent0) >= 64 / GROUP;   // wave-uniform
     for (int k = 0; k < p.K;) {
     const uint64_t tb = p.t0 + (uint64_t)k;
@@ -1421,6 +1445,10 @@ __global__ __launch_bounds__((PCM == 1 || PCM == 2) ? VN_PC_BLOCK : BLOCK,
             const uint4 o = philox4x32_10(p.policy_seed, p.gid_base + (uint64_t)ai, tb >> 2);
             acts = __umulhi(o.x, 6u) | (__umulhi(o.y, 6u) << 8) | (__umulhi(o.z, 6u) << 16) | (__umulhi(o.w, 6u) << 24);
         }
+    }
+    if (PC && (p.prio & 64) && p.K >= 8) {   // the rotating base level, every 4-step block
+        bprio = base_prio(k);
+        vn_setprio(bprio);
     }
     const int jn = (4 - (int)(tb & 3u)) < (p.K - k) ? (4 - (int)(tb & 3u)) : (p.K - k);
     uint64_t ev4 = 0;                                     // STRIPE_R: reward events by slot (t & 3), 16 bits each
@@ -1446,8 +1474,9 @@ __global__ __launch_bounds__((PCM == 1 || PCM == 2) ? VN_PC_BLOCK : BLOCK,
 // box rooms +3.3 % at 20- and 128-step launches, +0.7 % one-step; P-set rooms
 // +0-1 %.  Also priority on the reward stores, the shift commit, the launch's
 // flush, or level 1 / 2 on the issue: no better.  Runtime switch per call:
-// VOXNAV_ENV_PRIO bit 0 (issue) / bit 1 (flush), default 3; the compile-time
-// VN_SETPRIO / VN_SETPRIO_FLUSH (diagnostics build) set the levels.
+// VOXNAV_ENV_PRIO bit 0 (issue) / bit 1 (flush) / bit 6 (the rotating base
+// level below), default 67; the compile-time VN_SETPRIO / VN_SETPRIO_FLUSH
+// (diagnostics build) set the levels.
 #ifndef VN_SETPRIO
 #define VN_SETPRIO 3
 #endif
@@ -1493,8 +1522,8 @@ __global__ __launch_bounds__((PCM == 1 || PCM == 2) ? VN_PC_BLOCK : BLOCK,
                 rec = p.rays[R.ray_off + (uint32_t)((g.x * R.D + g.y) * R.H + g.z)];
             }
             if (!PC) plane_prefetch<PH>(p, map, pc_, g.x, g.y, g.z, q);
-            if (VN_SETPRIO && (p.prio & 1)) __builtin_amdgcn_s_setprio(0);
-            if (dflush && k > 0) wave_obs_flush<PC>(p, wst, tab, k - 1, wave_agent0, nvalid, lane, abl_sink);   // the previous step's rows, behind this step's loads
+            if (VN_SETPRIO && (p.prio & 1)) vn_setprio(bprio);
+            if (dflush && k > 0) wave_obs_flush<PC>(p, wst, tab, k - 1, wave_agent0, nvalid, lane, abl_sink, bprio);   // the previous step's rows, behind this step's loads
             ENV_T(0);
             if (shifted) {
                 if constexpr (PC) {
@@ -1588,7 +1617,7 @@ __global__ __launch_bounds__((PCM == 1 || PCM == 2) ? VN_PC_BLOCK : BLOCK,
             if (need) next_seed = seed + p.seed_stride;
         }
         ENV_T(4);
-        if (!dflush) wave_obs_flush<PC>(p, wst, tab, k, wave_agent0, nvalid, lane, abl_sink);
+        if (!dflush) wave_obs_flush<PC>(p, wst, tab, k, wave_agent0, nvalid, lane, abl_sink, bprio);
         ENV_T(5);
     }
     if constexpr (STRIPE_R) {
@@ -1615,7 +1644,7 @@ __global__ __launch_bounds__((PCM == 1 || PCM == 2) ? VN_PC_BLOCK : BLOCK,
         ENV_T(6);
     }
     }
-    if (dflush && p.K > 0) wave_obs_flush<PC>(p, wst, tab, p.K - 1, wave_agent0, nvalid, lane, abl_sink);      // the launch's last step's rows
+    if (dflush && p.K > 0) wave_obs_flush<PC>(p, wst, tab, p.K - 1, wave_agent0, nvalid, lane, abl_sink, bprio);      // the launch's last step's rows
     }
     if (active) {
         if constexpr (DM) {
@@ -1843,7 +1872,7 @@ Params base_params(VnEnv *e) {
     p.ablate = e->ablate;
     {   // read per call, so one env can A/B it (scripts/ab_same.py)
         const char *ev = std::getenv("VOXNAV_ENV_PRIO");
-        p.prio = ev ? std::atoi(ev) : 3;   // bit 0: the step's load issue, bit 1: the obs flush
+        p.prio = ev ? std::atoi(ev) : 67;   // bit 0: the step's load issue, 1: the obs flush, 6: rotating base
         const char *ed = std::getenv("VOXNAV_ENV_DFLUSH");
         p.dflush = (ed && ed[0] == '0') ? 0 : 1;
     }
