@@ -76,7 +76,7 @@ struct EnvConst {
     const uint32_t *starts;
     int32_t *err;
     int n_rooms, use_room_draw, nby, pcache;
-    uint32_t agent_bytes, xp_off, map_bytes, pad2;
+    uint32_t agent_bytes, xp_off, map_bytes, plane_bytes;   // plane_bytes: the planes a reset clears
     const uint4 *wimg;       // plane-set mode: per room, the bricked map with latent wall bits
 };
 

@@ -1032,7 +1032,7 @@ __device__ __noinline__ uint32_t reset_prepare(const EnvConst *ec, uint32_t seed
     }
     // and both marked-bit planes
     uint4 *pl = reinterpret_cast<uint4 *>(map + ec->xp_off);
-    const uint32_t pchunks = (ec->agent_bytes - ec->xp_off) / 16u;
+    const uint32_t pchunks = ec->plane_bytes / 16u;
     for (uint32_t c = (uint32_t)q; c < pchunks; c += 4u) pl[c] = make_uint4(0u, 0u, 0u, 0u);
     return (s & 0xffffffu) | ((uint32_t)room << 24);
 }
@@ -1799,6 +1799,7 @@ struct VnEnv {
     int n_rooms = 0;
     int pw = 0, pd = 0, ph = 0, nbx = 0, nby = 0;
     uint32_t map_bytes = 0, agent_bytes = 0, xp_off = 0, yp_off = 0;
+    uint32_t plane_bytes = 0;   // CubicEnv: the marked-bit planes after the map (what a reset clears)
     int nwx = 1, nwy = 1;
     size_t device_bytes = 0;
     std::vector<uint32_t> total_free;
@@ -1823,6 +1824,11 @@ struct VnEnv {
     int8_t *d_wimg = nullptr;
     float *d_scratch = nullptr;   // 4 KiB: targets of inactive lanes' output stores
     uint32_t *d_stood = nullptr;  // PCM 2: per agent 32 stood rows, then per agent the nonzero-set masks (uint2)
+    // the belief allocation (d_belief may sit at an offset inside it: placement study knobs, vn_create)
+    void *belief_alloc = nullptr;
+    size_t belief_alloc_bytes = 0;
+    bool belief_vmm = false;
+    hipMemGenericAllocationHandle_t belief_handle{};
 };
 
 namespace {
@@ -1962,7 +1968,13 @@ void free_env(VnEnv *e) {
     (void)hipFree(e->d_lut);
     (void)hipFree(e->d_hot);
     (void)hipFree(e->d_seed);
-    (void)hipFree(e->d_belief);
+    if (e->belief_vmm) {
+        (void)hipMemUnmap(e->belief_alloc, e->belief_alloc_bytes);
+        (void)hipMemAddressFree(e->belief_alloc, e->belief_alloc_bytes);
+        (void)hipMemRelease(e->belief_handle);
+    } else {
+        (void)hipFree(e->belief_alloc);
+    }
     (void)hipFree(e->d_err);
     (void)hipFree(e->d_envc);
     (void)hipFree(e->d_goal);
@@ -2161,6 +2173,9 @@ int vn_create(const VnRoomSet *rooms, int32_t n_agents, const VnConfig *cfg, int
         e->xp_off = e->map_bytes;                                           // rows (y, z): pd * ph * nwx words
         e->yp_off = e->xp_off + (uint32_t)(e->pd * e->ph * e->nwx * rowb);  // rows (x, z): pw * ph * nwy words
         e->agent_bytes = (e->yp_off + (uint32_t)(e->pw * e->ph * e->nwy * rowb) + 15u) & ~15u;
+        e->plane_bytes = e->agent_bytes - e->xp_off;
+        // placement study (diagnostics): VOXNAV_AGENT_PAD extra bytes of per-agent stride
+        if (const char *ap = getenv("VOXNAV_AGENT_PAD")) e->agent_bytes += ((uint32_t)atoi(ap) + 15u) & ~15u;
     }
 
     DeviceGuard dg(device);
@@ -2216,7 +2231,56 @@ int vn_create(const VnRoomSet *rooms, int32_t n_agents, const VnConfig *cfg, int
     VN_ALLOC(e->d_lut, sizeof(lut));
     VN_ALLOC(e->d_hot, (size_t)n_agents * sizeof(uint4));
     VN_ALLOC(e->d_seed, (size_t)n_agents * sizeof(uint32_t));
-    VN_ALLOC(e->d_belief, belief_bytes);
+    {
+        // The belief maps (placement study knobs, diagnostics: VOXNAV_BELIEF_OFFSET
+        // bytes into the allocation, VOXNAV_BELIEF_VMM=1 physical chunks of the
+        // VMM granularity mapped by hipMemCreate / hipMemMap instead of hipMalloc).
+        const char *bo = getenv("VOXNAV_BELIEF_OFFSET");
+        const size_t off = bo ? (((size_t)atoll(bo)) + 255u) & ~(size_t)255u : 0;
+        const char *bv = getenv("VOXNAV_BELIEF_VMM");
+        e->belief_alloc_bytes = belief_bytes + off;
+        if (bv && bv[0] == '1') {
+            hipMemAllocationProp prop{};
+            prop.type = hipMemAllocationTypePinned;
+            prop.location.type = hipMemLocationTypeDevice;
+            prop.location.id = device;
+            size_t gran = 0;
+            hipError_t ve = hipMemGetAllocationGranularity(&gran, &prop, hipMemAllocationGranularityRecommended);
+            if (ve == hipSuccess && gran == 0) gran = (size_t)2 << 20;
+            const size_t want = bv[1] == ':' ? (size_t)atoll(bv + 2) : 0;   // VOXNAV_BELIEF_VMM=1:<align>
+            const size_t align = want > gran ? want : gran;
+            e->belief_alloc_bytes = (e->belief_alloc_bytes + align - 1) / align * align;
+            if (ve == hipSuccess) ve = hipMemCreate(&e->belief_handle, e->belief_alloc_bytes, &prop, 0);
+            if (ve == hipSuccess) {
+                ve = hipMemAddressReserve(&e->belief_alloc, e->belief_alloc_bytes, align, nullptr, 0);
+                if (ve != hipSuccess) (void)hipMemRelease(e->belief_handle);
+            }
+            if (ve == hipSuccess) {
+                ve = hipMemMap(e->belief_alloc, e->belief_alloc_bytes, 0, e->belief_handle, 0);
+                if (ve != hipSuccess) {
+                    (void)hipMemAddressFree(e->belief_alloc, e->belief_alloc_bytes);
+                    (void)hipMemRelease(e->belief_handle);
+                }
+            }
+            if (ve == hipSuccess) {
+                e->belief_vmm = true;
+                hipMemAccessDesc acc{};
+                acc.location = prop.location;
+                acc.flags = hipMemAccessFlagsProtReadWrite;
+                ve = hipMemSetAccess(e->belief_alloc, e->belief_alloc_bytes, &acc, 1);
+            }
+            if (ve != hipSuccess) {
+                const bool mapped = e->belief_vmm;
+                if (!mapped) e->belief_alloc = nullptr;
+                free_env(e);
+                return fail(VN_ERR_OOM, "VMM belief allocation (%zu B): %s", (size_t)belief_bytes, hipGetErrorString(ve));
+            }
+        } else {
+            VN_ALLOC(e->belief_alloc, e->belief_alloc_bytes);
+        }
+        e->d_belief = reinterpret_cast<int8_t *>(e->belief_alloc) + off;
+        e->device_bytes += e->belief_vmm ? e->belief_alloc_bytes : 0;
+    }
     VN_ALLOC(e->d_err, sizeof(int32_t));
     VN_ALLOC(e->d_envc, sizeof(EnvConst));
     VN_ALLOC(e->d_goal, (size_t)n_agents * sizeof(uint32_t));
@@ -2269,6 +2333,7 @@ int vn_create(const VnRoomSet *rooms, int32_t n_agents, const VnConfig *cfg, int
         ec.agent_bytes = e->agent_bytes;
         ec.xp_off = e->xp_off;
         ec.map_bytes = e->map_bytes;
+        ec.plane_bytes = e->plane_bytes;
         ec.pcache = e->pcache;
         ec.wimg = reinterpret_cast<const uint4 *>(e->d_wimg);
         he = hipMemcpy(e->d_envc, &ec, sizeof(ec), hipMemcpyHostToDevice);
@@ -2380,6 +2445,14 @@ int vn_export_belief(VnEnv *env, int8_t *belief_out, void *stream) {
     hipLaunchKernelGGL(export_belief_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0,
                        (hipStream_t)stream, p, belief_out, env->pw, env->pd);
     VN_HIP(hipGetLastError());
+    return VN_OK;
+}
+
+// diagnostics (placement study): the device address of the belief maps and the per-agent stride
+int vn_debug_belief_addr(const VnEnv *env, uint64_t *addr, uint32_t *stride) {
+    if (!env || !addr || !stride) return fail(VN_ERR_INVALID, "NULL argument");
+    *addr = (uint64_t)(uintptr_t)env->d_belief;
+    *stride = env->agent_bytes;
     return VN_OK;
 }
 

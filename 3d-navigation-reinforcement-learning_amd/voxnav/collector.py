@@ -8,10 +8,15 @@ GPU with nothing crossing PCIe per step (one 4-byte count per rollout):
 
 per step t
   1. policy forward on obs[t] (states already zeroed for agents whose
-     previous step ended an episode): library GEMMs (x @ W_ih^T for both
-     LSTMs at once, h @ W_hh^T, the Tanh MLPs) and the HIP kernels
-     ``vn_lstm_cell`` (gates -> h, c; states stored into the buffer) and
-     ``vn_policy_head`` (logits, value, Categorical draw, log-prob)
+     previous step ended an episode), on the library's own f32 matrix-core
+     kernels (csrc/voxnav_policy_f32.hip): ``vn_lstm_fused_f32`` (both
+     LSTMs' ``[x | h] @ [W_ih | W_hh]^T`` with the cell update as epilogue,
+     the episode-start mask applied on read, (h, c) stored into the buffer)
+     and ``vn_mlp_head_f32`` (both Tanh MLPs, the action and value heads,
+     the Categorical draw and its log-prob in one launch).  Policies outside
+     those kernels' shapes take ``vn_linear_f32`` + ``vn_policy_head``;
+     torch.mm (library GEMMs) remains only for the bf16 option and for f32
+     shapes the f32 kernels do not take ("Collector paths")
   2. ``BatchedGridEnv.step_into`` -> obs[t+1], reward[t], terminated,
      truncated, terminal_obs (SB3 auto-reset inside the env kernel)
   3. ``vn_collect_post_step`` (one launch) -> episode_starts[t+1] = done;
@@ -355,6 +360,10 @@ class RolloutCollector:
         layer by layer through vn_linear_f32 into the collector's latent
         buffers; returns (lat_pi, lat_vf)."""
         w = self.w
+        if getattr(self, "_lat32", None) is None:      # (not allocated when the fused head is the default)
+            rows = max(self.N, self._stash_cap)
+            self._lat32 = [torch.zeros((2, rows, wt.shape[0]), dtype=torch.float32, device=self.device)
+                           for wt, _ in w.vf]
         br = [(x_pi, w.pi_packed, w.pi, 0)] if x_pi is not None else []
         br.append((x_vf, w.vf_packed, w.vf, 1))
         xs = [b[0] for b in br]
@@ -461,8 +470,9 @@ class RolloutCollector:
             x_pi, x_vf = (self.h_bf[0], self.h_bf[1]) if self.bf16 else (self.h[0], self.h[1])
         else:
             x_pi = x_vf = x
-        if w.mlp_head and x_pi.stride(0) == x_vf.stride(0) and x_pi.is_contiguous() and x_vf.is_contiguous():
-            self._mlp_head32(x_pi, x_vf, N, self.t_global, self.actions[t], self.values[t], self.log_probs[t])
+        if w.mlp_head:
+            self._mlp_head32(x_pi.contiguous(), x_vf.contiguous(), N, self.t_global, self.actions[t], self.values[t],
+                             self.log_probs[t])
             return
         if w.f32mlp:
             lat_pi, lat_vf = self._mlp32(x_pi, x_vf, N)

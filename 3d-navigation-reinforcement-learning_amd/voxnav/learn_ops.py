@@ -303,6 +303,10 @@ def adam_step(optimizer: torch.optim.Adam, clip_scale: Optional[torch.Tensor] = 
             st["step"] = torch.zeros((), dtype=torch.float32, device=dev)
             st["exp_avg"] = torch.zeros_like(p, memory_format=torch.preserve_format)
             st["exp_avg_sq"] = torch.zeros_like(p, memory_format=torch.preserve_format)
+        if skip is not None and (st["step"].device != dev or st["step"].dtype != torch.float32):
+            # a gated step: the counter must live on the device, where the kernel
+            # advances it only when the step is applied
+            st["step"] = st["step"].to(device=dev, dtype=torch.float32)
         steps.append(st["step"])
         for t in (p, p.grad, st["exp_avg"], st["exp_avg_sq"]):
             if t.dtype != torch.float32 or not t.is_contiguous() or t.device != dev:

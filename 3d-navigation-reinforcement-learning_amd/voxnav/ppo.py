@@ -99,10 +99,24 @@ class PPOLearner:
         return [self.rng.permutation(total) for _ in range(self.n_epochs)]
 
     def _allreduce_grads(self):
+        """Average the gradients over the group (one flattened all-reduce).
+        The recurrent learner appends its row-layout error word (1.0 when an
+        in-launch hand-off of this rank timed out) to the same buffer, and every
+        rank takes the reduced word as its own: if any rank's gradients are
+        garbage, every rank skips the Adam step and every rank raises in
+        ``update_many`` (no rank applies a corrupted average, no rank runs on
+        into the next collective alone)."""
         import torch.distributed as dist
         grads = [p.grad for p in self.params if p.grad is not None]
-        flat = torch.cat([g.reshape(-1) for g in grads])
+        parts = [g.reshape(-1) for g in grads]
+        err = lstm_seq._rows_err(grads[0].device) if self.recurrent else None
+        if err is not None:
+            parts.append((err != 0).to(grads[0].dtype).view(1))
+        flat = torch.cat(parts)
         dist.all_reduce(flat, op=dist.ReduceOp.SUM, group=self.group)
+        if err is not None:
+            err.copy_((flat[-1:] != 0).to(err.dtype))
+            flat = flat[:-1]
         flat /= dist.get_world_size(self.group)
         o = 0
         for g in grads:
@@ -208,7 +222,10 @@ class PPOLearner:
     def _rows_ok(self, D: int, rows: int) -> bool:
         """The row-layout LSTM kernels take (D, rows) for this policy (cached host query)."""
         cache = self.__dict__.setdefault("_rows_cache", {})
-        key = (D, rows)
+        # the layout knobs the library reads at every launch are part of the key,
+        # so the cached answer is always the one for the layout actually launched
+        key = (D, rows, os.environ.get("VOXNAV_ROWS_V1"), os.environ.get("VOXNAV_ROWS_V2"),
+               os.environ.get("VOXNAV_LSTM_ROWS"))
         if key not in cache:
             # VOXNAV_LSTM_ROWS=0: the per-sequence packed path (A/B knob)
             cache[key] = (not self._rows_off and os.environ.get("VOXNAV_LSTM_ROWS", "1") != "0"
@@ -354,6 +371,9 @@ class PPOLearner:
                     self.optimizer.grad_scale = None
         else:
             gnorm = torch.nn.utils.clip_grad_norm_(self.params, self.max_grad_norm)
+            err = lstm_seq.rows_err_word(self.params[0].device) if self.recurrent else None
+            if err is not None and err.device.type == "cpu" and int(err.item()) != 0:
+                return gnorm                # a rank's hand-off timed out (the reduced word): no step anywhere
             self.optimizer.step()
         self.n_updates += 1
         return gnorm
@@ -369,18 +389,24 @@ class PPOLearner:
         if not idxs:
             return torch.zeros((0, 7), dtype=torch.float64)
         nxt = self._pack_begin(buf, idxs[0], windows) if self.recurrent else None
+        n0 = self.n_updates
         logs = []
         for i, idx in enumerate(idxs):
             cur = nxt
             if self.recurrent and i + 1 < len(idxs):
                 nxt = self._pack_begin(buf, idxs[i + 1], windows)
             logs.append(self.update(buf, idx, packed=cur))
-        if self.recurrent and idxs[0].is_cuda:
+        if self.recurrent:
             try:
-                lstm_seq.rows_check(idxs[0].device)      # a timed-out row-layout launch raises
+                lstm_seq.rows_check(self.params[0].device)   # a timed-out row-layout launch raises
             except Exception:
                 # the skipped Adam steps did not advance the device step counters:
-                # re-read them on the next step
+                # n_updates counts the steps actually applied, and the host mirror
+                # of the step count is re-read on the next step
+                cache = getattr(self.optimizer, "_vn_adam_t", None)
+                if cache is not None:
+                    t_dev = int(round(float(cache[0].item())))
+                    self.n_updates = n0 + max(0, t_dev - (cache[1] - len(idxs)))
                 self.optimizer._vn_adam_t = None
                 raise
         return torch.stack(logs)

@@ -1,0 +1,111 @@
+#!/usr/bin/env python3
+"""Placement study: how the env step's rate depends on where its belief maps
+land in device memory.
+
+Per trial a ballast tensor of a different size is allocated first (so every
+later allocation moves), then for each variant a fresh env is created with
+the variant's knobs (environment variables vn_create reads:
+VOXNAV_AGENT_PAD, VOXNAV_BELIEF_OFFSET, VOXNAV_BELIEF_VMM), reset to the same
+seed `reps` times and timed over the same launch (HIP events on the launch
+stream), so every row is the same work on a different placement.  One JSON
+line per (trial, variant): median rate, the belief base address and stride.
+
+  python scripts/placement_probe.py --config 65536:32x32x8:10:20:5 --trials 8 \
+      --variants "base:,vmm:VOXNAV_BELIEF_VMM=1"
+"""
+import argparse
+import ctypes as C
+import json
+import os
+import sys
+from pathlib import Path
+
+REPO = Path(__file__).resolve().parent.parent
+sys.path.insert(0, str(REPO / "3d-navigation-reinforcement-learning_amd"))
+import torch  # noqa: E402
+
+from voxnav.env import BatchedGridEnv, Rollout  # noqa: E402
+from voxnav.rooms import box_room, load_archive_set, single_room_set  # noqa: E402
+
+
+def parse_variants(s):
+    out = []
+    for item in s.split(","):
+        name, _, kv = item.partition(":")
+        env = {}
+        for pair in [p for p in kv.split(";") if p]:
+            k, _, v = pair.partition("=")
+            env[k] = v
+        out.append((name, env))
+    return out
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--config", default="65536:32x32x8:10:20:5", help="N:room:L:K:warmup (K steps in one launch)")
+    ap.add_argument("--trials", type=int, default=8)
+    ap.add_argument("--reps", type=int, default=5)
+    ap.add_argument("--variants", default="base:")
+    ap.add_argument("--ballast-mb", type=int, default=97, help="ballast grows by this many MB per trial")
+    ap.add_argument("--out-realloc", type=int, default=1, help="re-allocate the obs buffer every trial")
+    a = ap.parse_args()
+    n, room, L, K, W = a.config.split(":")
+    n, L, K, W = int(n), int(L), int(K), int(W)
+    rs = load_archive_set(room) if room.startswith("P") else single_room_set(box_room(*map(int, room.split("x"))))
+    dev = torch.device("cuda:0")
+    variants = parse_variants(a.variants)
+    ballast = []
+    out = None
+    for t in range(a.trials):
+        ballast.append(torch.empty(((t * 7919) % 13 + 1) * a.ballast_mb * (1 << 20), dtype=torch.uint8, device=dev))
+        if out is None or a.out_realloc:
+            out = None
+            torch.cuda.empty_cache()
+            out = Rollout(torch.empty((K, n, 80), device=dev), torch.empty((K, n), device=dev),
+                          torch.empty((K, n), dtype=torch.uint8, device=dev),
+                          torch.empty((K, n), dtype=torch.uint8, device=dev), None)
+        for name, kv in variants:
+            saved = {k: os.environ.get(k) for k in kv}
+            os.environ.update(kv)
+            try:
+                e = BatchedGridEnv(num_agents=n, rooms=rs, local_map_length=L, autoreset=True, device=dev)
+            finally:
+                for k, v in saved.items():
+                    if v is None:
+                        os.environ.pop(k, None)
+                    else:
+                        os.environ[k] = v
+            lib = e.lib
+            fn = getattr(lib, "vn_debug_belief_addr", None)
+            addr, stride = C.c_uint64(0), C.c_uint32(0)
+            if fn is not None:
+                fn.restype = C.c_int
+                fn.argtypes = [C.c_void_p, C.POINTER(C.c_uint64), C.POINTER(C.c_uint32)]
+                fn(e._h, C.byref(addr), C.byref(stride))
+            us = []
+            stream = torch.cuda.current_stream(dev)
+            for _ in range(a.reps):
+                e.reset(seed=42)
+                if W:
+                    wv = Rollout(out.obs[:W], out.reward[:W], out.terminated[:W], out.truncated[:W], None)
+                    e.step_random(W, policy_seed=42, out=wv)
+                ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                torch.cuda.synchronize()
+                ev0.record(stream)
+                e.step_random(K, policy_seed=42, out=out)
+                ev1.record(stream)
+                torch.cuda.synchronize()
+                us.append(ev0.elapsed_time(ev1) * 1e3)
+            e.close()
+            del e
+            us.sort()
+            med = us[len(us) // 2]
+            print(json.dumps({"trial": t, "variant": name, "us_median": round(med, 2), "us_min": round(us[0], 2),
+                              "us_max": round(us[-1], 2), "Gsteps": round(n * K / med / 1e3, 3),
+                              "belief_addr": hex(addr.value), "addr_mod_2M": addr.value % (1 << 21),
+                              "stride": stride.value, "obs_addr": hex(out.obs.data_ptr()),
+                              "obs_mod_2M": out.obs.data_ptr() % (1 << 21)}), flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -63,3 +63,44 @@ def test_bindings_match_header_arity():
         assert m, name
         params = [p for p in m.group(1).split(",") if p.strip() and p.strip() != "void"]
         assert len(params) == len(args), (name, len(params), len(args))
+
+
+def _isa_check():
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("isa_check", REPO / "scripts" / "isa_check.py")
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    return mod
+
+
+def test_mlp_head_ring_wait_counts_hold_in_the_built_code():
+    """vn_mlp_head_f32's hand-counted ``s_waitcnt vmcnt(PER)`` ring waits
+    (csrc/voxnav_policy_f32.hip mh_layer) are right only if the compiled
+    ring loops issue exactly PER ring loads and no other VMEM instruction
+    between consecutive waits, and 2 x PER before the loop: checked on the
+    disassembly of the built library (scripts/isa_check.py), both template
+    instances (one- and two-tile loops)."""
+    from voxnav import _build
+    mod = _isa_check()
+    rep = mod.check(_build.LIB)
+    assert set(rep["loops"]) == {1, 2}
+    # the checker rejects what it guards against: an extra VMEM op in a ring
+    # loop (a spill / hoisted load), or one ring load too few before the loop
+    sym, ins = mod.kernel_listing(_build.LIB)
+    lo, hi = (int(v, 16) for v in rep["loops"][2]["loop"])
+    k = next(i for i, x in enumerate(ins) if lo < x[0] < hi and x[1] == mod.RING_LOAD)
+    bad = ins[:k] + [(ins[k][0] - 2, "global_load_dword", "v1, v[2:3], off", None)] + ins[k:]
+    try:
+        mod.check_listing(sym, bad)
+    except AssertionError as e:
+        assert "besides the ring loads" in str(e)
+    else:
+        raise AssertionError("the checker accepted a foreign VMEM load inside the ring loop")
+    first = next(i for i, x in enumerate(ins) if x[1] == mod.RING_LOAD)      # a prologue load
+    short = ins[:first] + ins[first + 1:]
+    try:
+        mod.check_listing(sym, short)
+    except AssertionError:
+        pass
+    else:
+        raise AssertionError("the checker accepted a ring prologue one load short")

@@ -3,7 +3,9 @@
 voxnav.ppo.PPOLearner(process_group=...) averages the gradients of the
 ranks' minibatches (one flattened all-reduce) before the clip.  Checked:
 with the same buffer on both ranks the update equals a single-process
-learner; with different buffers both ranks end with identical parameters.
+learner; with different buffers both ranks end with identical parameters;
+with the row-layout error word set on one rank only, every rank skips its
+step and raises (the word is reduced with the gradients).
 """
 import os
 import socket
@@ -59,8 +61,30 @@ def _worker(rank, world, port, q):
         g_stats = reduce_episode_stats(mine)
         stats_ok = (g_stats["n_episodes_global"] == 5 and abs(g_stats["avg_score"] - (21 + 63) / 5) < 1e-12
                     and abs(g_stats["finished_pct"] - 40.0) < 1e-12 and abs(g_stats["avg_steps"] - 38 / 5) < 1e-12)
+        # C: one rank's row-layout error word set (a timed-out hand-off) -> the
+        # reduced word makes every rank skip its Adam step and raise, in step
+        from voxnav import lstm_seq
+        from voxnav._native import VoxnavError
+        pol3 = tp._policy(True, seed=0)
+        ln3 = PPOLearner(pol3, n_epochs=1, batch_size=16, seed=5, process_group=dist.group.WORLD)
+        before = flat(pol3).clone()
+        lstm_seq._rows_err(torch.device("cpu")).fill_(1 if rank == 1 else 0)
+        raised = 0.0
+        try:
+            ln3.train(tp._as_rollout(tp._buffer(12, 5, 16, True, seed=20 + rank), "cpu"))
+        except VoxnavError:
+            raised = 1.0
+        kept = 1.0 if (float((flat(pol3) - before).abs().max()) == 0.0 and ln3.n_updates == 0) else 0.0
+        word = float(lstm_seq._rows_err(torch.device("cpu")).item())
+        res = torch.tensor([raised, kept, word])
+        allres = [torch.empty_like(res) for _ in range(world)]
+        dist.all_gather(allres, res)
+        skip_ok = all(r.tolist() == [1.0, 1.0, 0.0] for r in allres)
         if rank == 0:
-            q.put(("ok" if stats_ok else "stats mismatch", same, spread, moved))
+            status = "ok" if stats_ok else "stats mismatch"
+            if not skip_ok:
+                status = f"error-word skip: {[r.tolist() for r in allres]}"
+            q.put((status, same, spread, moved))
         dist.barrier()
         dist.destroy_process_group()
     except Exception as e:  # noqa: BLE001
