@@ -243,6 +243,9 @@ __device__ __forceinline__ bool mark_w(uint32_t &w, const Rays &ry, int r, int s
 #ifndef VN_STOOD
 #define VN_STOOD 1
 #endif
+#ifndef VN_STOOD_PART
+#define VN_STOOD_PART 1      // launches of <= 8 steps load only the stood-row shares they can reach
+#endif
 constexpr int kStoodStride = 33;   // u32 per agent in LDS (32 rows + 1: bank spread)
 struct Stood {
     uint32_t *row;                 // the agent's S rows in LDS (nullptr when off)
@@ -402,6 +405,18 @@ __device__ __forceinline__ void tile_write(uint64_t *tile, int slot, const Col<P
 
 __device__ __forceinline__ int tslot(int x, int y) { return ((x & 3) << 2) | (y & 3); }
 
+// Plane-set mode: the latent-wall room images, VN_WIMG_REP copies per room
+// ([room][copy][map_bytes]); agent a reads copy a % VN_WIMG_REP, so the
+// launch's window fill (every agent reading its room's image at once) is
+// spread over more L2 lines (diagnostics knob, default one copy).
+#ifndef VN_WIMG_REP
+#define VN_WIMG_REP 1
+#endif
+__device__ __forceinline__ const int8_t *room_image(const int8_t *wimg, int room, uint32_t map_bytes) {
+    const uint32_t agent = (blockIdx.x * blockDim.x + threadIdx.x) >> 2;
+    return wimg + ((size_t)room * VN_WIMG_REP + (VN_WIMG_REP > 1 ? agent % VN_WIMG_REP : 0u)) * map_bytes;
+}
+
 // The window bytes [z - 2, z + 1] of a tile column as one u32 (byte 0 = z - 2,
 // zeros outside [0, PH)): two dword reads and a funnel shift, so a sensing
 // pass holds one register per window column instead of the whole column
@@ -470,7 +485,7 @@ template <int PH, bool PC, typename RT, bool SB = false>
 __device__ __forceinline__ void tile_fill(const Params &p, const int8_t *map, uint64_t *tile, const RT *ps,
                                           const Agent &g, const Room &R, int q, const Stood &st) {
     const int cy = g.y + q - 2;
-    const int8_t *img = SB ? p.wimg + (size_t)g.room * p.map_bytes : map;
+    const int8_t *img = SB ? room_image(p.wimg, g.room, p.map_bytes) : map;
     const uint32_t srow = SB && cy >= 0 && cy < R.D ? st.row[cy] : ~0u;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
@@ -547,7 +562,7 @@ __device__ __forceinline__ void tile_shift_issue(const Params &p, int8_t *map, c
     } else if (!(VN_ABLATE & 1u) && sl.in) {
         // SB: a column never stood in is the room image's (L2), not an HBM read
         const bool stood = !SB || ((st.row[ey] >> ex) & 1u);
-        col_load<PH>((stood ? (const int8_t *)map : p.wimg + (size_t)room * p.map_bytes) + boff<PH>(ex, ey, 0, p.nby),
+        col_load<PH>((stood ? (const int8_t *)map : room_image(p.wimg, room, p.map_bytes)) + boff<PH>(ex, ey, 0, p.nby),
                      sl.c);
     }
     if (!(VN_ABLATE & 8u) && ((dirty >> sl.s) & 1u) && lx >= 0 && lx < R.W && ly >= 0 && ly < R.D) {
@@ -726,7 +741,7 @@ __device__ __forceinline__ int sense_observe(const Params &p, int8_t *map, uint6
     auto fresh_col = [&](int i, Col<PH> &c) {
         col_zero<PH>(c);
         if (PC && yin && x + i - 2 >= 0 && x + i - 2 < R.W)
-            col_load<PH>(p.wimg + (size_t)g.room * p.map_bytes + boff<PH>(x + i - 2, cy, 0, nby), c);
+            col_load<PH>(room_image(p.wimg, g.room, p.map_bytes) + boff<PH>(x + i - 2, cy, 0, nby), c);
     };
     uint32_t win[4];
     Col<PH> cen;
@@ -788,7 +803,7 @@ __device__ __forceinline__ int sense_observe(const Params &p, int8_t *map, uint6
             pc_.w0 = nw <= 2 ? 0 : pw0;
             pc_.w[0] = pc_.w[1] = 0ull;
             pc_.dirty = 0u;
-        } else if (nw > 2 && (pc_.row != rowi || pc_.w0 != pw0)) {
+        } else if (!DM && nw > 2 && (pc_.row != rowi || pc_.w0 != pw0)) {   // (DM: rows of <= 2 words, prefetched)
             pc_.row = rowi;
             pc_.w0 = pw0;
             pc_.w[0] = prow[pw0];
@@ -1021,7 +1036,9 @@ __device__ __noinline__ uint32_t reset_prepare(const EnvConst *ec, uint32_t seed
     // clear the room's bricks to "unknown" (0x00; PC: the room image, 0x40
     // at the walls), 16 B per lane per store
     uint4 *base = reinterpret_cast<uint4 *>(map);
-    const uint4 *img = PC ? ec->wimg + (size_t)room * (ec->map_bytes / 16u) : nullptr;
+    const uint4 *img = PC ? reinterpret_cast<const uint4 *>(room_image(reinterpret_cast<const int8_t *>(ec->wimg), room,
+                                                                       ec->map_bytes))
+                         : nullptr;
     const uint32_t per_brick = (uint32_t)PH;          // 16-byte chunks per brick
     const uint32_t total = (uint32_t)(R.nbx * R.nby) * per_brick;
     for (uint32_t c = (uint32_t)q; c < total; c += 4u) {
@@ -1177,6 +1194,9 @@ constexpr uint32_t kMoveDir = (2u << 0) | (0u << 2) | (3u << 4) | (1u << 6)     
 #ifndef VN_STAGE_OBS
 #define VN_STAGE_OBS 1
 #endif
+#ifndef VN_DFLUSH_DEFAULT
+#define VN_DFLUSH_DEFAULT 1  // VOXNAV_ENV_DFLUSH when unset: bit 0 byte-mark kernels, bit 1 plane-set kernels
+#endif
 // s_setprio with a wave-uniform runtime level (the instruction takes an immediate)
 __device__ __forceinline__ void vn_setprio(int v) {
     if (v <= 0) __builtin_amdgcn_s_setprio(0);
@@ -1187,7 +1207,16 @@ __device__ __forceinline__ void vn_setprio(int v) {
 
 // The wave's obs flush of launch step kk: its 16 staged rows (PC: code words
 // through the LUT) -> [K][N][80], 1 KiB contiguous per store.
-template <bool PC_>
+//
+// DFL (the deferred flush: step kk's rows stored after step kk + 1's loads
+// are issued, full waves only): exactly five store instructions on every
+// path, no lane mask and no branch -- kk < 0 (the launch's first step, which
+// has no previous rows) stores into the scratch buffer instead -- so the
+// compiler's wait for any load issued before them is vmcnt(>= 5): a step's
+// loads never wait for the previous step's obs stores to be acknowledged
+// (gfx9 counts loads and stores in one in-order vmcnt; a path with fewer
+// stores would merge into vmcnt(0) waits).
+template <bool PC_, bool DFL = false>
 __device__ __forceinline__ void wave_obs_flush(const Params &p, const uint32_t *wst, const float *tab, int kk,
                                                int wave_agent0, int nvalid, int lane, float &abl_sink, int bprio) {
     if (VN_SETPRIO_FLUSH && (p.prio & 2)) __builtin_amdgcn_s_setprio(VN_SETPRIO_FLUSH);
@@ -1195,6 +1224,7 @@ __device__ __forceinline__ void wave_obs_flush(const Params &p, const uint32_t *
     if (VN_STAGE_OBS && !(VN_ABLATE & 16u)) {
         const float4 *ws4 = reinterpret_cast<const float4 *>(wst);
         float4 *dst4 = reinterpret_cast<float4 *>(p.obs + ((size_t)kk * p.N + wave_agent0) * VN_OBS_DIM);
+        if (DFL) dst4 = kk >= 0 ? dst4 : reinterpret_cast<float4 *>(p.scratch);   // (select, not a branch)
         if (VN_ABLATE & 256u)      // diagnostics: the same stores into a 1.3 MB (L2-resident) region
             dst4 = reinterpret_cast<float4 *>(p.obs) + (size_t)((wave_agent0 / 16) & 255) * 320;
         if constexpr (PC_) {
@@ -1208,7 +1238,7 @@ __device__ __forceinline__ void wave_obs_flush(const Params &p, const uint32_t *
                 } else if (VN_ABLATE & 4096u) {   // diagnostics: the LUT without the stores
                     const float4 v = code_float4(wst[f], tab);
                     abl_sink += v.x + v.y + v.z + v.w;
-                } else if (f < nvalid) {
+                } else if (DFL || f < nvalid) {
                     obs_store(dst4 + f, code_float4(wst[f], tab));
                 }
             }
@@ -1216,14 +1246,14 @@ __device__ __forceinline__ void wave_obs_flush(const Params &p, const uint32_t *
 #pragma unroll
             for (int jj = 0; jj < (64 / GROUP) * (VN_OBS_DIM / 4) / 64; ++jj) {
                 const int f = lane + 64 * jj;
-                if (f < nvalid) obs_store(dst4 + f, ws4[f]);
+                if (DFL || f < nvalid) obs_store(dst4 + f, ws4[f]);
             }
         }
     }
     if (VN_SETPRIO_FLUSH && (p.prio & 2)) vn_setprio(bprio);
 }
 
-template <int PH, bool EXT, bool FAST, bool RESET_ONLY, int PCM>
+template <int PH, bool EXT, bool FAST, bool RESET_ONLY, int PCM, bool DFL = false>
 #ifndef VN_MIN_WAVES_PER_SIMD
 #define VN_MIN_WAVES_PER_SIMD 4   // <= 128 VGPRs: the 16 waves of 256 agents per CU resident at once
 #endif
@@ -1260,13 +1290,21 @@ __global__ __launch_bounds__((PCM == 1 || PCM == 2) ? VN_PC_BLOCK : BLOCK,
     // the agent's state loads are in flight while the block stages its LUT
     const uint4 hot0 = p.hot[ai];
     uint32_t next_seed = p.next_seed[ai];
-    // SB: lane q's share of the stood rows (8q .. 8q + 7) and the nonzero-set masks
+    // SB: lane q's share of the stood rows (8q .. 8q + 7) and the nonzero-set masks.
+    // A short launch (VN_STOOD_PART, K <= 8) can only reach the rows y - 2 - K ..
+    // y + 1 + K: the shares outside them are not loaded (they stay zero in LDS,
+    // are never read, and are never written back -- a share is stored only when
+    // one of its rows changed, and a reset rewrites all four).  The one-step
+    // call reads 1-2 of the 4 shares instead of 128 B per agent.
     uint4 sr0 = make_uint4(0u, 0u, 0u, 0u), sr1 = sr0;
     uint2 nz0 = make_uint2(0u, 0u);
+    const bool stood_all = !VN_STOOD_PART || p.K > 8;
+    const uint4 *sp_share = reinterpret_cast<const uint4 *>(p.stood + (size_t)ai * 32u + 8u * (uint32_t)q);
     if (SB && !RESET_ONLY) {
-        const uint4 *sp = reinterpret_cast<const uint4 *>(p.stood + (size_t)ai * 32u + 8u * (uint32_t)q);
-        sr0 = sp[0];
-        sr1 = sp[1];
+        if (stood_all) {
+            sr0 = sp_share[0];
+            sr1 = sp_share[1];
+        }
         nz0 = p.pnz[ai];
     }
     for (int k = threadIdx.x; k < TAB_SIZE; k += blockDim.x) tab[k < 256 ? tab_ix((uint32_t)k) : k] = p.lut[k];
@@ -1277,6 +1315,13 @@ __global__ __launch_bounds__((PCM == 1 || PCM == 2) ? VN_PC_BLOCK : BLOCK,
 
     uint64_t *tile = tiles + (threadIdx.x / GROUP) * TileGeom<PH>::STRIDE;
     Agent g = unpack(hot0);
+    if (SB && !RESET_ONLY && !stood_all) {     // the shares this launch can reach (issued beside the room load)
+        const int lo = g.y - 2 - p.K, hi = g.y + 1 + p.K;
+        if (8 * q + 7 >= lo && 8 * q <= hi) {
+            sr0 = sp_share[0];
+            sr1 = sp_share[1];
+        }
+    }
     Room R = load_room(p, active ? g.room : 0);
     room_touch(R);
     int8_t *map = p.belief + (size_t)ai * p.agent_bytes;
@@ -1432,7 +1477,11 @@ __global__ __launch_bounds__((PCM == 1 || PCM == 2) ? VN_PC_BLOCK : BLOCK,
     };
     int bprio = base_prio(0);
     if (bprio) vn_setprio(bprio);
-    const bool dflush = DM && p.dflush && p.K > 1 && (p.N - wave_agent0) >= 64 / GROUP;   // wave-uniform
+    // DFL: chosen by the host (launch_ph: VOXNAV_ENV_DFLUSH, launches of more
+    // than one step, every wave full); a separate instantiation, so the
+    // waits of the loop see the same five flush stores on every path
+    static_assert(!DFL || (!RESET_ONLY && (DM || PC)), "the deferred flush is for step launches of DM / PC kernels");
+    constexpr bool dflush = DFL;
     for (int k = 0; k < p.K;) {
     const uint64_t tb = p.t0 + (uint64_t)k;
     uint32_t acts = 0;                                    // 4 actions, 8 bits each, by (t & 3)
@@ -1523,7 +1572,13 @@ __global__ __launch_bounds__((PCM == 1 || PCM == 2) ? VN_PC_BLOCK : BLOCK,
             }
             if (!PC) plane_prefetch<PH>(p, map, pc_, g.x, g.y, g.z, q);
             if (VN_SETPRIO && (p.prio & 1)) vn_setprio(bprio);
-            if (dflush && k > 0) wave_obs_flush<PC>(p, wst, tab, k - 1, wave_agent0, nvalid, lane, abl_sink, bprio);   // the previous step's rows, behind this step's loads
+            // the previous step's rows, behind this step's loads (k == 0: into scratch);
+            // the compiler barrier keeps the loads above (the plane rows' conditional
+            // block included) ahead of the five stores
+            if constexpr (DFL) {
+                asm volatile("" ::: "memory");
+                wave_obs_flush<PC, true>(p, wst, tab, k - 1, wave_agent0, nvalid, lane, abl_sink, bprio);
+            }
             ENV_T(0);
             if (shifted) {
                 if constexpr (PC) {
@@ -1617,7 +1672,7 @@ __global__ __launch_bounds__((PCM == 1 || PCM == 2) ? VN_PC_BLOCK : BLOCK,
             if (need) next_seed = seed + p.seed_stride;
         }
         ENV_T(4);
-        if (!dflush) wave_obs_flush<PC>(p, wst, tab, k, wave_agent0, nvalid, lane, abl_sink, bprio);
+        if constexpr (!DFL) wave_obs_flush<PC>(p, wst, tab, k, wave_agent0, nvalid, lane, abl_sink, bprio);
         ENV_T(5);
     }
     if constexpr (STRIPE_R) {
@@ -1644,7 +1699,7 @@ __global__ __launch_bounds__((PCM == 1 || PCM == 2) ? VN_PC_BLOCK : BLOCK,
         ENV_T(6);
     }
     }
-    if (dflush && p.K > 0) wave_obs_flush<PC>(p, wst, tab, p.K - 1, wave_agent0, nvalid, lane, abl_sink, bprio);      // the launch's last step's rows
+    if constexpr (DFL) wave_obs_flush<PC, true>(p, wst, tab, p.K - 1, wave_agent0, nvalid, lane, abl_sink, bprio);      // the launch's last step's rows
     }
     if (active) {
         if constexpr (DM) {
@@ -1822,7 +1877,7 @@ struct VnEnv {
     int defer = 0;     // CubicEnv byte-mark mode with deferred plane marks (PCM 3; rows <= 2 words)
     int pcache = 0;    // CubicEnv plane-set mode (PH 8, rooms <= 64 x 64): see pset_fill
     int8_t *d_wimg = nullptr;
-    float *d_scratch = nullptr;   // 4 KiB: targets of inactive lanes' output stores
+    float *d_scratch = nullptr;   // 8 KiB: targets of dummy output stores (the deferred flush's first step)
     uint32_t *d_stood = nullptr;  // PCM 2: per agent 32 stood rows, then per agent the nonzero-set masks (uint2)
     // the belief allocation (d_belief may sit at an offset inside it: placement study knobs, vn_create)
     void *belief_alloc = nullptr;
@@ -1879,8 +1934,9 @@ Params base_params(VnEnv *e) {
     {   // read per call, so one env can A/B it (scripts/ab_same.py)
         const char *ev = std::getenv("VOXNAV_ENV_PRIO");
         p.prio = ev ? std::atoi(ev) : 67;   // bit 0: the step's load issue, 1: the obs flush, 6: rotating base
+        // bit 0: the deferred obs flush in the byte-mark kernels (PCM 3), bit 1: in the plane-set ones
         const char *ed = std::getenv("VOXNAV_ENV_DFLUSH");
-        p.dflush = (ed && ed[0] == '0') ? 0 : 1;
+        p.dflush = ed ? std::atoi(ed) : VN_DFLUSH_DEFAULT;
     }
     p.variant = e->variant;
     p.obs_dim = e->obs_dim;
@@ -1900,6 +1956,15 @@ Params base_params(VnEnv *e) {
     return p;
 }
 
+// The deferred obs flush (env_kernel's DFL): step launches of more than one
+// step with every wave full, in the kernel modes VOXNAV_ENV_DFLUSH enables
+// (bit 0: byte marks, PCM 3; bit 1: plane sets, PCM 1 / 2).
+constexpr bool pcm_dfl_capable(int pcm) { return pcm == 1 || pcm == 2 || pcm == 3; }
+static bool use_dfl(int pcm, int N, int K, int dflush_bits) {
+    if (!pcm_dfl_capable(pcm) || K <= 1 || N % (64 / GROUP) != 0) return false;
+    return (pcm == 3) ? (dflush_bits & 1) != 0 : (dflush_bits & 2) != 0;
+}
+
 template <int PH, bool RESET_ONLY, int PCM>
 int launch_ph(int N, hipStream_t s, const Params &p) {
     const int bs = (PCM == 1 || PCM == 2) ? VN_PC_BLOCK : BLOCK;
@@ -1908,14 +1973,20 @@ int launch_ph(int N, hipStream_t s, const Params &p) {
     // FAST: the rollout-buffer call (f32 reward, flags; the f64 reward for the
     // Monitor optional, stored once per 4-step block); no action record
     const bool fast = p.reward && p.term && p.trunc && !p.actions_out;
+    constexpr bool CAP = pcm_dfl_capable(PCM);
+    const bool dfl = CAP && !RESET_ONLY && use_dfl(PCM, N, p.K, p.dflush);
     if (RESET_ONLY)
         hipLaunchKernelGGL((env_kernel<PH, false, false, true, PCM>), grid, block, 0, s, p);
     else if (p.actions && fast)
         hipLaunchKernelGGL((env_kernel<PH, true, true, false, PCM>), grid, block, 0, s, p);
     else if (p.actions)
         hipLaunchKernelGGL((env_kernel<PH, true, false, false, PCM>), grid, block, 0, s, p);
+    else if (fast && dfl)
+        hipLaunchKernelGGL((env_kernel<PH, false, true, false, PCM, CAP>), grid, block, 0, s, p);
     else if (fast)
         hipLaunchKernelGGL((env_kernel<PH, false, true, false, PCM>), grid, block, 0, s, p);
+    else if (dfl)
+        hipLaunchKernelGGL((env_kernel<PH, false, false, false, PCM, CAP>), grid, block, 0, s, p);
     else
         hipLaunchKernelGGL((env_kernel<PH, false, false, false, PCM>), grid, block, 0, s, p);
     VN_HIP(hipGetLastError());
@@ -1952,11 +2023,12 @@ std::string kernel_label(const VnEnv *e, bool reset_only, bool ext, bool fast, i
     char buf[160];
     if (e->variant == VN_VARIANT_SIMPLE)
         return vn_simple::label(reset_only, ext, e->sline, e->sbits, e->cfg.local_map_length);
-    (void)k_steps;
     const int pcm = env_pcm(e);
     const bool x = !reset_only && ext, f = !reset_only && fast;
-    std::snprintf(buf, sizeof(buf), "env_kernel<%d, %s, %s, %s, %d>", e->ph, x ? "true" : "false",
-                  f ? "true" : "false", reset_only ? "true" : "false", pcm);
+    const char *ed = std::getenv("VOXNAV_ENV_DFLUSH");
+    const bool dfl = !reset_only && !x && use_dfl(pcm, e->N, k_steps, ed ? std::atoi(ed) : VN_DFLUSH_DEFAULT);
+    std::snprintf(buf, sizeof(buf), "env_kernel<%d, %s, %s, %s, %d%s>", e->ph, x ? "true" : "false",
+                  f ? "true" : "false", reset_only ? "true" : "false", pcm, dfl ? ", true" : "");
     return buf;
 }
 
@@ -2285,9 +2357,9 @@ int vn_create(const VnRoomSet *rooms, int32_t n_agents, const VnConfig *cfg, int
     VN_ALLOC(e->d_envc, sizeof(EnvConst));
     VN_ALLOC(e->d_goal, (size_t)n_agents * sizeof(uint32_t));
     VN_ALLOC(e->d_predraw, (size_t)n_agents * sizeof(uint4));
-    if (e->pcache) VN_ALLOC(e->d_wimg, (size_t)nr * e->map_bytes);
+    if (e->pcache) VN_ALLOC(e->d_wimg, (size_t)nr * VN_WIMG_REP * e->map_bytes);
     if (e->pcache == 2) VN_ALLOC(e->d_stood, (size_t)n_agents * 34u * sizeof(uint32_t));
-    VN_ALLOC(e->d_scratch, 4096);
+    VN_ALLOC(e->d_scratch, 8192);
 #undef VN_ALLOC
     hipError_t he = hipSuccess;
     if (he == hipSuccess) he = hipMemcpy(e->d_rooms, desc.data(), desc.size() * sizeof(uint32_t), hipMemcpyHostToDevice);
@@ -2306,17 +2378,18 @@ int vn_create(const VnRoomSet *rooms, int32_t n_agents, const VnConfig *cfg, int
     if (he == hipSuccess && e->pcache) {
         // per room: the bricked byte map of a fresh episode -- 0x40 (latent
         // wall, still unknown) at every wall cell, 0 elsewhere
-        std::vector<int8_t> img((size_t)nr * e->map_bytes, 0);
+        std::vector<int8_t> img((size_t)nr * VN_WIMG_REP * e->map_bytes, 0);
         size_t wo = 0;
         for (int r = 0; r < nr; ++r) {
             const int W = rooms->whd[3 * r], D = rooms->whd[3 * r + 1], H = rooms->whd[3 * r + 2];
-            int8_t *m = img.data() + (size_t)r * e->map_bytes;
+            int8_t *m = img.data() + (size_t)r * VN_WIMG_REP * e->map_bytes;
             for (int x = 0; x < W; ++x)
                 for (int y = 0; y < D; ++y)
                     for (int z = 0; z < H; ++z)
                         if (rooms->walls[wo + ((size_t)x * D + y) * H + z])
                             m[(((((x >> 2) * e->nby + (y >> 2)) << 4) + ((x & 3) << 2) + (y & 3)) * e->ph) + z] = 0x40;
             wo += (size_t)W * D * H;
+            for (int c = 1; c < VN_WIMG_REP; ++c) std::memcpy(m + (size_t)c * e->map_bytes, m, e->map_bytes);
         }
         he = hipMemcpy(e->d_wimg, img.data(), img.size(), hipMemcpyHostToDevice);
     }

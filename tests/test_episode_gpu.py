@@ -68,7 +68,8 @@ def run_random_episode(env, N, sample, F=16, gid_base=0, seed_stride=None, src=S
                   torch.empty((F, N), dtype=torch.float32, device=dev),
                   torch.empty((F, N), dtype=torch.uint8, device=dev),
                   torch.empty((F, N), dtype=torch.uint8, device=dev), None)
-    assert env.kernel_label(F) == "env_kernel<8, false, true, false, 2>"
+    # (", true": the deferred-flush instantiation, VOXNAV_ENV_DFLUSH bit 1)
+    assert env.kernel_label(F) in ("env_kernel<8, false, true, false, 2>", "env_kernel<8, false, true, false, 2, true>")
     idx = torch.as_tensor(sample, device=dev)
     orc_env = oracle_env(src, L, n_agents=len(sample))
     gids = gid_base + np.asarray(sample, dtype=np.int64)
