@@ -124,6 +124,8 @@ struct Params {
     float *scratch;          // 4 KiB: targets of inactive lanes' output stores
     uint32_t *stood;         // plane-set mode PCM 2: per agent 32 words, stood-column rows (bit x of row y)
     uint2 *pnz;              // ... and per agent the plane sets whose HBM copy may be nonzero (x: rows y', y: cols x')
+    int wrec_k;              // step launches of at most wrec_k steps write the window record (VOXNAV_ENV_WREC);
+                             // the records follow the hot state in its allocation (wrec_base)
 };
 
 __device__ __forceinline__ Agent unpack(uint4 s) {

@@ -156,9 +156,21 @@ __device__ __forceinline__ bool col_differs(const Col<PH> &a, const Col<PH> &b) 
     return d;
 }
 
+// Column index of (x, y) in the bricked map: bricks of 4 x 4 columns, x-major;
+// inside a brick y fast ((x & 3) << 2 | (y & 3)), or x fast with VN_BRICK_T
+// (diagnostics: a lane's 4 window columns -- one y, 4 consecutive x -- are
+// then contiguous in the brick row).
+#ifndef VN_BRICK_T
+#define VN_BRICK_T 0
+#endif
+__host__ __device__ __forceinline__ uint32_t bcol(int x, int y, int nby) {
+    const uint32_t in = VN_BRICK_T ? (uint32_t)(((y & 3) << 2) | (x & 3)) : (uint32_t)(((x & 3) << 2) | (y & 3));
+    return ((uint32_t)((x >> 2) * nby + (y >> 2)) << 4) + in;
+}
+
 template <int PH>
 __device__ __forceinline__ uint32_t boff(int x, int y, int z, int nby) {
-    return (uint32_t)((((((x >> 2) * nby + (y >> 2)) << 4) + ((x & 3) << 2) + (y & 3)) * PH) + z);
+    return bcol(x, y, nby) * (uint32_t)PH + (uint32_t)z;
 }
 
 // Destination of the observation row.  With auto-reset, a step that ends the
@@ -516,6 +528,88 @@ __device__ __forceinline__ void tile_flush(const Params &p, int8_t *map, const u
             col_store<PH>(map + boff<PH>(cx, cy, 0, p.nby), c);
         }
     }
+}
+
+// Window record (VOXNAV_ENV_WREC): a launch of at most p.wrec_k steps ends by
+// storing the agent's 16 tile columns contiguously (16 x PH bytes, in tile
+// slot order) and sets HOT_WREC in the hot state; the next launch then fills
+// its tile from that record -- 2 (PH 8) / 4 (PH 16) 16-B loads per lane, whole
+// 64-B pieces -- instead of 16 column loads spread over the bricks (a PH-16
+// brick row puts a lane's 4 columns in 4 different 64-B pieces), and loads
+// only the 4 columns the premoved step 0 brings into the window.  The byte
+// map stays complete (tile_flush still writes the dirty columns back), so the
+// record is a copy: every launch that does not write it clears HOT_WREC
+// (pack() leaves bit 30 clear), and only a record written for the agent's
+// current (x, y) is ever read.  What the one-step call gains is what its
+// fill cost (the collector's policy-in-the-loop env call, reference
+// envs/CubicEnv.py:110-132 per SubprocVecEnv worker).
+constexpr uint32_t HOT_WREC = 1u << 30;
+constexpr int PRIO_WREC_SAVE = 128;    // Params::prio bits set by the host: this launch writes the records,
+constexpr int PRIO_WREC_EARLY = 256;   // ... and the previous step launch wrote them (load each with the state)
+
+// the records sit behind the hot state in its allocation: no pointer of
+// their own stays live across the step loop (SGPR pressure)
+__device__ __forceinline__ uint64_t *wrec_base(const Params &p) { return reinterpret_cast<uint64_t *>(p.hot + p.N); }
+
+template <int PH>
+struct WrecV {
+    uint4 v[16 * PH / 64];               // lane q's 16-B pieces of the record (piece j: bytes 64 j + 16 q)
+};
+
+template <int PH>
+__device__ __forceinline__ void wrec_load(const Params &p, int agent, int q, WrecV<PH> &w) {
+    const uint4 *src = reinterpret_cast<const uint4 *>(wrec_base(p) + (size_t)agent * (2 * PH));
+#pragma unroll
+    for (int j = 0; j < 16 * PH / 64; ++j) w.v[j] = src[4 * j + q];
+}
+
+template <int PH>
+__device__ __forceinline__ void wrec_store(const Params &p, const uint64_t *tile, int agent, int q) {
+    constexpr int NI = 16 * PH / 64;           // 16-B pieces per lane
+    uint4 *dst = reinterpret_cast<uint4 *>(wrec_base(p) + (size_t)agent * (2 * PH));
+#pragma unroll
+    for (int j = 0; j < NI; ++j) {
+        const uint64_t a = tile[8 * j + 2 * q], b = tile[8 * j + 2 * q + 1];
+        dst[4 * j + q] = make_uint4((uint32_t)a, (uint32_t)(a >> 32), (uint32_t)b, (uint32_t)(b >> 32));
+    }
+}
+
+// The tile from the record written around g0 (the launch's start cell), then
+// the columns entering the window of gf (step 0's premoved cell; at most one
+// horizontal move away).  No write-back: the map holds every record column.
+template <int PH, bool PC, typename RT, bool SB>
+__device__ __forceinline__ void wrec_fill(const Params &p, const int8_t *map, uint64_t *tile, const RT *ps,
+                                          const Agent &g0, const Agent &gf, const Room &R, int q, const Stood &st,
+                                          const WrecV<PH> &w) {
+    constexpr int NI = 16 * PH / 64;
+    const bool shifted = gf.x != g0.x || gf.y != g0.y;
+    int ex = 0, ey = 0;
+    Col<PH> c;
+    col_zero<PH>(c);
+    if (shifted) {
+        if (gf.x != g0.x) {
+            ex = gf.x > g0.x ? gf.x + 1 : gf.x - 2;
+            ey = gf.y + q - 2;
+        } else {
+            ex = gf.x + q - 2;
+            ey = gf.y > g0.y ? gf.y + 1 : gf.y - 2;
+        }
+        if (ex >= 0 && ex < R.W && ey >= 0 && ey < R.D) {
+            const bool stood = !SB || ((st.row[ey] >> ex) & 1u);
+            col_load<PH>((stood ? map : room_image(p.wimg, gf.room, p.map_bytes)) + boff<PH>(ex, ey, 0, p.nby), c);
+            if constexpr (PC) c.w[0] |= pset_known(ps, ex, ey);
+        }
+    }
+#pragma unroll
+    for (int j = 0; j < NI; ++j) {
+        tile[8 * j + 2 * q] = (uint64_t)w.v[j].x | ((uint64_t)w.v[j].y << 32);
+        tile[8 * j + 2 * q + 1] = (uint64_t)w.v[j].z | ((uint64_t)w.v[j].w << 32);
+    }
+    // the record's slots are written by all 4 lanes: complete before a lane
+    // overwrites an entering slot and before the sensing reads other lanes' slots
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+    if (shifted) tile_write<PH>(tile, tslot(ex, ey), c);
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
 }
 
 // After a horizontal move in axis dir (0 +x, 1 -x, 2 +y, 3 -y) to (x, y):
@@ -1194,6 +1288,9 @@ constexpr uint32_t kMoveDir = (2u << 0) | (0u << 2) | (3u << 4) | (1u << 6)     
 #ifndef VN_STAGE_OBS
 #define VN_STAGE_OBS 1
 #endif
+#ifndef VN_WREC_K_DEFAULT
+#define VN_WREC_K_DEFAULT 1  // VOXNAV_ENV_WREC when unset: launches of at most this many steps write the window record
+#endif
 #ifndef VN_DFLUSH_DEFAULT
 #define VN_DFLUSH_DEFAULT 1  // VOXNAV_ENV_DFLUSH when unset: bit 0 byte-mark kernels, bit 1 plane-set kernels
 #endif
@@ -1290,6 +1387,11 @@ __global__ __launch_bounds__((PCM == 1 || PCM == 2) ? VN_PC_BLOCK : BLOCK,
     // the agent's state loads are in flight while the block stages its LUT
     const uint4 hot0 = p.hot[ai];
     uint32_t next_seed = p.next_seed[ai];
+    const bool wvalid = hot0.x & HOT_WREC;                // the window record holds the start cell's window
+    // the record loaded beside the state when the previous step launch wrote them (the host's bit)
+    const bool wearly = !RESET_ONLY && (p.prio & PRIO_WREC_EARLY);
+    WrecV<PH> wv;
+    if (wearly) wrec_load<PH>(p, ai, q, wv);
     // SB: lane q's share of the stood rows (8q .. 8q + 7) and the nonzero-set masks.
     // A short launch (VN_STOOD_PART, K <= 8) can only reach the rows y - 2 - K ..
     // y + 1 + K: the shares outside them are not loaded (they stay zero in LDS,
@@ -1427,7 +1529,12 @@ __global__ __launch_bounds__((PCM == 1 || PCM == 2) ? VN_PC_BLOCK : BLOCK,
         }
         if (!(VN_ABLATE & 16384u)) {   // diagnostics: 16384 skips the launch's fill
             if (PC) pset_fill<RT, SB>(p, map, ps, gf, R, q, st);
-            tile_fill<PH, PC, RT, SB>(p, map, tile, ps, gf, R, q, st);
+            if (wvalid) {                          // the window record of the start cell (wrec_fill)
+                if (!wearly) wrec_load<PH>(p, i, q, wv);
+                wrec_fill<PH, PC, RT, SB>(p, map, tile, ps, g, gf, R, q, st, wv);
+            } else {
+                tile_fill<PH, PC, RT, SB>(p, map, tile, ps, gf, R, q, st);
+            }
         }
     }
 #if VN_ENV_PROF
@@ -1710,9 +1817,16 @@ __global__ __launch_bounds__((PCM == 1 || PCM == 2) ? VN_PC_BLOCK : BLOCK,
             tile_flush<PH>(p, map, tile, g, R, dirty, q);
             if (PC) pset_flush<RT, SB>(p, map, ps, g, R, pdirty, q, st);
         }
+        const bool wsave = p.prio & PRIO_WREC_SAVE;     // the window record for the next launch (host: K <= wrec_k)
         if (q == 0) {
-            p.hot[i] = pack(g);
+            uint4 h = pack(g);
+            if (wsave) h.x |= HOT_WREC;
+            p.hot[i] = h;
             p.next_seed[i] = next_seed;
+        }
+        if (wsave) {
+            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");   // the slots other lanes wrote
+            wrec_store<PH>(p, tile, i, q);
         }
     }
     if (SB) {
@@ -1791,7 +1905,7 @@ __global__ void export_belief_kernel(Params p, int8_t *out, int pw, int pd) {
     const Room R = load_room(p, g.room);
     int8_t v = -128;
     if (x < R.W && y < R.D && z < R.H) {
-        const uint32_t off = (uint32_t)((((((x >> 2) * p.nby + (y >> 2)) << 4) + ((x & 3) << 2) + (y & 3)) * p.ph) + z);
+        const uint32_t off = bcol(x, y, p.nby) * (uint32_t)p.ph + (uint32_t)z;
         const int8_t *m = p.belief + (size_t)i * p.agent_bytes;
         const uint32_t b = (uint8_t)m[off];
         // a cell is known if its byte says so or a marked-bit plane holds it
@@ -1879,6 +1993,7 @@ struct VnEnv {
     int8_t *d_wimg = nullptr;
     float *d_scratch = nullptr;   // 8 KiB: targets of dummy output stores (the deferred flush's first step)
     uint32_t *d_stood = nullptr;  // PCM 2: per agent 32 stood rows, then per agent the nonzero-set masks (uint2)
+    bool wrec_written = false;    // the last step launch wrote every agent's window record (wrec_fill)
     // the belief allocation (d_belief may sit at an offset inside it: placement study knobs, vn_create)
     void *belief_alloc = nullptr;
     size_t belief_alloc_bytes = 0;
@@ -1953,6 +2068,10 @@ Params base_params(VnEnv *e) {
     p.scratch = e->d_scratch;
     p.stood = e->d_stood;
     p.pnz = e->d_stood ? reinterpret_cast<uint2 *>(e->d_stood + (size_t)e->N * 32u) : nullptr;
+    {   // read per call (scripts/ab_same.py): launches of at most this many steps write the window record
+        const char *ew = std::getenv("VOXNAV_ENV_WREC");
+        p.wrec_k = ew ? std::atoi(ew) : VN_WREC_K_DEFAULT;
+    }
     return p;
 }
 
@@ -1975,20 +2094,21 @@ int launch_ph(int N, hipStream_t s, const Params &p) {
     const bool fast = p.reward && p.term && p.trunc && !p.actions_out;
     constexpr bool CAP = pcm_dfl_capable(PCM);
     const bool dfl = CAP && !RESET_ONLY && use_dfl(PCM, N, p.K, p.dflush);
+    const Params &pl = p;
     if (RESET_ONLY)
-        hipLaunchKernelGGL((env_kernel<PH, false, false, true, PCM>), grid, block, 0, s, p);
+        hipLaunchKernelGGL((env_kernel<PH, false, false, true, PCM>), grid, block, 0, s, pl);
     else if (p.actions && fast)
-        hipLaunchKernelGGL((env_kernel<PH, true, true, false, PCM>), grid, block, 0, s, p);
+        hipLaunchKernelGGL((env_kernel<PH, true, true, false, PCM>), grid, block, 0, s, pl);
     else if (p.actions)
-        hipLaunchKernelGGL((env_kernel<PH, true, false, false, PCM>), grid, block, 0, s, p);
+        hipLaunchKernelGGL((env_kernel<PH, true, false, false, PCM>), grid, block, 0, s, pl);
     else if (fast && dfl)
-        hipLaunchKernelGGL((env_kernel<PH, false, true, false, PCM, CAP>), grid, block, 0, s, p);
+        hipLaunchKernelGGL((env_kernel<PH, false, true, false, PCM, CAP>), grid, block, 0, s, pl);
     else if (fast)
-        hipLaunchKernelGGL((env_kernel<PH, false, true, false, PCM>), grid, block, 0, s, p);
+        hipLaunchKernelGGL((env_kernel<PH, false, true, false, PCM>), grid, block, 0, s, pl);
     else if (dfl)
-        hipLaunchKernelGGL((env_kernel<PH, false, false, false, PCM, CAP>), grid, block, 0, s, p);
+        hipLaunchKernelGGL((env_kernel<PH, false, false, false, PCM, CAP>), grid, block, 0, s, pl);
     else
-        hipLaunchKernelGGL((env_kernel<PH, false, false, false, PCM>), grid, block, 0, s, p);
+        hipLaunchKernelGGL((env_kernel<PH, false, false, false, PCM>), grid, block, 0, s, pl);
     VN_HIP(hipGetLastError());
     return VN_OK;
 }
@@ -2002,10 +2122,33 @@ static int env_pcm(const VnEnv *e) {
 }
 
 template <bool RESET_ONLY>
+int launch_pcm(VnEnv *e, int pcm, const Params &p, hipStream_t s);
+
+// VOXNAV_ENV_WREC_EARLY (read per call; default 1): the window record loaded
+// beside the hot state instead of after it (one dependent round trip less)
+static bool wrec_early() {
+    const char *ev = std::getenv("VOXNAV_ENV_WREC_EARLY");
+    return ev ? std::atoi(ev) != 0 : true;
+}
+
+template <bool RESET_ONLY>
 int launch_env(VnEnv *e, const Params &p, hipStream_t s) {
     if (e->variant == VN_VARIANT_SIMPLE)
         return vn_simple::launch(RESET_ONLY, e->sline, e->sbits, e->cfg.local_map_length, e->N, e->obs_dim, &p, s);
     const int pcm = env_pcm(e);
+    // the window records (wrec_fill): written by step launches of at most
+    // wrec_k steps, loaded beside the state when the previous launch wrote them
+    Params pw = p;
+    if (!RESET_ONLY) {
+        if (p.K <= p.wrec_k) pw.prio |= PRIO_WREC_SAVE;
+        if (e->wrec_written && wrec_early()) pw.prio |= PRIO_WREC_EARLY;
+    }
+    e->wrec_written = !RESET_ONLY && p.K <= p.wrec_k;
+    return launch_pcm<RESET_ONLY>(e, pcm, pw, s);
+}
+
+template <bool RESET_ONLY>
+int launch_pcm(VnEnv *e, int pcm, const Params &p, hipStream_t s) {
     if (e->ph == 8) {
         if (pcm == 2) return launch_ph<8, RESET_ONLY, 2>(e->N, s, p);
         if (pcm == 1) return launch_ph<8, RESET_ONLY, 1>(e->N, s, p);
@@ -2301,7 +2444,8 @@ int vn_create(const VnRoomSet *rooms, int32_t n_agents, const VnConfig *cfg, int
     VN_ALLOC(e->d_rays, rays.size() * sizeof(uint2));
     VN_ALLOC(e->d_starts, starts.size() * sizeof(uint32_t));
     VN_ALLOC(e->d_lut, sizeof(lut));
-    VN_ALLOC(e->d_hot, (size_t)n_agents * sizeof(uint4));
+    // the hot state, then (CubicEnv) the window records: 16 columns x PH bytes per agent (wrec_base)
+    VN_ALLOC(e->d_hot, (size_t)n_agents * (sizeof(uint4) + (e->variant != VN_VARIANT_SIMPLE ? 16u * (size_t)e->ph : 0u)));
     VN_ALLOC(e->d_seed, (size_t)n_agents * sizeof(uint32_t));
     {
         // The belief maps (placement study knobs, diagnostics: VOXNAV_BELIEF_OFFSET
@@ -2387,7 +2531,7 @@ int vn_create(const VnRoomSet *rooms, int32_t n_agents, const VnConfig *cfg, int
                 for (int y = 0; y < D; ++y)
                     for (int z = 0; z < H; ++z)
                         if (rooms->walls[wo + ((size_t)x * D + y) * H + z])
-                            m[(((((x >> 2) * e->nby + (y >> 2)) << 4) + ((x & 3) << 2) + (y & 3)) * e->ph) + z] = 0x40;
+                            m[bcol(x, y, e->nby) * (size_t)e->ph + z] = 0x40;
             wo += (size_t)W * D * H;
             for (int c = 1; c < VN_WIMG_REP; ++c) std::memcpy(m + (size_t)c * e->map_bytes, m, e->map_bytes);
         }
