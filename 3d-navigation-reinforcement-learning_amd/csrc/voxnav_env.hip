@@ -255,6 +255,9 @@ __device__ __forceinline__ bool mark_w(uint32_t &w, const Rays &ry, int r, int s
 #ifndef VN_STOOD
 #define VN_STOOD 1
 #endif
+#ifndef VN_DM_CODES
+#define VN_DM_CODES 1        // byte-mark kernels stage obs rows as code words too (1.25 instead of 5 KiB of LDS per wave)
+#endif
 #ifndef VN_STOOD_PART
 #define VN_STOOD_PART 1      // launches of <= 8 steps load only the stood-row shares they can reach
 #endif
@@ -543,6 +546,9 @@ __device__ __forceinline__ void tile_flush(const Params &p, int8_t *map, const u
 // current (x, y) is ever read.  What the one-step call gains is what its
 // fill cost (the collector's policy-in-the-loop env call, reference
 // envs/CubicEnv.py:110-132 per SubprocVecEnv worker).
+#ifndef VN_WREC
+#define VN_WREC 1
+#endif
 constexpr uint32_t HOT_WREC = 1u << 30;
 constexpr int PRIO_WREC_SAVE = 128;    // Params::prio bits set by the host: this launch writes the records,
 constexpr int PRIO_WREC_EARLY = 256;   // ... and the previous step launch wrote them (load each with the state)
@@ -1060,7 +1066,8 @@ __device__ __forceinline__ int sense_observe(const Params &p, int8_t *map, uint6
                    : dst.stage     ? nullptr
                                    : reinterpret_cast<float4 *>(dst.row);
     float4 tail;                                                  // obs[64 + 4q .. +3]
-    if (PC && to_stage) {
+    constexpr bool CW = PC || (DM && VN_DM_CODES);   // code-word staging (below)
+    if (CW && to_stage) {
         tail = make_float4(0.f, 0.f, 0.f, 0.f);       // obs[72] is the agent's LUT entry (below)
     } else if (q == 0) {
         tail = make_float4(g.facing == 0 ? 1.0f : 0.0f, g.facing == 1 ? 1.0f : 0.0f, g.facing == 2 ? 1.0f : 0.0f,
@@ -1073,7 +1080,7 @@ __device__ __forceinline__ int sense_observe(const Params &p, int8_t *map, uint6
     } else {
         tail = make_float4(0.f, 0.f, 0.f, 0.f);
     }
-    if (to_stage && PC) {
+    if (to_stage && CW) {
         // the row's 20 code words: window bytes in obs order, then lane q's tail word
         LdsU32 *l = (LdsU32 *)dst.stage + dst.aslot * 20;
 #pragma unroll
@@ -1360,11 +1367,12 @@ __global__ __launch_bounds__((PCM == 1 || PCM == 2) ? VN_PC_BLOCK : BLOCK,
     constexpr bool DM = PCM == 3;                // byte-mark mode, deferred plane marks
     using RT = typename std::conditional<PCM == 2, uint32_t, uint64_t>::type;
     constexpr int kAgents = (PC ? VN_PC_BLOCK : BLOCK) / GROUP;
-    static_assert(!PC || kAgents <= 64, "tc_slot has 64 obs[72] codes per block");
+    constexpr bool CW = PC || (DM && VN_DM_CODES);     // obs staged as code words (STAGE_WORDS), expanded at the flush
+    static_assert(!CW || kAgents <= 64, "tc_slot has 64 obs[72] codes per block");
     __shared__ float tab[TAB_SIZE];
     __shared__ __attribute__((aligned(16))) uint64_t tiles[kAgents * TileGeom<PH>::STRIDE];
     // obs rows of the step, staged per wave (STAGE_WORDS) so HBM sees 1 KiB contiguous stores
-    constexpr int kStageWords = PC ? STAGE_WORDS : STAGE_WORDS_F;
+    constexpr int kStageWords = CW ? STAGE_WORDS : STAGE_WORDS_F;
     __shared__ __attribute__((aligned(16))) uint32_t stage[(kAgents / 16) * kStageWords];
     __shared__ __attribute__((aligned(16))) RT psets[PC ? kAgents * PsetGeom<RT>::STRIDE : 2];
     constexpr bool SB = PCM == 2 && VN_STOOD;
@@ -1387,9 +1395,9 @@ __global__ __launch_bounds__((PCM == 1 || PCM == 2) ? VN_PC_BLOCK : BLOCK,
     // the agent's state loads are in flight while the block stages its LUT
     const uint4 hot0 = p.hot[ai];
     uint32_t next_seed = p.next_seed[ai];
-    const bool wvalid = hot0.x & HOT_WREC;                // the window record holds the start cell's window
+    const bool wvalid = VN_WREC && (hot0.x & HOT_WREC);   // the window record holds the start cell's window
     // the record loaded beside the state when the previous step launch wrote them (the host's bit)
-    const bool wearly = !RESET_ONLY && (p.prio & PRIO_WREC_EARLY);
+    const bool wearly = VN_WREC && !RESET_ONLY && (p.prio & PRIO_WREC_EARLY);
     WrecV<PH> wv;
     if (wearly) wrec_load<PH>(p, ai, q, wv);
     // SB: lane q's share of the stood rows (8q .. 8q + 7) and the nonzero-set masks.
@@ -1489,7 +1497,12 @@ __global__ __launch_bounds__((PCM == 1 || PCM == 2) ? VN_PC_BLOCK : BLOCK,
     constexpr bool PREMOVE = VN_PREMOVE;
     uint32_t a16[4] = {0u, 0u, 0u, 0u};          // VN_PHILOX16: the actions of the current 16-step chunk
     auto philox_chunk = [&](uint64_t tb) {
-        const uint4 o = philox4x32_10(p.policy_seed, p.gid_base + (uint64_t)ai, ((tb >> 2) & ~3ull) + (uint64_t)q);
+        // the agent index through an opaque copy: the compiler would otherwise
+        // hoist the loop-invariant first Philox round out of the step loop and
+        // keep (or spill) its 64-bit products across it
+        int aio = ai;
+        asm volatile("" : "+v"(aio));
+        const uint4 o = philox4x32_10(p.policy_seed, p.gid_base + (uint64_t)aio, ((tb >> 2) & ~3ull) + (uint64_t)q);
         const uint32_t mine = __umulhi(o.x, 6u) | (__umulhi(o.y, 6u) << 8) | (__umulhi(o.z, 6u) << 16) |
                               (__umulhi(o.w, 6u) << 24);
         a16[0] = group_bcast<0>(mine);
@@ -1684,7 +1697,7 @@ __global__ __launch_bounds__((PCM == 1 || PCM == 2) ? VN_PC_BLOCK : BLOCK,
             // block included) ahead of the five stores
             if constexpr (DFL) {
                 asm volatile("" ::: "memory");
-                wave_obs_flush<PC, true>(p, wst, tab, k - 1, wave_agent0, nvalid, lane, abl_sink, bprio);
+                wave_obs_flush<CW, true>(p, wst, tab, k - 1, wave_agent0, nvalid, lane, abl_sink, bprio);
             }
             ENV_T(0);
             if (shifted) {
@@ -1779,7 +1792,7 @@ __global__ __launch_bounds__((PCM == 1 || PCM == 2) ? VN_PC_BLOCK : BLOCK,
             if (need) next_seed = seed + p.seed_stride;
         }
         ENV_T(4);
-        if constexpr (!DFL) wave_obs_flush<PC>(p, wst, tab, k, wave_agent0, nvalid, lane, abl_sink, bprio);
+        if constexpr (!DFL) wave_obs_flush<CW>(p, wst, tab, k, wave_agent0, nvalid, lane, abl_sink, bprio);
         ENV_T(5);
     }
     if constexpr (STRIPE_R) {
@@ -1806,7 +1819,7 @@ __global__ __launch_bounds__((PCM == 1 || PCM == 2) ? VN_PC_BLOCK : BLOCK,
         ENV_T(6);
     }
     }
-    if constexpr (DFL) wave_obs_flush<PC, true>(p, wst, tab, p.K - 1, wave_agent0, nvalid, lane, abl_sink, bprio);      // the launch's last step's rows
+    if constexpr (DFL) wave_obs_flush<CW, true>(p, wst, tab, p.K - 1, wave_agent0, nvalid, lane, abl_sink, bprio);      // the launch's last step's rows
     }
     if (active) {
         if constexpr (DM) {
@@ -1817,7 +1830,7 @@ __global__ __launch_bounds__((PCM == 1 || PCM == 2) ? VN_PC_BLOCK : BLOCK,
             tile_flush<PH>(p, map, tile, g, R, dirty, q);
             if (PC) pset_flush<RT, SB>(p, map, ps, g, R, pdirty, q, st);
         }
-        const bool wsave = p.prio & PRIO_WREC_SAVE;     // the window record for the next launch (host: K <= wrec_k)
+        const bool wsave = VN_WREC && (p.prio & PRIO_WREC_SAVE);   // the window record for the next launch (host: K <= wrec_k)
         if (q == 0) {
             uint4 h = pack(g);
             if (wsave) h.x |= HOT_WREC;
