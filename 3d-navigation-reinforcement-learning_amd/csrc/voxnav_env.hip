@@ -157,14 +157,17 @@ __device__ __forceinline__ bool col_differs(const Col<PH> &a, const Col<PH> &b) 
 }
 
 // Column index of (x, y) in the bricked map: bricks of 4 x 4 columns, x-major;
-// inside a brick y fast ((x & 3) << 2 | (y & 3)), or x fast with VN_BRICK_T
+// inside a brick y fast ((x & 3) << 2 | (y & 3)), or x fast with VN_BRICK_T 1
 // (diagnostics: a lane's 4 window columns -- one y, 4 consecutive x -- are
-// then contiguous in the brick row).
+// then contiguous in the brick row), or 2 x 2 sub-bricks with VN_BRICK_T 2
+// (a PH-16 64-B piece holds a 2 x 2 block of columns).
 #ifndef VN_BRICK_T
 #define VN_BRICK_T 0
 #endif
 __host__ __device__ __forceinline__ uint32_t bcol(int x, int y, int nby) {
-    const uint32_t in = VN_BRICK_T ? (uint32_t)(((y & 3) << 2) | (x & 3)) : (uint32_t)(((x & 3) << 2) | (y & 3));
+    const uint32_t in = VN_BRICK_T == 2 ? (uint32_t)(((x & 2) << 2) | ((y & 2) << 1) | ((x & 1) << 1) | (y & 1))
+                        : VN_BRICK_T ? (uint32_t)(((y & 3) << 2) | (x & 3))
+                                     : (uint32_t)(((x & 3) << 2) | (y & 3));
     return ((uint32_t)((x >> 2) * nby + (y >> 2)) << 4) + in;
 }
 
@@ -2010,8 +2013,6 @@ struct VnEnv {
     // the belief allocation (d_belief may sit at an offset inside it: placement study knobs, vn_create)
     void *belief_alloc = nullptr;
     size_t belief_alloc_bytes = 0;
-    bool belief_vmm = false;
-    hipMemGenericAllocationHandle_t belief_handle{};
 };
 
 namespace {
@@ -2196,13 +2197,7 @@ void free_env(VnEnv *e) {
     (void)hipFree(e->d_lut);
     (void)hipFree(e->d_hot);
     (void)hipFree(e->d_seed);
-    if (e->belief_vmm) {
-        (void)hipMemUnmap(e->belief_alloc, e->belief_alloc_bytes);
-        (void)hipMemAddressFree(e->belief_alloc, e->belief_alloc_bytes);
-        (void)hipMemRelease(e->belief_handle);
-    } else {
-        (void)hipFree(e->belief_alloc);
-    }
+    (void)hipFree(e->belief_alloc);
     (void)hipFree(e->d_err);
     (void)hipFree(e->d_envc);
     (void)hipFree(e->d_goal);
@@ -2461,54 +2456,18 @@ int vn_create(const VnRoomSet *rooms, int32_t n_agents, const VnConfig *cfg, int
     VN_ALLOC(e->d_hot, (size_t)n_agents * (sizeof(uint4) + (e->variant != VN_VARIANT_SIMPLE ? 16u * (size_t)e->ph : 0u)));
     VN_ALLOC(e->d_seed, (size_t)n_agents * sizeof(uint32_t));
     {
-        // The belief maps (placement study knobs, diagnostics: VOXNAV_BELIEF_OFFSET
-        // bytes into the allocation, VOXNAV_BELIEF_VMM=1 physical chunks of the
-        // VMM granularity mapped by hipMemCreate / hipMemMap instead of hipMalloc).
+        // The belief maps (placement study knob, diagnostics: VOXNAV_BELIEF_OFFSET
+        // bytes into the allocation).  A VMM-mapped variant (hipMemCreate /
+        // hipMemMap chunks) was measured in round 6 and removed: on that memory
+        // the kernels' results differed from the oracle (they rely on a wave's
+        // later load seeing its own earlier store of the same bytes, e.g. a blind
+        // mark read back by the next step's entering column), and it did not
+        // remove the P-set kernels' trial-to-trial swing.
         const char *bo = getenv("VOXNAV_BELIEF_OFFSET");
         const size_t off = bo ? (((size_t)atoll(bo)) + 255u) & ~(size_t)255u : 0;
-        const char *bv = getenv("VOXNAV_BELIEF_VMM");
         e->belief_alloc_bytes = belief_bytes + off;
-        if (bv && bv[0] == '1') {
-            hipMemAllocationProp prop{};
-            prop.type = hipMemAllocationTypePinned;
-            prop.location.type = hipMemLocationTypeDevice;
-            prop.location.id = device;
-            size_t gran = 0;
-            hipError_t ve = hipMemGetAllocationGranularity(&gran, &prop, hipMemAllocationGranularityRecommended);
-            if (ve == hipSuccess && gran == 0) gran = (size_t)2 << 20;
-            const size_t want = bv[1] == ':' ? (size_t)atoll(bv + 2) : 0;   // VOXNAV_BELIEF_VMM=1:<align>
-            const size_t align = want > gran ? want : gran;
-            e->belief_alloc_bytes = (e->belief_alloc_bytes + align - 1) / align * align;
-            if (ve == hipSuccess) ve = hipMemCreate(&e->belief_handle, e->belief_alloc_bytes, &prop, 0);
-            if (ve == hipSuccess) {
-                ve = hipMemAddressReserve(&e->belief_alloc, e->belief_alloc_bytes, align, nullptr, 0);
-                if (ve != hipSuccess) (void)hipMemRelease(e->belief_handle);
-            }
-            if (ve == hipSuccess) {
-                ve = hipMemMap(e->belief_alloc, e->belief_alloc_bytes, 0, e->belief_handle, 0);
-                if (ve != hipSuccess) {
-                    (void)hipMemAddressFree(e->belief_alloc, e->belief_alloc_bytes);
-                    (void)hipMemRelease(e->belief_handle);
-                }
-            }
-            if (ve == hipSuccess) {
-                e->belief_vmm = true;
-                hipMemAccessDesc acc{};
-                acc.location = prop.location;
-                acc.flags = hipMemAccessFlagsProtReadWrite;
-                ve = hipMemSetAccess(e->belief_alloc, e->belief_alloc_bytes, &acc, 1);
-            }
-            if (ve != hipSuccess) {
-                const bool mapped = e->belief_vmm;
-                if (!mapped) e->belief_alloc = nullptr;
-                free_env(e);
-                return fail(VN_ERR_OOM, "VMM belief allocation (%zu B): %s", (size_t)belief_bytes, hipGetErrorString(ve));
-            }
-        } else {
-            VN_ALLOC(e->belief_alloc, e->belief_alloc_bytes);
-        }
+        VN_ALLOC(e->belief_alloc, e->belief_alloc_bytes);
         e->d_belief = reinterpret_cast<int8_t *>(e->belief_alloc) + off;
-        e->device_bytes += e->belief_vmm ? e->belief_alloc_bytes : 0;
     }
     VN_ALLOC(e->d_err, sizeof(int32_t));
     VN_ALLOC(e->d_envc, sizeof(EnvConst));
