@@ -461,6 +461,52 @@ def test_launch_mix_belief_matches_oracle(voxnav, monkeypatch, pcache, defer, sr
         np.testing.assert_array_equal(b[a, :W, :D, :H], np.minimum(orc_env.belief(a), 63), err_msg=f"agent {a}")
 
 
+WREC_CASES = [("box:32x32x8", 10, 64, "2"), ("box:16x16x8", 7, 48, "0"), ("set:P3_training", 10, 64, "3"),
+              ("box:100x40x8", 10, 32, "0")]
+# window record settings: (VOXNAV_ENV_WREC: launches of at most this many steps write it, VOXNAV_ENV_WREC_EARLY)
+WREC_MODES = [("1", "1"), ("8", "1"), ("8", "0"), ("0", "1")]
+
+
+@pytest.mark.parametrize("wrec,early", WREC_MODES, ids=[f"wrec{a}-early{b}" for a, b in WREC_MODES])
+@pytest.mark.parametrize("src,L,N,pcache", WREC_CASES, ids=[f"{c[0]}-pc{c[3]}" for c in WREC_CASES])
+def test_window_record_launch_mix_matches_oracle(voxnav, monkeypatch, wrec, early, src, L, N, pcache):
+    """The window record (csrc/voxnav_env.hip wrec_fill): a step launch of at
+    most VOXNAV_ENV_WREC steps stores the agent's 16 window columns and the
+    next launch fills its window from them (loaded beside the state with
+    VOXNAV_ENV_WREC_EARLY=1).  Runs of one-step launches (record -> record),
+    short launches that write it and long ones that do not (their next launch
+    falls back to the map; the P3 set's small rooms end episodes inside the
+    76 steps, so auto-resets run between records): obs, f64 rewards, flags
+    and every agent's belief map equal the oracle's, in each belief mode
+    (pcache "3": the mode the room set selects; "0" forces byte marks)."""
+    monkeypatch.setenv("VOXNAV_ENV_WREC", wrec)
+    monkeypatch.setenv("VOXNAV_ENV_WREC_EARLY", early)
+    if pcache != "3":
+        monkeypatch.setenv("VOXNAV_PCACHE", pcache)
+    env = make_env(voxnav, src, L, n=N, autoreset=True)
+    env.reset(seed=42)
+    ks = [1, 1, 1, 5, 1, 1, 16, 1, 2, 1, 1, 8, 1, 30, 1, 1]
+    obs, rew, te, tr = [], [], [], []
+    for k in ks:
+        ro = env.step_random(k, policy_seed=7, reward_f64=True)
+        obs.append(ro.obs.cpu().numpy())
+        rew.append(ro.reward.cpu().numpy())
+        te.append(ro.terminated.cpu().numpy())
+        tr.append(ro.truncated.cpu().numpy())
+    orc_env = oracle_env(src, L, n_agents=N)
+    orc = orc_env.run_random(42 + np.arange(N, dtype=np.int64), policy_seed=7, K=sum(ks), seed_stride=N)
+    assert np.concatenate(obs).tobytes() == orc["obs"].tobytes()
+    np.testing.assert_array_equal(np.concatenate(rew), orc["reward"])
+    np.testing.assert_array_equal(np.concatenate(te), orc["terminated"])
+    np.testing.assert_array_equal(np.concatenate(tr), orc["truncated"])
+    b = env.belief().cpu().numpy().astype(np.int64)
+    st = env.export_state().cpu().numpy()
+    rooms = env.room_set.rooms
+    for a in range(N):
+        W, D, H = rooms[int(st[a, 13])].shape
+        np.testing.assert_array_equal(b[a, :W, :D, :H], np.minimum(orc_env.belief(a), 63), err_msg=f"agent {a}")
+
+
 @pytest.mark.parametrize("src", ["box:32x32x8", "box:16x16x8"])
 def test_masked_reset_mid_episode_matches_fresh_env(voxnav, src):
     """vn_reset with a mask in the middle of an episode (plane-set mode with
