@@ -296,6 +296,23 @@ __global__ __launch_bounds__(256) void gemm_reduce_kernel(const float *__restric
     }
 }
 
+#ifndef VN_GEMM_ASM
+#define VN_GEMM_ASM 1        // gemm_dl_kernel: raw barriers + asm fragment reads (the double buffering kept)
+#endif
+typedef float gm_f4 __attribute__((ext_vector_type(4)));
+// the LDS offset of a __shared__ pointer (the low 32 bits of its flat address)
+__device__ __forceinline__ uint32_t lds_addr(const void *p) { return (uint32_t)(uintptr_t)p; }
+__device__ __forceinline__ gm_f4 lds_b128(uint32_t a) {
+    gm_f4 r;
+    asm volatile("ds_read_b128 %0, %1" : "=v"(r) : "v"(a) : "memory");
+    return r;
+}
+__device__ __forceinline__ float lds_b32(uint32_t a) {
+    float r;
+    asm volatile("ds_read_b32 %0, %1" : "=v"(r) : "v"(a) : "memory");
+    return r;
+}
+
 // ----------------------------------------------------------------------------
 // Direct-load variant (the aligned shapes of the learner: K per split a
 // multiple of GKD, 16-B aligned rows, 4-aligned k-major column counts).  Same
@@ -387,6 +404,125 @@ __global__ __launch_bounds__(256, 2) void gemm_dl_kernel(GemmArgs g) {
     const bool do_cs = g.colsum && A_KM && tn == 0 && wc == 0;
 
     if (nchunks > 0) issue(0, 0);
+#if VN_GEMM_ASM
+    // The chunk loop with raw barriers and the fragment reads in asm.  A
+    // __syncthreads() is a workgroup-scope fence, and the compiler drains
+    // vmcnt(0) before it -- and before any LDS read that may alias an LDS-DMA
+    // load in flight -- so the next chunk's loads were waited for before this
+    // chunk's MFMAs (no double buffering left).  Here the waits are explicit:
+    // before the barrier that opens chunk ch, this wave's loads of chunk ch
+    // landed (vmcnt leaves chunk ch + 1's in flight); the barrier then says
+    // every wave's did; before the barrier that frees a stage for the next
+    // chunk's loads, this wave's reads of it completed (lgkmcnt(0)).  The
+    // reads are asm (invisible to the compiler's wait insertion), so each read
+    // batch is waited for with lgkmcnt(0) and its registers tied after the wait.
+    constexpr int OPS = AGRAD ? 3 : 2;           // LDS-DMA loads per unit of a chunk
+    const uint32_t aA[2] = {lds_addr(sA[0]), lds_addr(sA[1])}, aB[2] = {lds_addr(sB[0]), lds_addr(sB[1])};
+    const uint32_t aY[2] = {AGRAD ? lds_addr(sY[0]) : 0u, AGRAD ? lds_addr(sY[AGRAD ? 1 : 0]) : 0u};
+    // byte offset of row-major unit (r, u) and of k-major value (c, s) in a stage
+    auto rm_off = [&](int r, int u) -> uint32_t { return (uint32_t)(r * NU + (u ^ ((r / RPB) % NU))) * 16u; };
+    auto km_off = [&](int c, int s) -> uint32_t {
+        const int k = 4 * (kh + 2 * (s >> 2)) + (s & 3);
+        return (uint32_t)((k * 32 + ((c >> 2) ^ (8 * kh))) * 4 + (c & 3)) * 4u;
+    };
+    struct PassRegs {
+        gm_f4 ra[2], rb[2], ry[2];               // row-major fragments (A, B, and Y for AGRAD)
+        float ka[2][4], kb[2][4], ky[2][4];      // k-major values
+    };
+    auto pass_read = [&](int st, int sq, PassRegs &R) {
+#pragma unroll
+        for (int f = 0; f < 2; ++f) {
+            if (!A_KM) {
+                const uint32_t o = rm_off(wr + 32 * f + col, kh + 2 * sq);
+                R.ra[f] = lds_b128(aA[st] + o);
+                if (AGRAD) R.ry[f] = lds_b128(aY[st] + o);
+            } else {
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    const uint32_t o = km_off(wr + 32 * f + col, 4 * sq + e);
+                    R.ka[f][e] = lds_b32(aA[st] + o);
+                    if (AGRAD) R.ky[f][e] = lds_b32(aY[st] + o);
+                }
+            }
+            if (!B_KM) {
+                R.rb[f] = lds_b128(aB[st] + rm_off(wc + 32 * f + col, kh + 2 * sq));
+            } else {
+#pragma unroll
+                for (int e = 0; e < 4; ++e) R.kb[f][e] = lds_b32(aB[st] + km_off(wc + 32 * f + col, 4 * sq + e));
+            }
+        }
+    };
+    // after lgkmcnt(0): tie the registers, so no use moves above the wait
+    auto pass_tie = [&](PassRegs &R) {
+#pragma unroll
+        for (int f = 0; f < 2; ++f) {
+            if (!A_KM) {
+                asm volatile("" : "+v"(R.ra[f]));
+                if (AGRAD) asm volatile("" : "+v"(R.ry[f]));
+            } else {
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    asm volatile("" : "+v"(R.ka[f][e]));
+                    if (AGRAD) asm volatile("" : "+v"(R.ky[f][e]));
+                }
+            }
+            if (!B_KM) {
+                asm volatile("" : "+v"(R.rb[f]));
+            } else {
+#pragma unroll
+                for (int e = 0; e < 4; ++e) asm volatile("" : "+v"(R.kb[f][e]));
+            }
+        }
+    };
+    auto pass_mfma = [&](const PassRegs &R) {
+        float av[2][4], bv[2][4];
+#pragma unroll
+        for (int f = 0; f < 2; ++f)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                float v = A_KM ? R.ka[f][e] : R.ra[f][e];
+                if (AGRAD) {
+                    const float y = A_KM ? R.ky[f][e] : R.ry[f][e];
+                    v = v * (1.0f - y * y);
+                }
+                av[f][e] = v;
+                if (A_KM && do_cs) csum[f] += v;
+                bv[f][e] = B_KM ? R.kb[f][e] : R.rb[f][e];
+            }
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[0][e], bv[0][e], acc[0][0], 0, 0, 0);
+            acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[0][e], bv[1][e], acc[0][1], 0, 0, 0);
+            acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[1][e], bv[0][e], acc[1][0], 0, 0, 0);
+            acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[1][e], bv[1][e], acc[1][1], 0, 0, 0);
+        }
+    };
+    for (int ch = 0; ch < nchunks; ++ch) {
+        const int st = ch & 1;
+        if (ch + 1 < nchunks) {
+            asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");   // stage st ^ 1 (chunk ch - 1) read by every wave
+            issue(ch + 1, st ^ 1);
+            asm volatile("s_waitcnt vmcnt(%0)" ::"n"(OPS * PER) : "memory");  // this wave's chunk-ch loads landed
+        } else {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        asm volatile("s_barrier" ::: "memory");                               // ... and every wave's
+        // pass sq + 1's reads in flight during pass sq's MFMAs
+        PassRegs rr[2];
+        pass_read(st, 0, rr[0]);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        pass_tie(rr[0]);
+#pragma unroll
+        for (int sq = 0; sq < GKD / 8; ++sq) {
+            if (sq + 1 < GKD / 8) pass_read(st, sq + 1, rr[(sq + 1) & 1]);
+            pass_mfma(rr[sq & 1]);
+            if (sq + 1 < GKD / 8) {
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                pass_tie(rr[(sq + 1) & 1]);
+            }
+        }
+    }
+#else
     for (int ch = 0; ch < nchunks; ++ch) {
         const int st = ch & 1;
         if (ch + 1 < nchunks) {
@@ -453,6 +589,7 @@ __global__ __launch_bounds__(256, 2) void gemm_dl_kernel(GemmArgs g) {
         }
         (void)fA; (void)fB; (void)fY;
     }
+#endif
     if (g.colsum && A_KM && tn == 0) {   // (block-uniform) lanes l, l ^ 32 hold the two k halves of column wr + 32 f + l % 32
         if (do_cs) {
 #pragma unroll
