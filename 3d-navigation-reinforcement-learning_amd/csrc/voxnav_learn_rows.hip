@@ -106,6 +106,27 @@ __device__ __forceinline__ bool wait_ge(uint32_t *cnt, uint32_t target, int32_t 
     return true;
 }
 
+// Block barrier for LDS data only.  With a global -> LDS (LDS-DMA) load in
+// flight __syncthreads() compiles to `s_waitcnt vmcnt(0) lgkmcnt(0); s_barrier`
+// (the DMA counts as an LDS write): the backward's h_{t-1} / x_t rows, issued
+// before the hand-off wait for the off-path weight gradients, then completed
+// in front of the step's partial-dh loads -- one more memory round trip on the
+// recurrence of the block that arrives last.  Those rows are waited for
+// explicitly where they are read.
+#ifndef VN_ROWS_RAWBAR
+#define VN_ROWS_RAWBAR 1
+#endif
+#ifndef VN_ROWS_PRELOAD
+#define VN_ROWS_PRELOAD 1
+#endif
+__device__ __forceinline__ void lds_barrier() {
+#if VN_ROWS_RAWBAR
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+#else
+    __syncthreads();
+#endif
+}
+
 // after this block's payload stores: drain (every wave), block barrier, one add
 __device__ __forceinline__ void publish(uint32_t *cnt) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -832,6 +853,9 @@ __global__ __launch_bounds__(256, 2) void lstm_rows_bwd2_kernel(RowsBwd a) {
     __shared__ uint8_t stf[RW];
     const int tid = threadIdx.x, lane = tid & 63;
     const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);   // partial: units 64 wv .. + 63; dW: gate wv
+    // wave wv's cell operands [7][8 rows][16 units] (3.5 KB, inside pst)
+    static_assert(4 * 7 * 8 * UB2 <= (RW / 2) * PP && UB2 == 16, "cell operands fit the pst area");
+    float *const cops = &pst[0][0] + 7 * 8 * UB2 * wv;
     const int q = lane >> 4, ci = lane & 15;
     int ub, g;
     rows2_map(a.NT, ub, g);
@@ -888,10 +912,30 @@ __global__ __launch_bounds__(256, 2) void lstm_rows_bwd2_kernel(RowsBwd a) {
                     (const __attribute__((address_space(1))) void *)(a.x + ((size_t)t * B + row) * D + 4 * lane),
                     (__attribute__((address_space(3))) void *)&xsl[rr][0], 16, 0, 0);
         }
+#if VN_ROWS_PRELOAD
+        // the step's own cell operands (dh_out, the 4 gates, c_{t-1}, c_t) need
+        // nothing from the group: global -> LDS before the hand-off wait, each
+        // wave the 8 rows its cell lanes read (so no barrier is needed, only the
+        // wave's own vmcnt), into the pst area (free until the partial below).
+        // The partial-dh loads are then the one round trip after the wait (from
+        // registers the compiler issued these behind that wait: 3 round trips;
+        // the kernel sits at 256 VGPRs).  Lanes 0-31 / 32-63: operands 2 k, 2 k + 1.
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const int op = 2 * k + (lane >> 5);
+            const int row = min(row0 + 8 * wv + ((lane >> 2) & 7), B - 1);
+            const size_t rb = ((size_t)l * L + t) * B + row;
+            const float *src = op == 0 ? a.dh_out + rb * H : op == 5 ? a.cprev + rb * H : op == 6 ? a.cnew + rb * H
+                                                                                               : a.act + rb * 4 * H + (op - 1) * H;
+            if (op < 7)
+                __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void *)(src + u0 + 4 * (lane & 3)),
+                                                 (__attribute__((address_space(3))) void *)(cops + 256 * k), 16, 0, 0);
+        }
+#endif
         if (a.prio) __builtin_amdgcn_s_setprio(2);   // the hand-off path up to the publish
         if (s > 0) {
             if (tid == 0) wait_ge(cnt, (uint32_t)(NUB2 * s), a.err);
-            __syncthreads();
+            lds_barrier();
         }
         float2 dG2[4] = {f2(0.0f), f2(0.0f), f2(0.0f), f2(0.0f)};
         bool st = true;
@@ -902,6 +946,13 @@ __global__ __launch_bounds__(256, 2) void lstm_rows_bwd2_kernel(RowsBwd a) {
 #pragma unroll
                 for (int k = 0; k < NUB2; ++k) dhr = dhr + ld_sc1_b64(prs, pofs((t + 1) & 1, k, er, eu));
             }
+#if VN_ROWS_PRELOAD
+            auto cop = [&](int op) {   // this lane's 2 units of operand op
+                return *reinterpret_cast<const float2 *>(cops + 128 * op + 16 * (lane >> 3) + 2 * eq);
+            };
+            const float2 dh = cop(0) + dhr;
+            const float2 ig = cop(1), fg = cop(2), gg = cop(3), og = cop(4), cp = cop(5), cn = cop(6);
+#else
             const size_t so = (((size_t)l * L + t) * B + erow) * H + eu;
             const float2 dh = *reinterpret_cast<const float2 *>(a.dh_out + so) + dhr;
             const float *pa = a.act + (((size_t)l * L + t) * B + erow) * 4 * H + eu;
@@ -910,6 +961,7 @@ __global__ __launch_bounds__(256, 2) void lstm_rows_bwd2_kernel(RowsBwd a) {
             const float2 og = *reinterpret_cast<const float2 *>(pa + 3 * H);
             const float2 cp = *reinterpret_cast<const float2 *>(a.cprev + so);
             const float2 cn = *reinterpret_cast<const float2 *>(a.cnew + so);
+#endif
 #define VN_CELLB2(c)                                                  \
     {                                                                 \
         const float tc = tanh_fast(cn.c);                             \
@@ -935,7 +987,7 @@ __global__ __launch_bounds__(256, 2) void lstm_rows_bwd2_kernel(RowsBwd a) {
 #pragma unroll
         for (int gq = 0; gq < 4; ++gq) *reinterpret_cast<float2 *>(&dgs[er][gq * UB2 + 2 * eq]) = dG2[gq];
         if (eq == 0) stf[er] = st ? 1 : 0;
-        __syncthreads();
+        __syncthreads();   // (a full one: every wave's operand DMA has landed before pst is reused)
         if (t > 0) {
             f32x4_t acc[2][4];
 #pragma unroll
