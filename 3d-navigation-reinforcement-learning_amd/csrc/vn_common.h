@@ -26,7 +26,7 @@
     defined(VN_LDS_BARRIER) || defined(VN_ROW_WB) || defined(VN_SETPRIO) || \
     defined(VN_SETPRIO_FLUSH) || defined(VN_ENV_WT) || defined(VN_DFLUSH_DEFAULT) || defined(VN_STOOD_PART) || defined(VN_WIMG_REP) || \
     defined(VN_BRICK_T) || defined(VN_WREC_K_DEFAULT) || defined(VN_WREC) || defined(VN_DM_CODES) || defined(VN_GEMM_ASM) || \
-    defined(VN_ROWS_RAWBAR) || defined(VN_ROWS_PRELOAD)
+    defined(VN_ROWS_RAWBAR) || defined(VN_ROWS_PRELOAD) || defined(VN_ROWS_FLAGS)
 #error "compile-time knobs are for the diagnostics build only (define VN_DIAG)"
 #endif
 #endif

@@ -119,6 +119,9 @@ __device__ __forceinline__ bool wait_ge(uint32_t *cnt, uint32_t target, int32_t 
 #ifndef VN_ROWS_PRELOAD
 #define VN_ROWS_PRELOAD 1
 #endif
+#ifndef VN_ROWS_FLAGS
+#define VN_ROWS_FLAGS 1
+#endif
 __device__ __forceinline__ void lds_barrier() {
 #if VN_ROWS_RAWBAR
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
@@ -226,13 +229,29 @@ __global__ __launch_bounds__(256, 1) void lstm_rows_fwd_kernel(RowsFwd a) {
     }
     __syncthreads();
 
+#if VN_ROWS_FLAGS
+    // the tile's sequence-start flags, double-buffered: step t reads stf[t & 1];
+    // step t + 1's are loaded at the top of step t and written to LDS after the
+    // step's h loads (whose wait completes them).  Consumed at the top of the
+    // same step (below), the load was waited for at once -- together with the
+    // previous step's 7 result stores -- in front of the x part.
+    __shared__ uint8_t stf2[2][RW];
+    if (tid < RW) stf2[0][tid] = row0 + tid < B ? 1 : 0;   // step 0: every row starts
+    const int frow = min(row0 + (tid & (RW - 1)), B - 1);
+#else
     __shared__ uint8_t stf[RW];       // the tile's sequence-start flags of the step
     // loaded a step ahead (a load consumed in the same step stalled the x part)
     uint8_t st_next = (tid < RW && row0 + tid < B) ? 1 : 0;
+#endif
     for (int t = 0; t < L; ++t) {
         const int xb = t & 1;
+#if VN_ROWS_FLAGS
+        const uint8_t *stf = stf2[t & 1];
+        const uint8_t st_ld = a.start[(size_t)min(t + 1, L - 1) * B + frow];
+#else
         if (tid < RW) stf[tid] = st_next;
         if (tid < RW && t + 1 < L) st_next = (row0 + tid < B && a.start[(size_t)(t + 1) * B + row0 + tid]) ? 1 : 0;
+#endif
         float4 xn[XPT];
         if (t + 1 < L) load_x(t + 1, xn);
         // the x part of the product (needs nothing from the group)
@@ -268,6 +287,9 @@ __global__ __launch_bounds__(256, 1) void lstm_rows_fwd_kernel(RowsFwd a) {
             const int f = tid + 256 * i;
             *reinterpret_cast<float4 *>(&hsl[f >> 6][4 * (f & 63)]) = hv[i];
         }
+#if VN_ROWS_FLAGS
+        if (tid < RW) stf2[(t + 1) & 1][tid] = (t + 1 < L && row0 + tid < B && st_ld) ? 1 : 0;
+#endif
         __syncthreads();
         // ... then the rows that start a sequence at t (all of them at t = 0)
         // take the buffer's stored state x keep: one row per 64 threads
@@ -399,7 +421,9 @@ __global__ __launch_bounds__(256, 2) void lstm_rows_fwd2_kernel(RowsFwd a) {
     __shared__ __attribute__((aligned(16))) float xs[2][RW][XP];
     __shared__ __attribute__((aligned(16))) float hsl[RW][HP];
     __shared__ __attribute__((aligned(16))) float gts[4][RW][GP];
+#if !VN_ROWS_FLAGS
     __shared__ uint8_t stf[RW];
+#endif
     const int tid = threadIdx.x, lane = tid & 63;
     const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);   // this wave's gate
     const int q = lane >> 4, ci = lane & 15;
@@ -469,12 +493,24 @@ __global__ __launch_bounds__(256, 2) void lstm_rows_fwd2_kernel(RowsFwd a) {
         a.diag[2 * gridDim.x + ((size_t)blockIdx.x * L + t) * 8 + (k_)] = (uint32_t)__builtin_amdgcn_s_memrealtime();
     // the tile's sequence-start flags, loaded a step ahead (a load consumed in
     // the same step stalled the x part behind its round trip)
+#if VN_ROWS_FLAGS
+    // (double-buffered in LDS as in lstm_rows_fwd_kernel)
+    __shared__ uint8_t stf2[2][RW];
+    if (tid < RW) stf2[0][tid] = row0 + tid < B ? 1 : 0;
+    const int frow = min(row0 + (tid & (RW - 1)), B - 1);
+#else
     uint8_t st_next = (tid < RW && row0 + tid < B) ? 1 : 0;
+#endif
     for (int t = 0; t < L; ++t) {
         const int xb = t & 1;
         VN_DMARK(0);
+#if VN_ROWS_FLAGS
+        const uint8_t *stf = stf2[t & 1];
+        const uint8_t st_ld = a.start[(size_t)min(t + 1, L - 1) * B + frow];
+#else
         if (tid < RW) stf[tid] = st_next;
         if (tid < RW && t + 1 < L) st_next = (row0 + tid < B && a.start[(size_t)(t + 1) * B + row0 + tid]) ? 1 : 0;
+#endif
         float4 xn[XPT];
         if (t + 1 < L) load_x(t + 1, xn);
         // the x part (needs nothing from the group): rows ci and 16 + ci
@@ -513,6 +549,9 @@ __global__ __launch_bounds__(256, 2) void lstm_rows_fwd2_kernel(RowsFwd a) {
             const int f = tid + 256 * i;
             *reinterpret_cast<float4 *>(&hsl[f >> 6][4 * (f & 63)]) = hv[i];
         }
+#if VN_ROWS_FLAGS
+        if (tid < RW) stf2[(t + 1) & 1][tid] = (t + 1 < L && row0 + tid < B && st_ld) ? 1 : 0;
+#endif
         __syncthreads();
         VN_DMARK(3);
 #pragma unroll
