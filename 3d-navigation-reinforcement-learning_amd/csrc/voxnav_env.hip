@@ -2466,7 +2466,20 @@ int vn_create(const VnRoomSet *rooms, int32_t n_agents, const VnConfig *cfg, int
         const char *bo = getenv("VOXNAV_BELIEF_OFFSET");
         const size_t off = bo ? (((size_t)atoll(bo)) + 255u) & ~(size_t)255u : 0;
         e->belief_alloc_bytes = belief_bytes + off;
-        VN_ALLOC(e->belief_alloc, e->belief_alloc_bytes);
+        // VOXNAV_BELIEF_CONTIG=1: a physically contiguous allocation
+        // (hipDeviceMallocContiguous; placement study)
+        const char *bc = getenv("VOXNAV_BELIEF_CONTIG");
+        if (bc && bc[0] == '1') {
+            const hipError_t ce = hipExtMallocWithFlags(&e->belief_alloc, e->belief_alloc_bytes, hipDeviceMallocContiguous);
+            if (ce != hipSuccess) {
+                free_env(e);
+                return fail(VN_ERR_OOM, "hipExtMallocWithFlags(%zu, contiguous) failed: %s", e->belief_alloc_bytes,
+                            hipGetErrorString(ce));
+            }
+            e->device_bytes += e->belief_alloc_bytes;
+        } else {
+            VN_ALLOC(e->belief_alloc, e->belief_alloc_bytes);
+        }
         e->d_belief = reinterpret_cast<int8_t *>(e->belief_alloc) + off;
     }
     VN_ALLOC(e->d_err, sizeof(int32_t));

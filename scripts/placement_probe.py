@@ -5,7 +5,7 @@ land in device memory.
 Per trial a ballast tensor of a different size is allocated first (so every
 later allocation moves), then for each variant a fresh env is created with
 the variant's knobs (environment variables vn_create reads:
-VOXNAV_AGENT_PAD, VOXNAV_BELIEF_OFFSET; the round-6 VMM-mapped variant
+VOXNAV_AGENT_PAD, VOXNAV_BELIEF_OFFSET, VOXNAV_BELIEF_CONTIG; the round-6 VMM-mapped variant
 VOXNAV_BELIEF_VMM was removed), reset to the same
 seed `reps` times and timed over the same launch (HIP events on the launch
 stream), so every row is the same work on a different placement.  One JSON
