@@ -147,7 +147,8 @@ def _rows_reference(x, env, start, keep, hs, cs, lstm, l):
 
 @pytest.mark.parametrize("layout", ["auto", "units16", "units32"])
 @pytest.mark.parametrize("L,B,N,p_start", [(24, 512, 600, 0.03), (9, 37, 40, 0.2), (128, 64, 64, 0.01),
-                                           (128, 512, 512, 0.004)])
+                                           (128, 512, 512, 0.004), (1, 1, 4, 0.5), (2, 33, 8, 0.5),
+                                           (5, 289, 300, 1.0)])
 def test_dual_lstm_rows_matches_float64(L, B, N, p_start, layout, monkeypatch):
     """The persistent row-layout LSTM (csrc/voxnav_learn_rows.hip: weights
     resident, in-launch h / partial-dh hand-offs between the unit blocks of a
@@ -155,7 +156,10 @@ def test_dual_lstm_rows_matches_float64(L, B, N, p_start, layout, monkeypatch):
     gradients of both LSTMs, with sequence starts (stored states x keep) at t = 0,
     at random steps and mid-row; full 512-row tiles, a ragged last tile, a
     whole 128-step rollout, and the learner bench's own shape (512 rows x 128
-    steps: every block of the launch resident, 128 hand-offs per direction).
+    steps: every block of the launch resident, 128 hand-offs per direction);
+    edge shapes: one step of one row, two steps of a 33-row batch (one full
+    tile and a 1-row tile), and a batch where every row starts a sequence at
+    every step (no state crosses a step: only the stored states).
     Both layouts, forced: 16 unit blocks of 16 units (VOXNAV_ROWS_V2=1; two
     blocks per CU at 512 rows) and 8 of 32 (VOXNAV_ROWS_V1=1), and the
     default pick per direction."""
